@@ -1,0 +1,19 @@
+"""backuwup_amd -- MI355X (gfx950) dedup front end for backuwup.
+
+FastCDC-v2020 chunking -> BLAKE3 chunk IDs -> seen-chunk index, as hand-written HIP kernels
+behind the C ABI in include/backuwup_gpu.h (libbackuwup_amd.so, built in-tree).  The Python
+modules mirror the reference's call sites:
+
+  backuwup_amd.fastcdc.FastCDC   <- fastcdc::v2020::FastCDC   (dir_packer.rs:254-266)
+  backuwup_amd.blake3.hash       <- blake3::hash              (dir_packer.rs:286)
+  backuwup_amd.packer.BlobIndex  <- packfile::blob_index::BlobIndex (blob_index.rs:44-148)
+  backuwup_amd.packer.process_files <- dir_packer::process_file + add_file_blob
+"""
+from . import _lib
+from .context import BLOB_DTYPE, Context, default_context, make_params
+
+__all__ = ["Context", "default_context", "make_params", "BLOB_DTYPE", "load_library"]
+
+
+def load_library():
+    return _lib.load()

@@ -1,0 +1,98 @@
+"""ctypes binding of libbackuwup_amd.so (the C ABI in include/backuwup_gpu.h).
+
+There is no fallback: if the HIP library is missing or cannot be loaded this raises, and
+every compute call runs on the GPU through the library.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbackuwup_amd.so")
+
+BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -1, -2, -3, -4, -5, -6
+BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+
+class BwChunk(ctypes.Structure):
+    _fields_ = [("hash", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("length", ctypes.c_uint64)]
+
+
+class BwBlob(ctypes.Structure):
+    _fields_ = [("file", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("length", ctypes.c_uint64),
+                ("gear_hash", ctypes.c_uint64), ("digest", ctypes.c_uint8 * 32),
+                ("is_dup", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 7)]
+
+
+class BwParams(ctypes.Structure):
+    _fields_ = [("min_size", ctypes.c_uint32), ("avg_size", ctypes.c_uint32),
+                ("max_size", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("small_file_threshold", ctypes.c_uint64)]
+
+
+# (name, restype, argtypes) for every symbol of include/backuwup_gpu.h
+SIGNATURES = [
+    ("bw_params_default", None, [ctypes.POINTER(BwParams)]),
+    ("bw_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("bw_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+    ("bw_destroy", None, [vp]),
+    ("bw_last_error", ctypes.c_char_p, [vp]),
+    ("bw_set_stream", ctypes.c_int, [vp, vp]),
+    ("bw_get_stream", vp, [vp]),
+    ("bw_fastcdc_chunks", ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.POINTER(BwChunk), ctypes.c_uint64, u64p]),
+    ("bw_blake3_hash", ctypes.c_int, [vp, vp, ctypes.c_uint64, u8p]),
+    ("bw_blake3_hash_many", ctypes.c_int, [vp, vp, ctypes.c_uint64, u64p, u64p, ctypes.c_uint64, u8p]),
+    ("bw_index_reset", ctypes.c_int, [vp, ctypes.c_uint64]),
+    ("bw_index_seed", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+    ("bw_index_check_insert", ctypes.c_int, [vp, vp, ctypes.c_uint64, u8p]),
+    ("bw_index_size", ctypes.c_int, [vp, u64p]),
+    ("bw_process_files", ctypes.c_int, [vp, vp, ctypes.c_uint64, u64p, u64p, ctypes.c_uint64,
+                                        ctypes.POINTER(BwParams), ctypes.POINTER(BwBlob), ctypes.c_uint64,
+                                        u64p]),
+    ("bw_process_files_device", ctypes.c_int, [vp, vp, ctypes.c_uint64, u64p, u64p, ctypes.c_uint64,
+                                               ctypes.POINTER(BwParams)]),
+    ("bw_results", ctypes.c_int, [vp, ctypes.POINTER(BwBlob), ctypes.c_uint64, u64p]),
+    ("bw_batch_device_views", ctypes.c_int, [vp, u64p, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+    ("bw_partition_by_owner", ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, u64p]),
+    ("bw_index_check_insert_device", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),
+    ("bw_scatter_verdicts", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, vp]),
+]
+
+_lib = None
+
+
+def load():
+    """Load the HIP library; raises OSError/RuntimeError when it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libbackuwup_amd.so not built (run __graft_entry__.build() or "
+                           "python backuwup_amd/build.py); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class BwError(RuntimeError):
+    def __init__(self, rc, msg=""):
+        self.rc = rc
+        text = load().bw_strerror(rc).decode()
+        super().__init__("backuwup_amd error %d (%s)%s" % (rc, text, (": " + msg) if msg else ""))
+
+
+def check(rc, ctx=None):
+    if rc != BW_OK:
+        msg = ""
+        if ctx is not None:
+            m = load().bw_last_error(ctx)
+            msg = m.decode() if m else ""
+        raise BwError(rc, msg)

@@ -1,0 +1,184 @@
+"""GPU context (one bw_ctx: a HIP stream, device workspaces and the in-HBM dedup index)."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import BwBlob, BwParams, check
+
+BLOB_DTYPE = np.dtype([("file", "<u8"), ("offset", "<u8"), ("length", "<u8"), ("gear_hash", "<u8"),
+                       ("digest", "u1", (32,)), ("is_dup", "u1"), ("pad", "u1", (7,))])
+assert BLOB_DTYPE.itemsize == ctypes.sizeof(BwBlob) == 72
+
+# backuwup's chunker constants (client/src/defaults.rs:61-68)
+BLOB_MINIMUM_TARGET_SIZE = 256 * 1024
+BLOB_DESIRED_TARGET_SIZE = 1024 * 1024
+BLOB_MAX_UNCOMPRESSED_SIZE = 3 * 1024 * 1024
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(None)
+
+
+def _as_u8(data):
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+def make_params(min_size=BLOB_MINIMUM_TARGET_SIZE, avg_size=BLOB_DESIRED_TARGET_SIZE,
+                max_size=BLOB_MAX_UNCOMPRESSED_SIZE, small_file_threshold=None, flags=0):
+    p = BwParams()
+    p.min_size, p.avg_size, p.max_size, p.flags = min_size, avg_size, max_size, flags
+    p.small_file_threshold = avg_size if small_file_threshold is None else small_file_threshold
+    return p
+
+
+class Context:
+    """Owns one bw_ctx on `device`.  Not thread-safe (like the reference's packer mutex)."""
+
+    def __init__(self, device=0):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        check(self._L.bw_create(device, ctypes.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.bw_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -------------------------------------------------------------- streams
+    def set_stream(self, hip_stream_handle):
+        check(self._L.bw_set_stream(self.h, ctypes.c_void_p(hip_stream_handle)), self.h)
+
+    def stream(self):
+        return self._L.bw_get_stream(self.h)
+
+    # -------------------------------------------------------------- chunk / hash
+    def fastcdc_chunks(self, data, min_size, avg_size, max_size):
+        buf = _as_u8(data)
+        cap = buf.size // max(min_size, 1) + 2
+        out = (_lib.BwChunk * cap)()
+        n = ctypes.c_uint64()
+        check(self._L.bw_fastcdc_chunks(self.h, _ptr(buf), buf.size, min_size, avg_size, max_size, out, cap,
+                                        ctypes.byref(n)), self.h)
+        return [(out[i].hash, out[i].offset, out[i].length) for i in range(n.value)]
+
+    def blake3_many(self, data, offsets, lengths):
+        buf = _as_u8(data)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint64)
+        out = np.zeros((len(off), 32), dtype=np.uint8)
+        if len(off) == 0:
+            return out
+        check(self._L.bw_blake3_hash_many(self.h, _ptr(buf), buf.size, off.ctypes.data_as(_lib.u64p),
+                                          ln.ctypes.data_as(_lib.u64p), len(off),
+                                          out.ctypes.data_as(_lib.u8p)), self.h)
+        return out
+
+    def blake3(self, data):
+        buf = _as_u8(data)
+        out = (ctypes.c_uint8 * 32)()
+        check(self._L.bw_blake3_hash(self.h, _ptr(buf), buf.size, out), self.h)
+        return bytes(out)
+
+    # -------------------------------------------------------------- index
+    def index_reset(self, capacity_hint=0):
+        check(self._L.bw_index_reset(self.h, capacity_hint), self.h)
+
+    def index_seed(self, sorted_digests):
+        d = np.ascontiguousarray(np.asarray(sorted_digests, dtype=np.uint8).reshape(-1, 32))
+        check(self._L.bw_index_seed(self.h, _ptr(d), d.shape[0]), self.h)
+
+    def index_check_insert(self, digests):
+        d = np.ascontiguousarray(np.asarray(digests, dtype=np.uint8).reshape(-1, 32))
+        out = np.zeros(d.shape[0], dtype=np.uint8)
+        if d.shape[0]:
+            check(self._L.bw_index_check_insert(self.h, _ptr(d), d.shape[0], out.ctypes.data_as(_lib.u8p)), self.h)
+        return out
+
+    def index_size(self):
+        n = ctypes.c_uint64()
+        check(self._L.bw_index_size(self.h, ctypes.byref(n)), self.h)
+        return n.value
+
+    # -------------------------------------------------------------- batches
+    def process_files(self, data, file_off, file_len, params=None):
+        buf = _as_u8(data)
+        fo = np.ascontiguousarray(file_off, dtype=np.uint64)
+        fl = np.ascontiguousarray(file_len, dtype=np.uint64)
+        p = params or make_params()
+        cap = int(sum(int(x) // max(p.min_size - 1, 1) + 2 for x in fl)) + 1
+        out = np.zeros(cap, dtype=BLOB_DTYPE)
+        n = ctypes.c_uint64()
+        check(self._L.bw_process_files(self.h, _ptr(buf), buf.size, fo.ctypes.data_as(_lib.u64p),
+                                       fl.ctypes.data_as(_lib.u64p), len(fo), ctypes.byref(p),
+                                       out.ctypes.data_as(ctypes.POINTER(BwBlob)), cap, ctypes.byref(n)), self.h)
+        return out[:n.value]
+
+    def submit_device(self, d_ptr, data_len, file_off, file_len, params=None):
+        """Enqueue a batch whose bytes are already in HBM (d_ptr = device address)."""
+        fo = np.ascontiguousarray(file_off, dtype=np.uint64)
+        fl = np.ascontiguousarray(file_len, dtype=np.uint64)
+        self._keep = (fo, fl)
+        p = params or make_params()
+        check(self._L.bw_process_files_device(self.h, ctypes.c_void_p(d_ptr), data_len,
+                                              fo.ctypes.data_as(_lib.u64p), fl.ctypes.data_as(_lib.u64p),
+                                              len(fo), ctypes.byref(p)), self.h)
+
+    def results(self, cap=None):
+        n = ctypes.c_uint64()
+        if cap is None:
+            rc = self._L.bw_results(self.h, None, 0, ctypes.byref(n))
+            if rc not in (_lib.BW_OK, _lib.BW_ENOSPC):
+                check(rc, self.h)
+            cap = n.value
+        out = np.zeros(max(cap, 1), dtype=BLOB_DTYPE)
+        check(self._L.bw_results(self.h, out.ctypes.data_as(ctypes.POINTER(BwBlob)), cap, ctypes.byref(n)), self.h)
+        return out[:n.value]
+
+    def device_views(self):
+        n = ctypes.c_uint64()
+        d, dup = ctypes.c_void_p(), ctypes.c_void_p()
+        check(self._L.bw_batch_device_views(self.h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(dup)), self.h)
+        return n.value, d.value, dup.value
+
+    # -------------------------------------------------------------- multi-GPU helpers (device pointers)
+    def partition_by_owner(self, d_digests, n, n_owners, d_out, d_perm):
+        counts = np.zeros(n_owners, dtype=np.uint64)
+        check(self._L.bw_partition_by_owner(self.h, ctypes.c_void_p(d_digests), n, n_owners,
+                                            ctypes.c_void_p(d_out), ctypes.c_void_p(d_perm),
+                                            counts.ctypes.data_as(_lib.u64p)), self.h)
+        return counts
+
+    def index_check_insert_device(self, d_digests, n, d_is_dup):
+        check(self._L.bw_index_check_insert_device(self.h, ctypes.c_void_p(d_digests), n,
+                                                   ctypes.c_void_p(d_is_dup)), self.h)
+
+    def scatter_verdicts(self, d_verdict, d_perm, n, d_is_dup):
+        check(self._L.bw_scatter_verdicts(self.h, ctypes.c_void_p(d_verdict), ctypes.c_void_p(d_perm), n,
+                                          ctypes.c_void_p(d_is_dup)), self.h)
+
+
+_default = None
+
+
+def default_context():
+    global _default
+    if _default is None:
+        _default = Context(0)
+    return _default

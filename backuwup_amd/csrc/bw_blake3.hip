@@ -1,0 +1,183 @@
+// bw_blake3.hip -- BLAKE3 chunk IDs on gfx950.
+//
+// Replaces `blake3::hash(data).into()` of add_file_blob (client/src/backup/filesystem/
+// dir_packer.rs:286; crate blake3 1.3.3, Cargo.lock:149-159).  Spec restated in SURVEY.md A.4.
+//
+// A blob of n BLAKE3 leaves (1 KiB each) hashes as: complete binary subtrees over every aligned
+// run of 2^l leaves that fits in n, plus a right spine that merges, from the right, the last
+// complete node of every level l whose bit is set in n; the final merge (or the single node when
+// n is a power of two, or the leaf when n == 1) carries ROOT.
+//
+//   k_b3_groups  one lane per aligned 4-leaf group (4 KiB of input, 64 compressions + <=3
+//                parents, all lanes busy).  Blobs of <= 4 leaves finish here (ROOT in-lane);
+//                otherwise the lane stores the level-2 node, or for a blob's ragged last group
+//                the merged tail of the spine (bits 0..1 of n).
+//   k_b3_tree    one workgroup per blob with n > 4: the remaining levels in LDS + the spine.
+#include "bw_device.h"
+#include "bw_internal.h"
+
+namespace bw {
+
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// Chaining value of one leaf (<= 1024 bytes at global position `ls`), chunk counter `t`.
+// `bend` is the end of the blob: loads never touch bytes at or beyond it except through the
+// byte-exact tail path, so a blob at the very end of the caller's buffer is safe.
+__device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64_t ls, uint32_t ll, uint64_t bend,
+                                        uint64_t t, uint32_t root, uint32_t cv[8]) {
+    b3_iv(cv);
+    const uint32_t nblk = ll == 0 ? 1 : (ll + 63) / 64;
+    const uint8_t* base = data + ls;
+    const uint32_t sh = (uint32_t)((uintptr_t)base & 3);
+    const uint32_t* wb = (const uint32_t*)(base - sh);
+    for (uint32_t blk = 0; blk < nblk; blk++) {
+        uint32_t m[16];
+        const uint32_t left = ll - blk * 64;
+        const uint32_t blen = ll == 0 ? 0 : (left < 64 ? left : 64);
+        if (ls + blk * 64 + 68 <= bend) {
+            const u32x4_a4* q = (const u32x4_a4*)(wb + blk * 16);
+            const u32x4_a4 a = q[0], b = q[1], c = q[2], d = q[3];
+            const uint32_t e = wb[blk * 16 + 16];
+            const uint32_t w[17] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e};
+#pragma unroll
+            for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+        } else {
+            const uint8_t* p = base + blk * 64;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if ((uint32_t)(4 * i + j) < blen) v |= (uint32_t)p[4 * i + j] << (8 * j);
+                m[i] = v;
+            }
+        }
+        uint32_t flags = 0;
+        if (blk == 0) flags |= B3_CHUNK_START;
+        if (blk == nblk - 1) flags |= B3_CHUNK_END | root;
+        b3_compress(cv, m, blen, t, flags);
+    }
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* out, const uint32_t cv[8]) {
+    uint32_t* o = (uint32_t*)out;
+#pragma unroll
+    for (int i = 0; i < 8; i++) o[i] = cv[i];  // little-endian words = the digest bytes
+}
+
+__global__ __launch_bounds__(256) void k_b3_groups(const uint8_t* __restrict__ data, const uint64_t* ctr,
+                                                   BlobArrays b, uint32_t* __restrict__ cv_buf,
+                                                   uint8_t* __restrict__ digests) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ctr[C_NGROUPS]) return;
+    const uint64_t nb = ctr[C_NBLOBS];
+    uint64_t lo = 0, hi = nb;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (b.goff[mid] <= g) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint64_t blob = lo - 1;
+    const uint64_t start = b.start[blob], len = b.len[blob], gi = g - b.goff[blob];
+    const uint64_t bend = start + len;
+    const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
+    const uint64_t first = gi * 4;
+    const uint32_t k = (uint32_t)(n - first < 4 ? n - first : 4);
+    uint32_t acc[8], sv[8], cv[8];
+    for (uint32_t t = 0; t < k; t++) {
+        const uint64_t li = first + t, ls = start + li * B3_LEAF_BYTES;
+        const uint64_t rest = len - li * B3_LEAF_BYTES;
+        const uint32_t ll = len == 0 ? 0 : (uint32_t)(rest < B3_LEAF_BYTES ? rest : B3_LEAF_BYTES);
+        b3_leaf(data, ls, ll, bend, li, n == 1 ? B3_ROOT : 0, cv);
+        if (t == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[i] = cv[i];
+        } else if (t == 1) {
+            b3_parent(acc, cv, n == 2 ? B3_ROOT : 0, acc);
+        } else if (t == 2) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) sv[i] = cv[i];
+        } else {
+            b3_parent(sv, cv, 0, sv);
+            b3_parent(acc, sv, n == 4 ? B3_ROOT : 0, acc);
+        }
+    }
+    if (k == 3) b3_parent(acc, sv, n == 3 ? B3_ROOT : 0, acc);
+    if (n <= 4) store_digest(digests + blob * 32, acc);
+    else {
+        uint32_t* o = cv_buf + g * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i++) o[i] = acc[i];
+    }
+}
+
+// Upper levels of one blob (n > 4 leaves).  Level-2 nodes come from k_b3_groups; level l+1 is
+// built in LDS from level l; thread 0 folds the right spine as each level becomes available.
+__global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays b,
+                                                 const uint32_t* __restrict__ cv_buf,
+                                                 uint8_t* __restrict__ digests) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t nodes[];  // [cap][8]
+    const uint64_t blob = blockIdx.x;
+    if (blob >= ctr[C_NBLOBS]) return;
+    const uint64_t len = b.len[blob];
+    const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
+    if (n <= 4) return;
+    const uint32_t* lvl2 = cv_buf + b.goff[blob] * 8;
+    uint64_t cnt = n / 4;
+    uint32_t acc[8];
+    bool have = false;
+    if (threadIdx.x == 0 && (n & 3)) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc[i] = lvl2[cnt * 8 + i];
+        have = true;
+    }
+    const uint32_t* src = lvl2;
+    for (int l = 2;; l++) {
+        if (threadIdx.x == 0 && ((n >> l) & 1)) {
+            uint32_t T[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) T[i] = src[(cnt - 1) * 8 + i];
+            if (!have) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = T[i];
+                have = true;
+            } else {
+                b3_parent(T, acc, (n >> (l + 1)) == 0 ? B3_ROOT : 0, acc);
+            }
+        }
+        const uint64_t next = cnt / 2;
+        if (next == 0) break;
+        const uint32_t root = (n == (1ull << (l + 1))) ? B3_ROOT : 0;
+        for (uint64_t c0 = 0; c0 < next; c0 += blockDim.x) {
+            const uint64_t i = c0 + threadIdx.x;
+            uint32_t L[8], R[8], P[8];
+            if (i < next) {
+#pragma unroll
+                for (int w = 0; w < 8; w++) { L[w] = src[(2 * i) * 8 + w]; R[w] = src[(2 * i + 1) * 8 + w]; }
+            }
+            __syncthreads();
+            if (i < next) {
+                b3_parent(L, R, root, P);
+#pragma unroll
+                for (int w = 0; w < 8; w++) nodes[i * 8 + w] = P[w];
+            }
+            __syncthreads();
+        }
+        src = nodes;
+        cnt = next;
+    }
+    if (threadIdx.x == 0) store_digest(digests + blob * 32, acc);
+}
+
+void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
+                   uint64_t max_groups, uint32_t* cv_buf, uint8_t* digests, int max_leaves) {
+    if (!max_blobs) return;
+    hipLaunchKernelGGL(k_b3_groups, dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data, ctr, b,
+                       cv_buf, digests);
+    if (max_leaves > 4) {
+        const size_t lds = (size_t)((max_leaves / 4) / 2 + 1) * 32;
+        hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)max_blobs), dim3(256), lds, st, ctr, b, cv_buf, digests);
+    }
+}
+
+}  // namespace bw

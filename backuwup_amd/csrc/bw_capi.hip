@@ -1,0 +1,650 @@
+// bw_capi.hip -- the C ABI (include/backuwup_gpu.h) and the host-side batch orchestration.
+//
+// The host side only turns file sizes into small metadata tables (segments, canonical units);
+// every byte of file data is read on the GPU.  A batch is enqueued on one HIP stream with no
+// host synchronisation until results are requested, so a caller can keep batches in flight.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/backuwup_gpu.h"
+#include "bw_internal.h"
+#include "bw_tables.inc"
+
+using namespace bw;
+
+static const uint64_t H_MASKS[26] = BW_MASKS_INIT;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+}  // namespace
+
+struct bw_ctx {
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    std::string err;
+    hipEvent_t meta_done = nullptr;  // staging buffer reusable once this fired
+    bool meta_pending = false;
+
+    // per-batch device buffers
+    DevBuf tile_count, tile_slots, tile_off, cand, ovf, ctr;
+    DevBuf segs, cfiles, units, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
+    DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
+    DevBuf cv, digests, is_dup, packed, fstart, data, scratch;
+    PinBuf stage;
+
+    // persistent dedup index
+    DevBuf table, log, dstate;
+    uint64_t table_cap = 0, log_cap = 0, log_hi = 0;  // log_hi: host upper bound of log length
+
+    // last batch (kept so a batch whose candidate array overflowed can be re-run exactly)
+    uint64_t cand_override = 0;
+    const uint8_t* last_data = nullptr;
+    uint64_t last_len = 0;
+    std::vector<uint64_t> last_off, last_flen;
+    bw_params last_prm{};
+    bool pending = false;
+    uint64_t last_max_blobs = 0;
+    uint64_t last_nfiles = 0;
+    bool last_dedup = false;
+};
+
+// ------------------------------------------------------------------ helpers
+
+#define HIPCHK(ctx, expr)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+            return BW_EHIP;                                                                 \
+        }                                                                                   \
+    } while (0)
+
+static int ensure(bw_ctx* c, DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return BW_OK;
+    if (b.p) {
+        hipStreamSynchronize(c->stream);
+        hipFree(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    size_t want = bytes + bytes / 4 + 256;
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        c->err = "hipMalloc(" + std::to_string(want) + ") failed";
+        b.p = nullptr;
+        return BW_ENOMEM;
+    }
+    b.cap = want;
+    return BW_OK;
+}
+
+static int ensure_pinned(bw_ctx* c, PinBuf& b, size_t bytes) {
+    if (c->meta_pending) {
+        hipEventSynchronize(c->meta_done);
+        c->meta_pending = false;
+    }
+    if (b.cap >= bytes) return BW_OK;
+    if (b.p) hipHostFree(b.p);
+    size_t want = bytes + bytes / 4 + 4096;
+    if (hipHostMalloc(&b.p, want, hipHostMallocDefault) != hipSuccess) {
+        c->err = "hipHostMalloc failed";
+        b.p = nullptr;
+        b.cap = 0;
+        return BW_ENOMEM;
+    }
+    b.cap = want;
+    return BW_OK;
+}
+
+template <typename T>
+static T* P(DevBuf& b) { return (T*)b.p; }
+
+static int make_masks(uint32_t mn, uint32_t av, uint32_t mx, Masks* mk) {
+    // FastCDC::with_level asserts (fastcdc 3.0.3 v2020) -> BW_EINVAL instead of a panic.
+    if (mn < BW_MINIMUM_MIN || mn > BW_MINIMUM_MAX) return BW_EINVAL;
+    if (av < BW_AVERAGE_MIN || av > BW_AVERAGE_MAX) return BW_EINVAL;
+    if (mx < BW_MAXIMUM_MIN || mx > BW_MAXIMUM_MAX) return BW_EINVAL;
+    const uint32_t bits = (uint32_t)lround(log2((double)av));  // logarithm2(): round(log2(avg))
+    mk->min = mn;
+    mk->avg = av;
+    mk->max = mx;
+    mk->s0 = 2 * (mn / 2);
+    mk->mask_s = H_MASKS[bits + 1];  // Normalization::Level1
+    mk->mask_l = H_MASKS[bits - 1];
+    mk->mask_pre = mk->mask_s & mk->mask_l;
+    return BW_OK;
+}
+
+static uint64_t seg_len_for(const Masks& mk) {
+    // Segments are a multiple of max_size so that chains through data without candidates
+    // (e.g. zeros: every chunk is exactly max) stay phase-aligned and merge immediately; the
+    // multiple keeps a segment's own cuts within CHAIN_CAP / 2.
+    uint64_t k = (uint64_t)(CHAIN_CAP / 2) * mk.s0 / mk.max;
+    if (k < 1) k = 1;
+    if (k > 8) k = 8;
+    return k * mk.max;
+}
+
+// ------------------------------------------------------------------ C ABI: basics
+
+extern "C" void bw_params_default(bw_params* p) {
+    p->min_size = BW_BLOB_MINIMUM_TARGET_SIZE;
+    p->avg_size = BW_BLOB_DESIRED_TARGET_SIZE;
+    p->max_size = BW_BLOB_MAX_UNCOMPRESSED_SIZE;
+    p->flags = 0;
+    p->small_file_threshold = BW_BLOB_DESIRED_TARGET_SIZE;  // dir_packer.rs:246
+}
+
+extern "C" const char* bw_strerror(int rc) {
+    switch (rc) {
+        case BW_OK: return "ok";
+        case BW_EINVAL: return "invalid argument (fastcdc parameter range or pointer)";
+        case BW_ENOSPC: return "output capacity too small";
+        case BW_EHIP: return "HIP runtime error";
+        case BW_ENOMEM: return "out of memory";
+        case BW_ECOLLISION: return "64-bit digest key collision in the index";
+        case BW_ESTATE: return "invalid call order";
+        default: return "unknown error";
+    }
+}
+
+extern "C" int bw_create(int device, bw_ctx** out) {
+    if (!out) return BW_EINVAL;
+    *out = nullptr;
+    bw_ctx* c = new bw_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->meta_done, hipEventDisableTiming) != hipSuccess) {
+        delete c;
+        return BW_EHIP;
+    }
+    c->stream = c->own;
+    if (ensure(c, c->dstate, D_COUNT * 8) || ensure(c, c->ctr, C_COUNT * 8)) {
+        delete c;
+        return BW_ENOMEM;
+    }
+    hipMemsetAsync(c->dstate.p, 0, D_COUNT * 8, c->stream);
+    hipMemsetAsync(c->ctr.p, 0, C_COUNT * 8, c->stream);
+    *out = c;
+    return BW_OK;
+}
+
+extern "C" void bw_destroy(bw_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->cand, &c->ovf, &c->ctr, &c->segs,
+                     &c->cfiles, &c->units, &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
+                     &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
+                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->digests,
+                     &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->table, &c->log, &c->dstate};
+    for (DevBuf* b : all)
+        if (b->p) hipFree(b->p);
+    if (c->stage.p) hipHostFree(c->stage.p);
+    if (c->meta_done) hipEventDestroy(c->meta_done);
+    if (c->own) hipStreamDestroy(c->own);
+    delete c;
+}
+
+extern "C" const char* bw_last_error(const bw_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int bw_set_stream(bw_ctx* c, void* s) {
+    if (!c) return BW_EINVAL;
+    hipStreamSynchronize(c->stream);
+    c->stream = s ? (hipStream_t)s : c->own;
+    return BW_OK;
+}
+
+extern "C" void* bw_get_stream(bw_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// ------------------------------------------------------------------ dedup index
+
+static int index_capacity(bw_ctx* c, uint64_t incoming) {
+    const uint64_t need_log = c->log_hi + incoming;
+    if (need_log > c->log_cap) {
+        uint64_t cap = c->log_cap ? c->log_cap : 1 << 16;
+        while (cap < need_log) cap *= 2;
+        DevBuf nb;
+        if (hipMalloc(&nb.p, cap * 32) != hipSuccess) return BW_ENOMEM;
+        nb.cap = cap * 32;
+        if (c->log.p) {
+            hipMemcpyAsync(nb.p, c->log.p, c->log_cap * 32, hipMemcpyDeviceToDevice, c->stream);
+            hipStreamSynchronize(c->stream);
+            hipFree(c->log.p);
+        }
+        c->log = nb;
+        c->log_cap = cap;
+    }
+    // keep the table at most half full (upper bound: every logged digest distinct)
+    if (need_log * 2 > c->table_cap) {
+        uint64_t cap = c->table_cap ? c->table_cap : 1 << 16;
+        while (cap < need_log * 2) cap *= 2;
+        if (c->table.p) {
+            hipStreamSynchronize(c->stream);
+            hipFree(c->table.p);
+            c->table.p = nullptr;
+        }
+        if (hipMalloc(&c->table.p, cap * 16) != hipSuccess) return BW_ENOMEM;
+        c->table.cap = cap * 16;
+        const uint64_t old = c->table_cap;
+        c->table_cap = cap;
+        launch_table_clear(c->stream, P<uint64_t>(c->table), cap);
+        if (old) launch_rehash(c->stream, P<uint64_t>(c->table), cap, P<uint8_t>(c->log), P<uint64_t>(c->dstate),
+                               c->log_hi);
+    }
+    return BW_OK;
+}
+
+extern "C" int bw_index_reset(bw_ctx* c, uint64_t hint) {
+    if (!c) return BW_EINVAL;
+    hipSetDevice(c->device);
+    c->log_hi = 0;
+    hipMemsetAsync(c->dstate.p, 0, D_COUNT * 8, c->stream);
+    if (int rc = index_capacity(c, hint ? hint : 1024)) return rc;
+    launch_table_clear(c->stream, P<uint64_t>(c->table), c->table_cap);
+    HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
+                        uint8_t* d_is_dup) {
+    if (!c->table_cap)
+        if (int rc = bw_index_reset(c, 0)) return rc;
+    if (int rc = index_capacity(c, max_n)) return rc;
+    launch_dedup(c->stream, P<uint64_t>(c->table), c->table_cap, P<uint8_t>(c->log), P<uint64_t>(c->dstate),
+                 d_digests, n_dev, n_host, max_n, d_is_dup);
+    c->log_hi += max_n;
+    HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+static int check_collision(bw_ctx* c) {
+    uint64_t st[D_COUNT];
+    HIPCHK(c, hipMemcpyAsync(st, c->dstate.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->log_hi = st[D_LOGLEN];  // tighten the host bound
+    if (st[D_COLLIDE]) {
+        c->err = "64-bit key collision between distinct digests";
+        return BW_ECOLLISION;
+    }
+    return BW_OK;
+}
+
+extern "C" int bw_index_seed(bw_ctx* c, const uint8_t* sorted, uint64_t n) {
+    if (!c || (n && !sorted)) return BW_EINVAL;
+    if (!n) return BW_OK;
+    hipSetDevice(c->device);
+    if (int rc = ensure(c, c->scratch, n * 32)) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->scratch.p, sorted, n * 32, hipMemcpyHostToDevice, c->stream));
+    if (int rc = dedup_device(c, P<uint8_t>(c->scratch), nullptr, n, n, nullptr)) return rc;
+    return check_collision(c);
+}
+
+extern "C" int bw_index_check_insert(bw_ctx* c, const uint8_t* digests, uint64_t n, uint8_t* is_dup) {
+    if (!c || (n && (!digests || !is_dup))) return BW_EINVAL;
+    if (!n) return BW_OK;
+    hipSetDevice(c->device);
+    if (int rc = ensure(c, c->scratch, n * 33)) return rc;
+    uint8_t* dd = P<uint8_t>(c->scratch);
+    HIPCHK(c, hipMemcpyAsync(dd, digests, n * 32, hipMemcpyHostToDevice, c->stream));
+    if (int rc = dedup_device(c, dd, nullptr, n, n, dd + n * 32)) return rc;
+    HIPCHK(c, hipMemcpyAsync(is_dup, dd + n * 32, n, hipMemcpyDeviceToHost, c->stream));
+    return check_collision(c);
+}
+
+extern "C" int bw_index_check_insert_device(bw_ctx* c, const uint8_t* d_digests, uint64_t n, uint8_t* d_is_dup) {
+    if (!c || (n && (!d_digests || !d_is_dup))) return BW_EINVAL;
+    if (!n) return BW_OK;
+    hipSetDevice(c->device);
+    return dedup_device(c, d_digests, nullptr, n, n, d_is_dup);
+}
+
+extern "C" int bw_index_size(bw_ctx* c, uint64_t* n) {
+    if (!c || !n) return BW_EINVAL;
+    uint64_t st[D_COUNT];
+    HIPCHK(c, hipMemcpyAsync(st, c->dstate.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *n = st[D_NUNIQUE];
+    return BW_OK;
+}
+
+// ------------------------------------------------------------------ the batch pipeline
+
+static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff, const uint64_t* flen,
+                  uint64_t nf, const bw_params* prm) {
+    Masks mk;
+    if (int rc = make_masks(prm->min_size, prm->avg_size, prm->max_size, &mk)) {
+        c->err = "fastcdc parameters out of range";
+        return rc;
+    }
+    if (nf && (!foff || !flen)) return BW_EINVAL;
+    if (data_len && !d_data) return BW_EINVAL;
+    if (((uintptr_t)d_data & 15) != 0) {
+        c->err = "device data pointer must be 16-byte aligned";
+        return BW_EINVAL;
+    }
+    for (uint64_t f = 0; f < nf; f++)
+        if (foff[f] > data_len || flen[f] > data_len - foff[f]) {
+            c->err = "file " + std::to_string(f) + " lies outside the data buffer";
+            return BW_EINVAL;
+        }
+    hipSetDevice(c->device);
+    const bool force_serial = (prm->flags & BW_F_SERIAL_RESOLVE) != 0;
+    const bool do_hash = !(prm->flags & BW_F_NO_HASH);
+    const bool do_dedup = do_hash && !(prm->flags & BW_F_NO_DEDUP);
+
+    // ---- host metadata: CDC files, segments, canonical units
+    const uint64_t L = seg_len_for(mk);
+    std::vector<SegDesc> segs;
+    std::vector<CFileDesc> cfs;
+    std::vector<UnitDesc> units;
+    units.reserve(nf);
+    uint64_t max_blobs = 0, fb_total = 0, max_blob_len = mk.max, total_len = 0;
+    for (uint64_t f = 0; f < nf; f++) {
+        total_len += flen[f];
+        if (flen[f] > prm->small_file_threshold && flen[f] > 0) {
+            CFileDesc cf;
+            cf.start = foff[f];
+            cf.end = foff[f] + flen[f];
+            cf.fb_off = fb_total;
+            cf.first_seg = (uint32_t)segs.size();
+            const uint64_t ns = (flen[f] + L - 1) / L;
+            cf.nseg = (uint32_t)ns;
+            for (uint64_t j = 0; j < ns; j++) {
+                SegDesc sd;
+                sd.start = cf.start + j * L;
+                sd.end = std::min(cf.start + (j + 1) * L, cf.end);
+                sd.file_end = cf.end;
+                sd.cfile = (uint32_t)cfs.size();
+                sd.last = j + 1 == ns;
+                UnitDesc u;
+                u.start = 0;
+                u.len = 0;
+                u.file = (uint32_t)f;
+                u.kind = 1;
+                u.seg = (uint32_t)segs.size();
+                u.cfile = sd.cfile;
+                units.push_back(u);
+                segs.push_back(sd);
+            }
+            const uint64_t nb = flen[f] / mk.s0 + 2;
+            fb_total += nb;
+            max_blobs += nb;
+            cfs.push_back(cf);
+        } else {
+            UnitDesc u;
+            u.start = foff[f];
+            u.len = flen[f];
+            u.file = (uint32_t)f;
+            u.kind = 0;
+            u.seg = 0;
+            u.cfile = 0;
+            units.push_back(u);
+            max_blobs += 1;
+            max_blob_len = std::max<uint64_t>(max_blob_len, flen[f]);
+        }
+    }
+    const uint64_t nseg = segs.size(), ncf = cfs.size(), nunits = units.size();
+    const uint64_t max_groups = total_len / 4096 + max_blobs + 1;
+    const int max_leaves = (int)std::min<uint64_t>((max_blob_len + 1023) / 1024, 1u << 30);
+    const uint64_t n_tiles = ncf ? (data_len + SCAN_TILE - 1) / SCAN_TILE : 0;
+
+    // ---- device buffers
+    int rc = 0;
+    rc |= ensure(c, c->tile_count, n_tiles * 4);
+    rc |= ensure(c, c->tile_slots, n_tiles * SCAN_CAP * 8);
+    rc |= ensure(c, c->tile_off, (n_tiles + 1) * 8);
+    rc |= ensure(c, c->ovf, n_tiles * 4);
+    rc |= ensure(c, c->segs, nseg * sizeof(SegDesc));
+    rc |= ensure(c, c->cfiles, ncf * sizeof(CFileDesc));
+    rc |= ensure(c, c->units, nunits * sizeof(UnitDesc));
+    rc |= ensure(c, c->chains, nseg * CHAIN_CAP * 8);
+    rc |= ensure(c, c->chain_n, nseg * 4);
+    rc |= ensure(c, c->chain_cptr, nseg * 8);
+    rc |= ensure(c, c->merge, nseg * 8);
+    rc |= ensure(c, c->seg_M, nseg * 8);
+    rc |= ensure(c, c->seg_cnt, nseg * 4);
+    rc |= ensure(c, c->cf_invalid, ncf * 4);
+    rc |= ensure(c, c->fb_starts, fb_total * 8);
+    rc |= ensure(c, c->fb_count, ncf * 8);
+    rc |= ensure(c, c->b_start, max_blobs * 8);
+    rc |= ensure(c, c->b_len, max_blobs * 8);
+    rc |= ensure(c, c->b_goff, max_blobs * 8);
+    rc |= ensure(c, c->b_file, max_blobs * 4);
+    rc |= ensure(c, c->b_kind, max_blobs * 4);
+    rc |= ensure(c, c->b_fend, max_blobs * 8);
+    rc |= ensure(c, c->b_ghash, max_blobs * 8);
+    rc |= ensure(c, c->cv, max_groups * 32);
+    rc |= ensure(c, c->digests, max_blobs * 32);
+    rc |= ensure(c, c->is_dup, max_blobs);
+    rc |= ensure(c, c->packed, max_blobs * sizeof(bw_blob));
+    rc |= ensure(c, c->fstart, nf * 8);
+    if (rc) return BW_ENOMEM;
+    // candidate array: 4x the expected count (2^-popcount(mask) per byte) plus slack; a batch
+    // that finds more is re-run by bw_results with the exact count (pathological inputs only)
+    uint64_t cand_cap = 16;
+    if (ncf) {
+        const int bits = __builtin_popcountll(mk.mask_pre);
+        cand_cap = 4 * (data_len >> bits) + 2 * n_tiles + 4096;
+        cand_cap = std::max(cand_cap, c->cand_override);
+    }
+    if (int r2 = ensure(c, c->cand, cand_cap * 8)) return r2;
+
+    // ---- metadata upload through pinned staging
+    const size_t meta_bytes = nseg * sizeof(SegDesc) + ncf * sizeof(CFileDesc) + nunits * sizeof(UnitDesc) + nf * 8;
+    if (int r3 = ensure_pinned(c, c->stage, meta_bytes + 64)) return r3;
+    uint8_t* sp = (uint8_t*)c->stage.p;
+    size_t o = 0;
+    auto up = [&](DevBuf& dst, const void* src, size_t bytes) -> hipError_t {
+        if (!bytes) return hipSuccess;
+        memcpy(sp + o, src, bytes);
+        hipError_t e = hipMemcpyAsync(dst.p, sp + o, bytes, hipMemcpyHostToDevice, c->stream);
+        o += bytes;
+        return e;
+    };
+    HIPCHK(c, up(c->segs, segs.data(), nseg * sizeof(SegDesc)));
+    HIPCHK(c, up(c->cfiles, cfs.data(), ncf * sizeof(CFileDesc)));
+    HIPCHK(c, up(c->units, units.data(), nunits * sizeof(UnitDesc)));
+    HIPCHK(c, up(c->fstart, foff, nf * 8));
+    hipEventRecord(c->meta_done, c->stream);
+    c->meta_pending = true;
+    HIPCHK(c, hipMemsetAsync(c->ctr.p, 0, C_COUNT * 8, c->stream));
+
+    BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
+                 P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash)};
+    uint64_t* ctr = P<uint64_t>(c->ctr);
+    hipStream_t st = c->stream;
+
+    // ---- chunking
+    if (ncf) {
+        launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots));
+        launch_compact(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
+                       P<uint64_t>(c->tile_off), P<uint64_t>(c->cand), cand_cap, P<uint32_t>(c->ovf), ctr);
+        launch_chains(st, d_data, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs), nseg,
+                      P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->chain_cptr),
+                      P<uint64_t>(c->merge), force_serial);
+        launch_resolve(st, d_data, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs), nseg,
+                       P<CFileDesc>(c->cfiles), ncf, P<uint64_t>(c->chains), P<uint32_t>(c->chain_n),
+                       P<uint64_t>(c->merge), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
+                       P<uint32_t>(c->cf_invalid), P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), force_serial);
+    }
+    launch_assemble(st, ctr, P<UnitDesc>(c->units), nunits, P<SegDesc>(c->segs), P<CFileDesc>(c->cfiles),
+                    P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
+                    P<uint32_t>(c->cf_invalid), P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), b, max_blobs);
+    if (ncf) launch_cut_hash(st, d_data, mk, ctr, b, max_blobs);
+    else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, st));
+
+    // ---- hashing + dedup
+    if (do_hash) {
+        launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint8_t>(c->digests),
+                      max_leaves);
+    } else {
+        HIPCHK(c, hipMemsetAsync(c->digests.p, 0, max_blobs * 32, st));
+    }
+    if (do_dedup) {
+        if (int r4 = dedup_device(c, P<uint8_t>(c->digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(c->is_dup)))
+            return r4;
+    }
+    launch_pack(st, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(c->digests), do_dedup ? P<uint8_t>(c->is_dup) : nullptr,
+                P<uint8_t>(c->packed), max_blobs);
+    HIPCHK(c, hipGetLastError());
+    c->pending = true;
+    c->last_data = d_data;
+    c->last_len = data_len;
+    c->last_off.assign(foff, foff + nf);
+    c->last_flen.assign(flen, flen + nf);
+    c->last_prm = *prm;
+    c->last_max_blobs = max_blobs;
+    c->last_nfiles = nf;
+    c->last_dedup = do_dedup;
+    return BW_OK;
+}
+
+extern "C" int bw_process_files_device(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
+                                       const uint64_t* flen, uint64_t nf, const bw_params* prm) {
+    if (!c) return BW_EINVAL;
+    bw_params def;
+    if (!prm) {
+        bw_params_default(&def);
+        prm = &def;
+    }
+    return submit(c, d_data, data_len, foff, flen, nf, prm);
+}
+
+extern "C" int bw_results(bw_ctx* c, bw_blob* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return BW_EINVAL;
+    if (!c->pending) return BW_ESTATE;
+    hipSetDevice(c->device);
+    uint64_t ctr[C_COUNT];
+    HIPCHK(c, hipMemcpyAsync(ctr, c->ctr.p, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ctr[C_CANDTOTAL] > ctr[C_NCAND]) {
+        // candidate array overflowed: the chunk lists are incomplete -> re-run with exact room.
+        // (k_assemble handed 0 blobs to the index, so the re-run sees the same index.)
+        c->cand_override = ctr[C_CANDTOTAL] + 1024;
+        std::vector<uint64_t> fo = c->last_off, fl = c->last_flen;
+        if (int rc = submit(c, c->last_data, c->last_len, fo.data(), fl.data(), fo.size(), &c->last_prm)) return rc;
+        return bw_results(c, out, cap, n_out);
+    }
+    *n_out = ctr[C_NBLOBS];
+    if (c->last_dedup)
+        if (int rc = check_collision(c)) return rc;
+    if (ctr[C_NBLOBS] > cap) return BW_ENOSPC;
+    if (ctr[C_NBLOBS] && out)
+        HIPCHK(c, hipMemcpy(out, c->packed.p, ctr[C_NBLOBS] * sizeof(bw_blob), hipMemcpyDeviceToHost));
+    return BW_OK;
+}
+
+extern "C" int bw_batch_device_views(bw_ctx* c, uint64_t* n_blobs, const uint8_t** d_digests, uint8_t** d_is_dup) {
+    if (!c) return BW_EINVAL;
+    if (!c->pending) return BW_ESTATE;
+    uint64_t n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, (uint64_t*)c->ctr.p + C_NBLOBS, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (n_blobs) *n_blobs = n;
+    if (d_digests) *d_digests = P<uint8_t>(c->digests);
+    if (d_is_dup) *d_is_dup = P<uint8_t>(c->is_dup);
+    return BW_OK;
+}
+
+static int upload_data(bw_ctx* c, const uint8_t* data, uint64_t len) {
+    if (int rc = ensure(c, c->data, len + 64)) return rc;
+    if (len) HIPCHK(c, hipMemcpyAsync(c->data.p, data, len, hipMemcpyHostToDevice, c->stream));
+    return BW_OK;
+}
+
+extern "C" int bw_process_files(bw_ctx* c, const uint8_t* data, uint64_t data_len, const uint64_t* foff,
+                                const uint64_t* flen, uint64_t nf, const bw_params* prm, bw_blob* out, uint64_t cap,
+                                uint64_t* n_out) {
+    if (!c || !n_out || (data_len && !data)) return BW_EINVAL;
+    hipSetDevice(c->device);
+    if (int rc = upload_data(c, data, data_len)) return rc;
+    if (int rc = bw_process_files_device(c, P<uint8_t>(c->data), data_len, foff, flen, nf, prm)) return rc;
+    return bw_results(c, out, cap, n_out);
+}
+
+extern "C" int bw_fastcdc_chunks(bw_ctx* c, const uint8_t* src, uint64_t len, uint32_t mn, uint32_t av, uint32_t mx,
+                                 bw_chunk* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out || (len && !src)) return BW_EINVAL;
+    Masks mk;
+    if (int rc = make_masks(mn, av, mx, &mk)) return rc;
+    *n_out = 0;
+    if (len == 0) return BW_OK;  // the iterator yields nothing for an empty source
+    bw_params p;
+    p.min_size = mn;
+    p.avg_size = av;
+    p.max_size = mx;
+    p.flags = BW_F_NO_HASH;
+    p.small_file_threshold = 0;
+    const uint64_t off = 0;
+    std::vector<bw_blob> tmp(len / mk.s0 + 2);
+    uint64_t n = 0;
+    if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
+    *n_out = n;
+    if (n > cap) return BW_ENOSPC;
+    for (uint64_t i = 0; i < n; i++) {
+        out[i].hash = tmp[i].gear_hash;
+        out[i].offset = tmp[i].offset;
+        out[i].length = tmp[i].length;
+    }
+    return BW_OK;
+}
+
+extern "C" int bw_blake3_hash_many(bw_ctx* c, const uint8_t* data, uint64_t data_len, const uint64_t* offsets,
+                                   const uint64_t* lengths, uint64_t n, uint8_t* out) {
+    if (!c || (n && (!offsets || !lengths || !out))) return BW_EINVAL;
+    if (!n) return BW_OK;
+    bw_params p;
+    bw_params_default(&p);
+    p.flags = BW_F_NO_DEDUP;
+    p.small_file_threshold = ~0ull;  // every message is one whole blob
+    std::vector<bw_blob> tmp(n);
+    uint64_t got = 0;
+    if (int rc = bw_process_files(c, data, data_len, offsets, lengths, n, &p, tmp.data(), n, &got)) return rc;
+    if (got != n) return BW_EHIP;
+    for (uint64_t i = 0; i < n; i++) memcpy(out + 32 * i, tmp[i].digest, 32);
+    return BW_OK;
+}
+
+extern "C" int bw_blake3_hash(bw_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    const uint64_t off = 0;
+    static const uint8_t empty[16] = {0};
+    return bw_blake3_hash_many(c, len ? data : empty, len, &off, &len, 1, out);
+}
+
+// ------------------------------------------------------------------ multi-GPU helpers
+
+extern "C" int bw_partition_by_owner(bw_ctx* c, const uint8_t* d_digests, uint64_t n, uint32_t n_owners,
+                                     uint8_t* d_out, uint64_t* d_perm, uint64_t* h_counts) {
+    if (!c || !h_counts || n_owners == 0 || n_owners > 256 || (n_owners & (n_owners - 1))) return BW_EINVAL;
+    hipSetDevice(c->device);
+    if (int rc = ensure(c, c->scratch, 256 * 8)) return rc;
+    launch_partition(c->stream, d_digests, n, n_owners, d_out, d_perm, P<uint64_t>(c->scratch));
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(h_counts, c->scratch.p, n_owners * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BW_OK;
+}
+
+extern "C" int bw_scatter_verdicts(bw_ctx* c, const uint8_t* d_verdict, const uint64_t* d_perm, uint64_t n,
+                                   uint8_t* d_is_dup) {
+    if (!c) return BW_EINVAL;
+    hipSetDevice(c->device);
+    launch_scatter(c->stream, d_verdict, d_perm, n, d_is_dup);
+    HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}

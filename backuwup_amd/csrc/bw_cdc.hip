@@ -1,0 +1,677 @@
+// bw_cdc.hip -- FastCDC v2020 content-defined chunking on gfx950.
+//
+// Replaces `FastCDC::new(&mmap, 262144, 1048576, 3145728)` + its iterator as called by
+// process_file (client/src/backup/filesystem/dir_packer.rs:254-266); crate fastcdc 3.0.3
+// (Cargo.lock:557-560), semantics restated in SURVEY.md A.1 and oracle/bw_oracle.c.
+//
+// The crate's cut() is a serial two-bytes-per-step loop; the equivalent per-byte form is
+//   h_p = (h_{p-1} << 1) + GEAR[src[p]],  hash reset to 0 at chunk_start + 2*(min/2),
+// and position p cuts iff (h_p & mask) == 0 (mask_s before `center`, mask_l after).  Because
+// every mask bit is <= 47, (h_p & mask) depends only on src[p-47 ..= p]; so the candidate test
+// can run at EVERY byte of the stream in parallel, and only the first 47 positions after each
+// chunk's start+min need the truncated (chunk-local) hash.
+//
+// Pipeline (all on the stream, no host round trip):
+//   k_scan      gear hash at every byte, LDS lane-replicated table, per-tile candidate slots
+//   k_tilescan  exclusive scan of per-tile counts -> sorted global candidate array offsets
+//   k_compact   copy slots; k_rescan handles (rare) overflowing tiles exactly
+//   k_chains    one wave per segment: speculative boundary chain from the segment start
+//   k_extend    continue each chain until it merges with the next segment's chain (CDC resync)
+//   k_resolve   prefix-max of merge points -> true chain entry of every segment, validity
+//   k_fallback  serial wave walker for files whose chains did not merge (exact, slower)
+//   k_assemble  canonical-order blob table + BLAKE3 group offsets
+//   k_cut_hash  Chunk.hash (the crate's returned gear state) for every CDC chunk
+#include "bw_device.h"
+#include "bw_internal.h"
+
+namespace bw {
+
+__constant__ uint64_t c_gear[256] = BW_GEAR_INIT;
+
+// ======================================================================== gear scan
+
+__device__ __forceinline__ uint64_t gear_fetch(uint32_t word, uint32_t sel, uint32_t lane_off, const uint64_t* lds) {
+    // v_perm_b32 builds the LDS byte address (byte << 8) | lane_off in one instruction:
+    // result byte0 = lane_off, byte1 = byte k of `word`, bytes 2..3 = 0.  The table holds 32
+    // lane-replicated copies of each entry, so a half-wave's ds_read_b64 is bank-conflict free.
+    const uint32_t addr = __builtin_amdgcn_perm(word, lane_off, sel);
+    return *(const uint64_t*)((const uint8_t*)lds + addr);
+}
+
+__device__ __forceinline__ void gear_step(uint64_t& h, uint32_t word, uint32_t sel, uint32_t lane_off,
+                                          const uint64_t* lds) {
+    h = (h << 1) + gear_fetch(word, sel, lane_off, lds);
+}
+
+#define BW_SEL(k) (0x0c0c0000u | ((4u + (k)) << 8))
+
+__device__ __forceinline__ uint32_t mask_test(uint64_t h, uint32_t mlo, uint32_t mhi) {
+    // (lo & mlo) | (hi & mhi): zero iff (h & mask) == 0 -- one v_and + one v_and_or
+    uint32_t r;
+    const uint32_t t = (uint32_t)h & mlo;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"((uint32_t)(h >> 32)), "s"(mhi), "v"(t));
+    return r;
+}
+
+__device__ __forceinline__ void record_hit(uint64_t pos, uint64_t h, const Masks& mk, uint32_t* s_cnt,
+                                           uint64_t* s_slots) {
+    const bool S = (h & mk.mask_s) == 0, L = (h & mk.mask_l) == 0;
+    if (S || L) {
+        uint32_t i = atomicAdd(s_cnt, 1u);
+        if (i < (uint32_t)SCAN_CAP) s_slots[i] = pos | (S ? BW_CAND_S : 0) | (L ? BW_CAND_L : 0);
+    }
+}
+
+// Every thread owns a 2 KiB strip of the tile, warms the 64-bit gear state up on the 64 bytes
+// before it (the state after 64 steps is exactly the windowed hash), then tests every byte.
+// The test folds 128 positions into one min() and takes the slow recording path only when some
+// position passes the prefilter mask (~2.4e-4 per line at backuwup's parameters).
+__global__ __launch_bounds__(SCAN_THREADS, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
+                                                         uint64_t n_tiles, Masks mk,
+                                                         uint32_t* __restrict__ tile_count,
+                                                         uint64_t* __restrict__ tile_slots) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_REP];  // 64 KiB at LDS offset 0
+    __shared__ uint64_t s_slots[SCAN_CAP];
+    __shared__ uint32_t s_cnt[1];
+    for (int i = threadIdx.x; i < 256 * GEAR_REP; i += blockDim.x) s_gear[i] = c_gear[i / GEAR_REP];
+    const uint32_t lane_off = (threadIdx.x & 31) * 8;
+    const uint32_t mlo = (uint32_t)mk.mask_pre, mhi = (uint32_t)(mk.mask_pre >> 32);
+
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        if (threadIdx.x == 0) *s_cnt = 0;
+        __syncthreads();
+        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_STRIP;
+        if (ss < n_bytes) {
+            const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
+            uint64_t h = 0;
+            if (ss >= 64) {
+                const uint4* wp = (const uint4*)(data + ss - 64);
+                uint4 w[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) w[i] = wp[i];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t ww[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+#pragma unroll
+                        for (int k = 0; k < 4; k++) gear_step(h, ww[j], BW_SEL(k), lane_off, s_gear);
+                }
+            }
+            uint64_t p = ss;
+            for (; p + 128 <= se; p += 128) {
+                const uint4* wp = (const uint4*)(data + p);
+                uint4 w[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) w[i] = wp[i];
+                const uint64_t h0 = h;
+                uint32_t acc = 0xffffffffu;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const uint32_t ww[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
+#pragma unroll
+                    for (int half = 0; half < 2; half++) {
+                        uint64_t g[8];  // issue 8 independent LDS reads before the serial chain
+#pragma unroll
+                        for (int q = 0; q < 8; q++)
+                            g[q] = gear_fetch(ww[half * 2 + q / 4], BW_SEL(q % 4), lane_off, s_gear);
+#pragma unroll
+                        for (int q = 0; q < 8; q += 2) {
+                            h = (h << 1) + g[q];
+                            const uint32_t t0 = mask_test(h, mlo, mhi);
+                            h = (h << 1) + g[q + 1];
+                            const uint32_t t1 = mask_test(h, mlo, mhi);
+                            acc = min(acc, min(t0, t1));
+                        }
+                    }
+                }
+                if (__builtin_expect(acc == 0, 0)) {
+                    // rare: replay the line byte by byte (L1/L2-hot) and record the hits
+                    uint64_t hh = h0;
+                    for (int i = 0; i < 128; i++) {
+                        hh = (hh << 1) + s_gear[(uint32_t)data[p + i] * GEAR_REP];
+                        if (mask_test(hh, mlo, mhi) == 0) record_hit(p + i, hh, mk, s_cnt, s_slots);
+                    }
+                }
+            }
+            for (; p < se; p++) {  // ragged end of the buffer only
+                const uint64_t g = s_gear[(uint32_t)data[p] * GEAR_REP];
+                h = (h << 1) + g;
+                if (mask_test(h, mlo, mhi) == 0) record_hit(p, h, mk, s_cnt, s_slots);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t cnt = *s_cnt, n = cnt < (uint32_t)SCAN_CAP ? cnt : (uint32_t)SCAN_CAP;
+            for (uint32_t i = 1; i < n; i++) {  // insertion sort by position (n is ~1)
+                uint64_t v = s_slots[i];
+                int k = (int)i - 1;
+                while (k >= 0 && BW_CAND_POS(s_slots[k]) > BW_CAND_POS(v)) {
+                    s_slots[k + 1] = s_slots[k];
+                    k--;
+                }
+                s_slots[k + 1] = v;
+            }
+            tile_count[tile] = cnt;
+            for (uint32_t i = 0; i < n; i++) tile_slots[tile * SCAN_CAP + i] = s_slots[i];
+        }
+        __syncthreads();
+    }
+}
+
+void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
+                 uint32_t* tile_count, uint64_t* tile_slots) {
+    if (!n_tiles) return;
+    const size_t lds = 0;
+    const uint64_t grid = n_tiles < 1024 ? n_tiles : 1024;
+    hipLaunchKernelGGL(k_scan, dim3((unsigned)grid), dim3(SCAN_THREADS), lds, st, data, n_bytes, n_tiles, mk,
+                       tile_count, tile_slots);
+}
+
+// ======================================================================== block scan helpers
+
+template <int T>
+__device__ __forceinline__ uint64_t block_excl_sum(uint64_t v, uint64_t* s, uint64_t* total) {
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < T; d <<= 1) {
+        uint64_t a = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0;
+        __syncthreads();
+        s[threadIdx.x] += a;
+        __syncthreads();
+    }
+    const uint64_t incl = s[threadIdx.x];
+    if (total) *total = s[T - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+// (flag, max) segmented exclusive scan; flag = this element starts a new segment
+template <int T>
+__device__ __forceinline__ uint64_t block_excl_segmax(uint32_t f, uint64_t v, uint64_t* s, uint32_t* sf) {
+    s[threadIdx.x] = v;
+    sf[threadIdx.x] = f;
+    __syncthreads();
+    for (int d = 1; d < T; d <<= 1) {
+        uint64_t a = 0;
+        uint32_t af = 0;
+        const bool has = threadIdx.x >= (unsigned)d;
+        if (has) { a = s[threadIdx.x - d]; af = sf[threadIdx.x - d]; }
+        __syncthreads();
+        if (has && !sf[threadIdx.x]) { s[threadIdx.x] = a > s[threadIdx.x] ? a : s[threadIdx.x]; sf[threadIdx.x] = af; }
+        __syncthreads();
+    }
+    // exclusive: value of previous element's inclusive result unless this starts a segment
+    uint64_t r = (threadIdx.x > 0) ? s[threadIdx.x - 1] : 0;
+    __syncthreads();
+    return r;
+}
+
+// ======================================================================== candidate compaction
+
+constexpr int BLK = 1024;
+
+__global__ __launch_bounds__(BLK) void k_tilescan(const uint32_t* __restrict__ cnt, uint64_t n,
+                                                  uint64_t* __restrict__ off, uint64_t cap, uint64_t* ctr) {
+    __shared__ uint64_t s[BLK];
+    const uint64_t per = (n + BLK - 1) / BLK, lo = threadIdx.x * per;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    uint64_t sum = 0;
+    for (uint64_t i = lo; i < hi; i++) sum += cnt[i];
+    uint64_t total;
+    uint64_t run = block_excl_sum<BLK>(sum, s, &total);
+    for (uint64_t i = lo; i < hi; i++) { off[i] = run; run += cnt[i]; }
+    if (threadIdx.x == 0) {
+        off[n] = total;
+        ctr[C_NCAND] = total < cap ? total : cap;
+        ctr[C_CANDTOTAL] = total;
+        ctr[C_NOVF] = 0;
+    }
+}
+
+__global__ void k_compact(const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ slots,
+                          const uint64_t* __restrict__ off, uint64_t n_tiles, uint64_t* __restrict__ cand,
+                          uint64_t cap, uint32_t* __restrict__ ovf, uint64_t* ctr) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tiles) return;
+    const uint32_t c = cnt[t];
+    if (c <= (uint32_t)SCAN_CAP) {
+        for (uint32_t i = 0; i < c; i++)
+            if (off[t] + i < cap) cand[off[t] + i] = slots[t * SCAN_CAP + i];
+    } else {
+        const uint64_t k = atomicAdd((unsigned long long*)&ctr[C_NOVF], 1ull);
+        ovf[k] = (uint32_t)t;
+    }
+}
+
+// Exact ordered re-scan of a tile whose candidates overflowed the slots (pathological data).
+__global__ __launch_bounds__(SCAN_THREADS) void k_rescan(const uint8_t* __restrict__ data, uint64_t n_bytes,
+                                                         Masks mk, const uint32_t* __restrict__ ovf,
+                                                         const uint64_t* __restrict__ off,
+                                                         uint64_t* __restrict__ cand, uint64_t cap,
+                                                         const uint64_t* ctr) {
+    __shared__ uint64_t s_gear[256];
+    __shared__ uint64_t s_scan[SCAN_THREADS];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_gear[i] = c_gear[i];
+    __syncthreads();
+    const uint64_t novf = ctr[C_NOVF];
+    for (uint64_t k = blockIdx.x; k < novf; k += gridDim.x) {
+        const uint64_t tile = ovf[k];
+        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_STRIP;
+        const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
+        uint64_t mine = 0;
+        for (int pass = 0; pass < 2; pass++) {
+            uint64_t h = 0, w = 0;
+            if (pass == 1) w = off[tile] + block_excl_sum<SCAN_THREADS>(mine, s_scan, nullptr);
+            if (ss < n_bytes) {
+                for (uint64_t p = ss >= 64 ? ss - 64 : 0; p < se; p++) {
+                    h = (h << 1) + s_gear[data[p]];
+                    if (p < ss) continue;
+                    const bool S = (h & mk.mask_s) == 0, L = (h & mk.mask_l) == 0;
+                    if (S || L) {
+                        if (pass == 0) mine++;
+                        else if (w < cap) cand[w++] = p | (S ? BW_CAND_S : 0) | (L ? BW_CAND_L : 0);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
+                    const uint32_t* tile_count, const uint64_t* tile_slots, uint64_t* tile_off, uint64_t* cand,
+                    uint64_t cand_cap, uint32_t* ovf_list, uint64_t* ctr) {
+    hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(BLK), 0, st, tile_count, n_tiles, tile_off, cand_cap, ctr);
+    if (!n_tiles) return;
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count,
+                       tile_slots, tile_off, n_tiles, cand, cand_cap, ovf_list, ctr);
+    hipLaunchKernelGGL(k_rescan, dim3(64), dim3(SCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
+                       cand, cand_cap, ctr);
+}
+
+// ======================================================================== the boundary walker
+
+struct Walker {
+    const uint8_t* data;
+    const uint64_t* cand;
+    uint64_t ncand;
+    const uint64_t* lgear;  // plain 256-entry table in LDS
+    Masks mk;
+};
+
+// One step of fastcdc::v2020::cut for the chunk starting at s in a file ending at fe, executed by a
+// whole wavefront (all 64 lanes, wave-uniform control flow).  Returns the next chunk start.
+// `cptr` is the wave's running index into the sorted candidate array; it only moves forward.
+__device__ uint64_t walk_next(const Walker& W, uint64_t s, uint64_t fe, uint64_t& cptr) {
+    const int lane = bw_lane();
+    const uint64_t rem = fe - s;
+    if (rem <= W.mk.min) return fe;  // cut(): remaining <= min_size -> (0, remaining)
+    uint64_t center = W.mk.avg, remaining = rem;
+    if (rem > W.mk.max) remaining = W.mk.max;
+    else if (rem < center) center = rem;
+    const uint64_t s0 = W.mk.s0, c2 = center & ~1ull, r2 = remaining & ~1ull;
+
+    // Head: the first 47 tested positions see a hash truncated at s + s0; recompute them with a
+    // wave-wide shift-scan of the gear recurrence.
+    const uint64_t p = s0 + (uint64_t)lane;
+    const bool valid = lane < 47 && p < r2;
+    const uint64_t g = valid ? W.lgear[W.data[s + p]] : 0;
+    const uint64_t h = bw_gear_scan(g);
+    const uint64_t mask = p < c2 ? W.mk.mask_s : W.mk.mask_l;
+    const uint64_t hb = __ballot(valid && (h & mask) == 0);
+    if (hb) return s + s0 + (uint64_t)__builtin_ctzll(hb);
+
+    // Body: first candidate in [s+s0+47, s+r2) that passes its region's mask.
+    const uint64_t lo = s + s0 + 47, hi = s + r2, c2a = s + c2;
+    for (;;) {
+        const uint64_t idx = cptr + (uint64_t)lane;
+        const uint64_t c = idx < W.ncand ? W.cand[idx] : BW_NONE;
+        const uint64_t pos = c == BW_NONE ? BW_NONE : BW_CAND_POS(c);
+        const uint64_t below = __ballot(pos < lo);
+        const bool match = pos >= lo && pos < hi && ((pos < c2a) ? (c & BW_CAND_S) != 0 : (c & BW_CAND_L) != 0);
+        const uint64_t mb = __ballot(match);
+        if (mb) {
+            const uint64_t cut = bw_shfl64(pos, __builtin_ctzll(mb));
+            cptr += (uint64_t)__popcll(below);
+            return cut;
+        }
+        if (__ballot(pos >= hi) != 0) {  // window exhausted (also covers the array end)
+            cptr += (uint64_t)__popcll(below);
+            return s + remaining;
+        }
+        cptr += 64;
+    }
+}
+
+__device__ __forceinline__ void load_lgear(uint64_t* lg) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = c_gear[i];
+    __syncthreads();
+}
+
+// ======================================================================== speculative chains
+
+constexpr int WAVES_PER_BLOCK = 4;
+
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_chains(Walker W, const uint64_t* __restrict__ tile_off,
+                                                                 const uint64_t* ctr, const SegDesc* __restrict__ segs,
+                                                                 uint64_t nseg, uint64_t* __restrict__ chains,
+                                                                 uint32_t* __restrict__ chain_n,
+                                                                 uint64_t* __restrict__ chain_cptr) {
+    __shared__ uint64_t lg[256];
+    load_lgear(lg);
+    W.lgear = lg;
+    W.ncand = ctr[C_NCAND];
+    const uint64_t j = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
+    if (j >= nseg) return;
+    const SegDesc sd = segs[j];
+    uint64_t s = sd.start, cptr = tile_off[s / SCAN_TILE];
+    uint32_t n = 0;
+    for (;;) {
+        const uint64_t c = walk_next(W, s, sd.file_end, cptr);
+        if (n < (uint32_t)CHAIN_CAP && bw_lane() == 0) chains[j * CHAIN_CAP + n] = c;
+        n++;
+        if (c >= sd.end || n > (uint32_t)CHAIN_CAP) break;
+        s = c;
+    }
+    if (bw_lane() == 0) { chain_n[j] = n; chain_cptr[j] = cptr; }
+}
+
+// Continue chain j past the next segment's start until one of its cuts is also a cut of chain
+// j+1 (CDC resynchronises: from a shared cut on, both chains are identical).  merge[j] = that
+// cut, or BW_NONE when chain j+1's coverage is exhausted first (-> serial walker).
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_extend(Walker W, const uint64_t* ctr,
+                                                                 const SegDesc* __restrict__ segs, uint64_t nseg,
+                                                                 uint64_t* __restrict__ chains,
+                                                                 uint32_t* __restrict__ chain_n,
+                                                                 const uint64_t* __restrict__ chain_cptr,
+                                                                 uint64_t* __restrict__ merge) {
+    __shared__ uint64_t lg[256];
+    load_lgear(lg);
+    W.lgear = lg;
+    W.ncand = ctr[C_NCAND];
+    const uint64_t j = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
+    if (j >= nseg) return;
+    const int lane = bw_lane();
+    const SegDesc sd = segs[j];
+    if (sd.last) { if (lane == 0) merge[j] = sd.file_end; return; }
+    uint32_t n = chain_n[j];
+    const uint32_t n1r = chain_n[j + 1];
+    if (n > (uint32_t)CHAIN_CAP || n1r == 0) { if (lane == 0) merge[j] = BW_NONE; return; }
+    const uint32_t n1 = n1r < (uint32_t)CHAIN_CAP ? n1r : (uint32_t)CHAIN_CAP;
+    const uint64_t* c1 = chains + (j + 1) * CHAIN_CAP;
+    const uint64_t v0 = (uint32_t)lane < n1 ? c1[lane] : BW_NONE;
+    const uint64_t v1 = (uint32_t)lane + 64 < n1 ? c1[lane + 64] : BW_NONE;
+    const uint64_t last1 = c1[n1 - 1];
+    const uint64_t b1 = segs[j + 1].start;
+    uint64_t e = chains[j * CHAIN_CAP + n - 1], cptr = chain_cptr[j], m = BW_NONE;
+    for (;;) {
+        if (e == b1 || __ballot(v0 == e || v1 == e) != 0) { m = e; break; }
+        if (e >= last1 || n >= (uint32_t)CHAIN_CAP) break;
+        e = walk_next(W, e, sd.file_end, cptr);
+        if (lane == 0) chains[j * CHAIN_CAP + n] = e;
+        n++;
+    }
+    if (lane == 0) { chain_n[j] = n; merge[j] = m; }
+}
+
+void launch_chains(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+                   const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg, uint64_t* chains,
+                   uint32_t* chain_n, uint64_t* chain_cptr, uint64_t* merge, int force_serial) {
+    if (!nseg || force_serial) return;
+    Walker W{data, cand, 0, nullptr, mk};
+    const unsigned grid = (unsigned)((nseg + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    hipLaunchKernelGGL(k_chains, dim3(grid), dim3(64 * WAVES_PER_BLOCK), 0, st, W, tile_off, ctr, segs, nseg,
+                       chains, chain_n, chain_cptr);
+    hipLaunchKernelGGL(k_extend, dim3(grid), dim3(64 * WAVES_PER_BLOCK), 0, st, W, ctr, segs, nseg, chains,
+                       chain_n, chain_cptr, merge);
+}
+
+// ======================================================================== resolution
+
+// M_j (first true chunk start inside chain j) = file start for a file's first segment, else
+// max(merge[first .. j-1]).  Segment j contributes its chain entries in [M_j, M_{j+1}).
+__global__ __launch_bounds__(BLK) void k_resolve(const SegDesc* __restrict__ segs, uint64_t nseg,
+                                                 const CFileDesc* __restrict__ cfiles,
+                                                 const uint64_t* __restrict__ chains,
+                                                 const uint32_t* __restrict__ chain_n,
+                                                 const uint64_t* __restrict__ merge, uint64_t* __restrict__ seg_M,
+                                                 uint32_t* __restrict__ seg_cnt, uint32_t* __restrict__ cf_invalid,
+                                                 int force_serial) {
+    __shared__ uint64_t s_v[BLK];
+    __shared__ uint32_t s_f[BLK];
+    const uint64_t per = (nseg + BLK - 1) / BLK, lo = threadIdx.x * per;
+    const uint64_t hi = lo + per < nseg ? lo + per : nseg;
+    // local aggregate of (starts-new-file, max merge)
+    uint32_t af = 0;
+    uint64_t av = 0;
+    for (uint64_t j = lo; j < hi; j++) {
+        const bool head = cfiles[segs[j].cfile].first_seg == j;
+        const uint64_t m = merge[j];
+        if (head) { af = 1; av = m; } else { av = m > av ? m : av; }
+    }
+    uint64_t run = block_excl_segmax<BLK>(af, av, s_v, s_f);
+    for (uint64_t j = lo; j < hi; j++) {
+        const SegDesc sd = segs[j];
+        const bool head = cfiles[sd.cfile].first_seg == j;
+        if (head) run = 0;
+        const uint64_t M = head ? sd.start : run;
+        seg_M[j] = M;
+        const uint64_t m = merge[j];
+        run = m > run ? m : run;
+        if (force_serial) { cf_invalid[sd.cfile] = 1; continue; }
+    }
+    __syncthreads();
+    if (force_serial) return;
+    // membership + counts (needs every seg_M)
+    for (uint64_t j = lo; j < hi; j++) {
+        const SegDesc sd = segs[j];
+        const uint32_t nr = chain_n[j];
+        const uint64_t M = seg_M[j];
+        const uint64_t R = sd.last ? sd.file_end : seg_M[j + 1];
+        bool ok = nr <= (uint32_t)CHAIN_CAP && M != BW_NONE && R != BW_NONE;
+        uint32_t cnt = 0;
+        if (ok) {
+            bool found = (M == sd.start);
+            cnt = (M == sd.start && sd.start < R) ? 1 : 0;
+            for (uint32_t k = 0; k < nr; k++) {
+                const uint64_t e = chains[j * CHAIN_CAP + k];
+                if (e == M) found = true;
+                if (e >= M && e < R && e != sd.start) cnt++;
+            }
+            if (!sd.last && R > M) {  // the chain must reach R (R is one of its cuts)
+                bool reach = false;
+                for (uint32_t k = 0; k < nr; k++) reach |= chains[j * CHAIN_CAP + k] == R;
+                ok = reach;
+            }
+            ok = ok && found;
+        }
+        seg_cnt[j] = cnt;
+        if (!ok) cf_invalid[sd.cfile] = 1;
+    }
+}
+
+// Serial walker for files whose speculative chains did not resolve: one wave walks the whole
+// file, exactly like the crate's iterator, and records every chunk start.
+__global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_fallback(Walker W, const uint64_t* __restrict__ tile_off,
+                                                                   uint64_t* ctr, const CFileDesc* __restrict__ cfiles,
+                                                                   uint64_t ncf, const uint32_t* __restrict__ cf_invalid,
+                                                                   uint64_t* __restrict__ fb_starts,
+                                                                   uint64_t* __restrict__ fb_count) {
+    __shared__ uint64_t lg[256];
+    load_lgear(lg);
+    W.lgear = lg;
+    W.ncand = ctr[C_NCAND];
+    const uint64_t f = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
+    if (f >= ncf || !cf_invalid[f]) return;
+    const CFileDesc cf = cfiles[f];
+    uint64_t s = cf.start, cptr = tile_off[s / SCAN_TILE], n = 0;
+    while (s < cf.end) {
+        if (bw_lane() == 0) fb_starts[cf.fb_off + n] = s;
+        n++;
+        s = walk_next(W, s, cf.end, cptr);
+    }
+    if (bw_lane() == 0) {
+        fb_count[f] = n;
+        atomicAdd((unsigned long long*)&ctr[C_NINVALID], 1ull);
+    }
+}
+
+void launch_resolve(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+                    const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg,
+                    const CFileDesc* cfiles, uint64_t ncf, const uint64_t* chains, const uint32_t* chain_n,
+                    const uint64_t* merge, uint64_t* seg_M, uint32_t* seg_cnt, uint32_t* cf_invalid,
+                    uint64_t* fb_starts, uint64_t* fb_count, int force_serial) {
+    if (!nseg) return;
+    hipMemsetAsync(cf_invalid, 0, ncf * sizeof(uint32_t), st);
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(BLK), 0, st, segs, nseg, cfiles, chains, chain_n, merge, seg_M,
+                       seg_cnt, cf_invalid, force_serial);
+    Walker W{data, cand, 0, nullptr, mk};
+    const unsigned grid = (unsigned)((ncf + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    hipLaunchKernelGGL(k_fallback, dim3(grid), dim3(64 * WAVES_PER_BLOCK), 0, st, W, tile_off, ctr, cfiles, ncf,
+                       cf_invalid, fb_starts, fb_count);
+}
+
+// ======================================================================== assembly
+
+__device__ __forceinline__ uint64_t groups_of(uint64_t len) {
+    const uint64_t leaves = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
+    return (leaves + 3) / 4;
+}
+
+// Emit (or just count) the blobs of unit u.  Returns blob and group counts.
+template <bool WRITE>
+__device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDesc* cfiles, const uint64_t* chains,
+                           const uint32_t* chain_n, const uint64_t* seg_M, const uint32_t* cf_invalid,
+                           const uint64_t* fb_starts, const uint64_t* fb_count, BlobArrays b, uint64_t bbase,
+                           uint64_t gbase, uint64_t& nb, uint64_t& ng) {
+    nb = 0;
+    ng = 0;
+    auto emit = [&](uint64_t start, uint64_t end, uint32_t kind, uint64_t fend) {
+        const uint64_t len = end - start;
+        if (WRITE) {
+            const uint64_t k = bbase + nb;
+            b.start[k] = start;
+            b.len[k] = len;
+            b.goff[k] = gbase + ng;
+            b.file[k] = u.file;
+            b.kind[k] = kind;
+            b.fend[k] = fend;
+        }
+        nb++;
+        ng += groups_of(len);
+    };
+    if (u.kind == 0) { emit(u.start, u.start + u.len, 0, u.start + u.len); return; }
+    const SegDesc sd = segs[u.seg];
+    if (cf_invalid[u.cfile]) {
+        const CFileDesc cf = cfiles[u.cfile];
+        if (cf.first_seg != u.seg) return;
+        const uint64_t n = fb_count[u.cfile];
+        for (uint64_t i = 0; i < n; i++) {
+            const uint64_t s = fb_starts[cf.fb_off + i];
+            const uint64_t e = i + 1 < n ? fb_starts[cf.fb_off + i + 1] : cf.end;
+            emit(s, e, 1, cf.end);
+        }
+        return;
+    }
+    const uint64_t M = seg_M[u.seg];
+    const uint64_t R = sd.last ? sd.file_end : seg_M[u.seg + 1];
+    if (M >= R) return;
+    const uint32_t nr = chain_n[u.seg];
+    uint64_t prev = BW_NONE;
+    if (M == sd.start) prev = sd.start;
+    for (uint32_t k = 0; k < nr; k++) {
+        const uint64_t e = chains[u.seg * CHAIN_CAP + k];
+        if (e < M || e == sd.start) continue;
+        if (e >= R) break;
+        if (prev != BW_NONE) emit(prev, e, 1, sd.file_end);
+        prev = e;
+    }
+    if (prev != BW_NONE) emit(prev, R, 1, sd.file_end);
+}
+
+__global__ __launch_bounds__(BLK) void k_assemble(uint64_t* ctr, const UnitDesc* __restrict__ units, uint64_t nunits,
+                                                  const SegDesc* __restrict__ segs,
+                                                  const CFileDesc* __restrict__ cfiles,
+                                                  const uint64_t* __restrict__ chains,
+                                                  const uint32_t* __restrict__ chain_n,
+                                                  const uint64_t* __restrict__ seg_M,
+                                                  const uint32_t* __restrict__ cf_invalid,
+                                                  const uint64_t* __restrict__ fb_starts,
+                                                  const uint64_t* __restrict__ fb_count, BlobArrays b) {
+    __shared__ uint64_t s[BLK];
+    const uint64_t per = (nunits + BLK - 1) / BLK, lo = threadIdx.x * per;
+    const uint64_t hi = lo + per < nunits ? lo + per : nunits;
+    uint64_t tb = 0, tg = 0;
+    for (uint64_t u = lo; u < hi; u++) {
+        uint64_t nb, ng;
+        unit_blobs<false>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, 0, 0,
+                          nb, ng);
+        tb += nb;
+        tg += ng;
+    }
+    uint64_t totb, totg;
+    uint64_t bb = block_excl_sum<BLK>(tb, s, &totb);
+    uint64_t gb = block_excl_sum<BLK>(tg, s, &totg);
+    for (uint64_t u = lo; u < hi; u++) {
+        uint64_t nb, ng;
+        unit_blobs<true>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, bb, gb,
+                         nb, ng);
+        bb += nb;
+        gb += ng;
+    }
+    if (threadIdx.x == 0) {
+        ctr[C_NBLOBS] = totb;
+        ctr[C_NGROUPS] = totg;
+        ctr[C_DEDUPN] = ctr[C_CANDTOTAL] > ctr[C_NCAND] ? 0 : totb;  // incomplete lists never reach the index
+    }
+}
+
+void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint64_t nunits, const SegDesc* segs,
+                     const CFileDesc* cfiles, const uint64_t* chains, const uint32_t* chain_n, const uint64_t* seg_M,
+                     const uint32_t* seg_cnt, const uint32_t* cf_invalid, const uint64_t* fb_starts,
+                     const uint64_t* fb_count, BlobArrays b, uint64_t max_blobs) {
+    (void)seg_cnt;
+    (void)max_blobs;
+    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(BLK), 0, st, ctr, units, nunits, segs, cfiles, chains, chain_n,
+                       seg_M, cf_invalid, fb_starts, fb_count, b);
+}
+
+// ======================================================================== Chunk.hash
+
+// The crate returns its running gear state with the cut: h_p (odd p) or h_p << 1 (even p, the
+// two-byte loop keeps the even half-step shifted), h of the last tested position when no
+// position cut, and 0 for a tail of <= min bytes.  One wave per CDC chunk, <= 64 terms.
+__global__ __launch_bounds__(256) void k_cut_hash(const uint8_t* __restrict__ data, Masks mk,
+                                                  const uint64_t* ctr, BlobArrays b) {
+    const uint64_t k = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    if (k >= ctr[C_NBLOBS]) return;
+    const int lane = bw_lane();
+    if (b.kind[k] == 0) { if (lane == 0) b.ghash[k] = 0; return; }
+    const uint64_t s = b.start[k], len = b.len[k], fe = b.fend[k];
+    const uint64_t rem = fe - s;
+    uint64_t out = 0;
+    if (rem > mk.min) {
+        const uint64_t remaining = rem > mk.max ? mk.max : rem;
+        const uint64_t r2 = remaining & ~1ull;
+        uint64_t p = BW_NONE;
+        if (len == remaining) { if (r2 > mk.s0) p = r2 - 1; }
+        else p = len;
+        if (p != BW_NONE) {
+            const uint64_t q = p - (uint64_t)lane;
+            uint64_t term = 0;
+            if ((uint64_t)lane <= p && q >= mk.s0) term = c_gear[data[s + q]] << lane;
+            out = bw_wave_sum64(term);
+            if ((p & 1) == 0) out <<= 1;
+        }
+    }
+    if (lane == 0) b.ghash[k] = out;
+}
+
+void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* ctr, BlobArrays b,
+                     uint64_t max_blobs) {
+    if (!max_blobs) return;
+    hipLaunchKernelGGL(k_cut_hash, dim3((unsigned)((max_blobs + 3) / 4)), dim3(256), 0, st, data, mk, ctr, b);
+}
+
+}  // namespace bw

@@ -1,0 +1,119 @@
+// bw_internal.h -- host-side declarations shared by the backuwup_amd translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bw {
+
+// ------------------------------------------------------------------ tunables
+constexpr int SCAN_THREADS = 512;
+constexpr int SCAN_STRIP = 2048;                                  // bytes per thread
+constexpr uint64_t SCAN_TILE = (uint64_t)SCAN_THREADS * SCAN_STRIP; // 1 MiB per tile
+constexpr int SCAN_CAP = 32;                                      // candidate slots per tile
+constexpr int GEAR_REP = 32;                                      // LDS gear replicas
+constexpr int CHAIN_CAP = 128;                                    // cuts stored per segment
+
+// device counter slots (uint64 each)
+enum Ctr : int {
+    C_NCAND = 0,     // gear candidates stored (clamped to the candidate array capacity)
+    C_NOVF = 1,      // tiles whose candidates overflowed SCAN_CAP
+    C_NBLOBS = 2,    // blobs produced by the batch
+    C_NGROUPS = 3,   // BLAKE3 4-leaf groups
+    C_SEQBASE = 4,   // dedup log position of the batch's first blob
+    C_COLLIDE = 5,   // 64-bit key collision seen by the index
+    C_NINVALID = 6,  // files that needed the serial boundary walker
+    C_NUNIQUE = 7,   // distinct digests in the index
+    C_CANDTOTAL = 8, // gear candidates found (> C_NCAND: capacity too small, batch re-run)
+    C_DEDUPN = 9,    // blobs handed to the index (0 when the batch must be re-run)
+    C_COUNT = 16
+};
+
+struct Masks {
+    uint32_t min, avg, max, s0;  // s0 = 2 * (min / 2): first position the crate hashes
+    uint64_t mask_s, mask_l, mask_pre;  // mask_pre = mask_s & mask_l (scan prefilter)
+};
+
+// One boundary-resolution segment: a window [start, end) of one CDC file.
+struct SegDesc {
+    uint64_t start, end, file_end;
+    uint32_t cfile;  // index among the batch's CDC files
+    uint32_t last;   // 1 = last segment of its file
+};
+
+struct CFileDesc {
+    uint64_t start, end;  // global byte range of the file
+    uint64_t fb_off;      // offset into the serial-walker output buffer
+    uint32_t first_seg, nseg;
+};
+
+// Canonical-order unit: either a whole small file (kind 0) or one CDC segment (kind 1).
+struct UnitDesc {
+    uint64_t start, len;  // small file: its range; segment: unused
+    uint32_t file;        // batch file index
+    uint32_t kind;        // 0 = small-file blob, 1 = CDC segment
+    uint32_t seg;         // segment index (kind 1)
+    uint32_t cfile;       // CDC file index (kind 1)
+};
+
+// Blob table (struct of arrays), canonical order.
+struct BlobArrays {
+    uint64_t* start;  // global byte position
+    uint64_t* len;
+    uint64_t* goff;   // first BLAKE3 group
+    uint32_t* file;
+    uint32_t* kind;   // 0 = whole-file blob, 1 = CDC chunk
+    uint64_t* fend;   // end of the owning file (for Chunk.hash of CDC chunks)
+    uint64_t* ghash;  // Chunk.hash
+};
+
+// ------------------------------------------------------------------ launchers (bw_cdc.hip)
+void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
+                 const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots);
+void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
+                    const Masks& mk, const uint32_t* tile_count, const uint64_t* tile_slots,
+                    uint64_t* tile_off, uint64_t* cand, uint64_t cand_cap, uint32_t* ovf_list,
+                    uint64_t* ctr);
+void launch_chains(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+                   const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg,
+                   uint64_t* chains, uint32_t* chain_n, uint64_t* chain_cptr, uint64_t* merge,
+                   int force_serial);
+void launch_resolve(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+                    const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg,
+                    const CFileDesc* cfiles, uint64_t ncf, const uint64_t* chains,
+                    const uint32_t* chain_n, const uint64_t* merge, uint64_t* seg_M,
+                    uint32_t* seg_cnt, uint32_t* cf_invalid, uint64_t* fb_starts,
+                    uint64_t* fb_count, int force_serial);
+void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint64_t nunits,
+                     const SegDesc* segs, const CFileDesc* cfiles, const uint64_t* chains,
+                     const uint32_t* chain_n, const uint64_t* seg_M, const uint32_t* seg_cnt,
+                     const uint32_t* cf_invalid, const uint64_t* fb_starts,
+                     const uint64_t* fb_count, BlobArrays b, uint64_t max_blobs);
+void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* ctr,
+                     BlobArrays b, uint64_t max_blobs);
+
+// ------------------------------------------------------------------ launchers (bw_blake3.hip)
+void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b,
+                   uint64_t max_blobs, uint64_t max_groups, uint32_t* cv_buf,
+                   uint8_t* digest_log /* + ctr[C_SEQBASE] * 32 */, int max_leaves);
+
+// ------------------------------------------------------------------ launchers (bw_dedup.hip)
+// Dedup state (device, persistent across batches): st[0] = log length (next seq),
+// st[1] = distinct digests, st[2] = collision flag.
+enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_COLLIDE = 2, D_COUNT = 4 };
+void launch_table_clear(hipStream_t st, uint64_t* table, uint64_t cap);
+// Append n digests (n from *n_dev if non-null, else n_host) to the log and decide them in
+// order: is_dup[i] (may be null) = digest seen at an earlier log position.
+void launch_dedup(hipStream_t st, uint64_t* table, uint64_t cap, uint8_t* log, uint64_t* dstate,
+                  const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
+                  uint8_t* is_dup);
+// Re-claim log[0 .. *len) into a fresh table (growth).
+void launch_rehash(hipStream_t st, uint64_t* table, uint64_t cap, const uint8_t* log,
+                   const uint64_t* dstate, uint64_t max_n);
+void launch_partition(hipStream_t st, const uint8_t* digests, uint64_t n, uint32_t n_owners,
+                      uint8_t* out, uint64_t* perm, uint64_t* counts_dev);
+void launch_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, uint64_t n,
+                    uint8_t* is_dup);
+void launch_pack(hipStream_t st, const uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
+                 const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs);
+
+}  // namespace bw

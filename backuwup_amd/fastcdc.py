@@ -1,0 +1,48 @@
+"""Drop-in for `fastcdc::v2020` as backuwup uses it (crate fastcdc 3.0.3, Cargo.lock:557-560).
+
+    let chunker = FastCDC::new(&mmap, min, avg, max);      // dir_packer.rs:254-259
+    for chunk in chunker { &mmap[chunk.offset..chunk.offset + chunk.length] }   // :261-266
+
+Here `FastCDC(source, min_size, avg_size, max_size)` chunks the whole source on the GPU when
+it is constructed and iterates `Chunk(hash, offset, length)` like the crate's iterator.  Size
+parameters outside the crate's asserted ranges raise ValueError (the crate panics).
+"""
+from collections import namedtuple
+
+from ._lib import BW_EINVAL, BwError
+from .context import default_context
+
+MINIMUM_MIN = 64
+MINIMUM_MAX = 1_048_576
+AVERAGE_MIN = 256
+AVERAGE_MAX = 4_194_304
+MAXIMUM_MIN = 1024
+MAXIMUM_MAX = 16_777_216
+
+Chunk = namedtuple("Chunk", ["hash", "offset", "length"])
+
+
+class ChunkParameterError(ValueError):
+    pass
+
+
+class FastCDC:
+    def __init__(self, source, min_size, avg_size, max_size, ctx=None):
+        if not (MINIMUM_MIN <= min_size <= MINIMUM_MAX and AVERAGE_MIN <= avg_size <= AVERAGE_MAX
+                and MAXIMUM_MIN <= max_size <= MAXIMUM_MAX):
+            raise ChunkParameterError("fastcdc size parameters out of range: %d/%d/%d"
+                                      % (min_size, avg_size, max_size))
+        ctx = ctx or default_context()
+        try:
+            self._chunks = [Chunk(*c) for c in ctx.fastcdc_chunks(source, min_size, avg_size, max_size)]
+        except BwError as e:
+            if e.rc == BW_EINVAL:
+                raise ChunkParameterError(str(e)) from e
+            raise
+        self.min_size, self.avg_size, self.max_size = min_size, avg_size, max_size
+
+    def __iter__(self):
+        return iter(self._chunks)
+
+    def __len__(self):
+        return len(self._chunks)

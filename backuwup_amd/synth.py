@@ -1,0 +1,145 @@
+"""Deterministic synthetic corpora for the BASELINE.json configurations.
+
+All byte streams are counter-based splitmix64: word i of stream `seed` is
+mix(seed + (i + 1) * 0x9E3779B97F4A7C15), emitted little-endian.  The same stream is produced
+by numpy on the host and by torch on the GPU (`splitmix_torch`), so a device-resident corpus can
+be checked slice by slice on the CPU.
+"""
+import numpy as np
+
+GOLDEN = 0x9E3779B97F4A7C15
+M1 = 0xBF58476D1CE4E5B9
+M2 = 0x94D049BB133111EB
+
+
+def splitmix_words(seed, first_word, n_words):
+    with np.errstate(over="ignore"):
+        i = np.arange(first_word + 1, first_word + 1 + n_words, dtype=np.uint64)
+        z = np.uint64(seed) + i * np.uint64(GOLDEN)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(M1)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(M2)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def splitmix_bytes(seed, nbytes, offset=0):
+    """bytes [offset, offset + nbytes) of stream `seed`."""
+    w0 = offset // 8
+    w1 = (offset + nbytes + 7) // 8
+    words = splitmix_words(seed, w0, w1 - w0)
+    b = words.view(np.uint8)
+    s = offset - w0 * 8
+    return b[s:s + nbytes].copy()
+
+
+def _to_i64(x):
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def splitmix_torch(seed, nbytes, device, out=None, chunk_words=1 << 27):
+    """The same stream generated on the GPU with torch int64 arithmetic (wrapping multiply,
+    logical shifts via masks).  Returns a uint8 tensor of nbytes (16-byte aligned storage)."""
+    import torch
+    n_words = (nbytes + 7) // 8
+    if out is None:
+        out = torch.empty(n_words * 8, dtype=torch.uint8, device=device)
+    ow = out.view(torch.int64) if out.numel() % 8 == 0 else None
+    g, m1, m2, sd = _to_i64(GOLDEN), _to_i64(M1), _to_i64(M2), _to_i64(seed)
+
+    def lsr(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+
+    for w0 in range(0, n_words, chunk_words):
+        w1 = min(n_words, w0 + chunk_words)
+        z = torch.arange(w0 + 1, w1 + 1, dtype=torch.int64, device=device)
+        z.mul_(g).add_(sd)
+        z = (z ^ lsr(z, 30)).mul_(m1)
+        z = (z ^ lsr(z, 27)).mul_(m2)
+        z = z ^ lsr(z, 31)
+        ow[w0:w1] = z
+    return out[:nbytes]
+
+
+# ------------------------------------------------------------------ corpora
+
+def tree_corpus(total_bytes, seed=0x6261636B, dup_fraction=0.30, min_file=4096, max_file=64 << 20):
+    """C1: log-uniform file sizes, unique PRNG content, plus `dup_fraction` of the bytes as
+    whole-file copies of earlier files.  Returns (data uint8, file_off, file_len)."""
+    rng = np.random.default_rng(seed)
+    uniq_target = int(total_bytes * (1 - dup_fraction))
+    sizes = []
+    acc = 0
+    while acc < uniq_target:
+        s = int(np.exp(rng.uniform(np.log(min_file), np.log(max_file))))
+        s = min(s, uniq_target - acc) if uniq_target - acc > min_file else s
+        sizes.append(s)
+        acc += s
+    files = [(i, s) for i, s in enumerate(sizes)]
+    copies = []
+    dup_acc = 0
+    while dup_acc < total_bytes - acc and files:
+        i = int(rng.integers(len(files)))
+        copies.append(i)
+        dup_acc += sizes[i]
+    order = list(range(len(sizes))) + [("copy", c) for c in copies]
+    rng.shuffle(order)
+    lens = [sizes[o[1]] if isinstance(o, tuple) else sizes[o] for o in order]
+    total = sum(lens)
+    data = np.empty(total, dtype=np.uint8)
+    offs = np.zeros(len(order), dtype=np.uint64)
+    pos = 0
+    for k, o in enumerate(order):
+        src = o[1] if isinstance(o, tuple) else o
+        n = sizes[src]
+        data[pos:pos + n] = splitmix_bytes(seed * 1000 + src, n)
+        offs[k] = pos
+        pos += n
+    return data, offs, np.array(lens, dtype=np.uint64)
+
+
+def vm_image_variants(base_bytes, n_variants, seed=1, n_indels=32, n_overwrites=16, max_indel=64):
+    """C3: a random base image plus variants with small insertions/deletions (byte shifts) and
+    4 KiB overwrites.  Returns (data, file_off, file_len) with the base as file 0."""
+    rng = np.random.default_rng(seed)
+    base = splitmix_bytes(seed, base_bytes)
+    images = [base]
+    for v in range(1, n_variants):
+        r = np.random.default_rng(seed * 7919 + v)
+        img = base.copy()
+        for _ in range(n_overwrites):
+            at = int(r.integers(0, max(1, img.size - 4096)))
+            img[at:at + 4096] = r.integers(0, 256, 4096, dtype=np.uint8)
+        edits = sorted(int(x) for x in r.integers(0, img.size, n_indels))
+        parts = []
+        prev = 0
+        for at in edits:
+            parts.append(img[prev:at])
+            k = int(r.integers(1, max_indel + 1))
+            if r.integers(2):
+                parts.append(r.integers(0, 256, k, dtype=np.uint8))
+                prev = at
+            else:
+                prev = min(img.size, at + k)
+        parts.append(img[prev:])
+        images.append(np.concatenate(parts))
+    offs = np.cumsum([0] + [im.size for im in images[:-1]]).astype(np.uint64)
+    lens = np.array([im.size for im in images], dtype=np.uint64)
+    return np.concatenate(images), offs, lens
+
+
+def small_files(n_files, seed=3, lo=4096, hi=65536, dup_fraction=0.30):
+    """C4: n_files with sizes uniform in [lo, hi] plus whole-file copies."""
+    rng = np.random.default_rng(seed)
+    n_uniq = int(round(n_files * (1 - dup_fraction)))
+    sizes = rng.integers(lo, hi + 1, n_uniq)
+    src = list(range(n_uniq)) + [int(x) for x in rng.integers(0, n_uniq, n_files - n_uniq)]
+    rng.shuffle(src)
+    uniq_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    blob = splitmix_bytes(seed, int(sizes.sum()))
+    lens = np.array([sizes[s] for s in src], dtype=np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = np.empty(int(lens.sum()), dtype=np.uint8)
+    for k, s in enumerate(src):
+        data[int(offs[k]):int(offs[k]) + int(lens[k])] = blob[int(uniq_off[s]):int(uniq_off[s]) + int(sizes[s])]
+    return data, offs, lens

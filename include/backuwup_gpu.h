@@ -1,0 +1,168 @@
+/*
+ * backuwup_gpu.h -- C ABI of the MI355X (gfx950) dedup front end for backuwup.
+ *
+ * The reference has no FFI layer on this path; it reaches three Rust call sites directly
+ * (SURVEY.md §8b).  Each entry point below replaces one of them and keeps its argument
+ * meaning and error behaviour; INTEGRATION.md shows the Rust `extern "C"` binding:
+ *
+ *   fastcdc::v2020::FastCDC::new(&[u8], min, avg, max) + Iterator<Item = Chunk>
+ *       client/src/backup/filesystem/dir_packer.rs:254-266          -> bw_fastcdc_chunks
+ *   blake3::hash(&[u8]) -> Hash  (then .into(): [u8; 32])
+ *       client/src/backup/filesystem/dir_packer.rs:286, :320, :353  -> bw_blake3_hash(_many)
+ *   BlobIndex::load() (sorted `items`)            blob_index.rs:167-200  -> bw_index_seed
+ *   Manager::add_blob dedup gate -> BlobIndex::is_blob_duplicate, then blobs_queued.insert
+ *       pack.rs:37-39, blob_index.rs:109,130-148                     -> bw_index_check_insert
+ *   dir_packer::process_file + add_file_blob for a batch of files (dir_packer.rs:231-311)
+ *                                                                   -> bw_process_files(_device)
+ *
+ * Conventions: every function returns an int status (BW_OK = 0, negative = error) and never
+ * unwinds across the boundary.  Where the fastcdc crate panics on an assert (parameter ranges)
+ * this returns BW_EINVAL.  Output arrays are caller-owned; when one is too small BW_ENOSPC is
+ * returned and *n_out holds the required count.  Device buffers, streams and the dedup table
+ * are owned by the opaque bw_ctx.  A context is not thread-safe: the reference serializes
+ * index access under the packer mutex (packfile/mod.rs:77); callers hashing from several
+ * threads use one context per thread.
+ *
+ * Scalars: "device pointer" arguments are HIP device addresses (e.g. from hipMalloc or a
+ * torch tensor's data_ptr()), 16-byte aligned; everything else is host memory.
+ */
+#ifndef BACKUWUP_GPU_H
+#define BACKUWUP_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BW_API_VERSION 1
+
+enum {
+    BW_OK = 0,
+    BW_EINVAL = -1,     /* parameter outside the fastcdc crate's asserted ranges, bad pointer  */
+    BW_ENOSPC = -2,     /* caller's output array too small; *n_out = required count            */
+    BW_EHIP = -3,       /* HIP runtime error (message in bw_last_error)                        */
+    BW_ENOMEM = -4,     /* device or host allocation failed                                    */
+    BW_ECOLLISION = -5, /* two distinct digests share a 64-bit table key: verdicts withheld    */
+    BW_ESTATE = -6      /* call order violated (e.g. bw_results before a batch was submitted)   */
+};
+
+/* fastcdc::v2020 size bounds (asserted by FastCDC::with_level) */
+#define BW_MINIMUM_MIN 64u
+#define BW_MINIMUM_MAX 1048576u
+#define BW_AVERAGE_MIN 256u
+#define BW_AVERAGE_MAX 4194304u
+#define BW_MAXIMUM_MIN 1024u
+#define BW_MAXIMUM_MAX 16777216u
+
+/* backuwup's chunker constants, client/src/defaults.rs:61-68 */
+#define BW_BLOB_MINIMUM_TARGET_SIZE 262144u  /* 256 KiB */
+#define BW_BLOB_DESIRED_TARGET_SIZE 1048576u /* 1 MiB   */
+#define BW_BLOB_MAX_UNCOMPRESSED_SIZE 3145728u /* 3 MiB */
+
+typedef struct bw_ctx bw_ctx;
+
+/* fastcdc::v2020::Chunk { hash: u64, offset: usize, length: usize } */
+typedef struct bw_chunk {
+    uint64_t hash;
+    uint64_t offset;
+    uint64_t length;
+} bw_chunk;
+
+/* One blob produced by process_file/add_file_blob (dir_packer.rs:231-311), in canonical order
+ * (files in the order given, chunks in offset order). */
+typedef struct bw_blob {
+    uint64_t file;      /* index of the source file in the batch                            */
+    uint64_t offset;    /* offset of the blob inside its file                                */
+    uint64_t length;    /* blob length                                                       */
+    uint64_t gear_hash; /* Chunk.hash for CDC chunks; 0 for whole-file blobs                 */
+    uint8_t digest[32]; /* blake3::hash(blob) = BlobHash                                     */
+    uint8_t is_dup;     /* 1 = Manager::add_blob returns Ok(None) (already seen)             */
+    uint8_t pad[7];
+} bw_blob;
+
+/* Batch parameters.  Defaults (bw_params_default): backuwup's 256 KiB / 1 MiB / 3 MiB and the
+ * small-file rule `len > BLOB_DESIRED_TARGET_SIZE` -> CDC (dir_packer.rs:246). */
+typedef struct bw_params {
+    uint32_t min_size;
+    uint32_t avg_size;
+    uint32_t max_size;
+    uint32_t flags;                /* BW_F_* below                                      */
+    uint64_t small_file_threshold; /* files with len > threshold are chunked by CDC     */
+} bw_params;
+
+#define BW_F_NO_HASH 1u        /* chunk only (digests left zero)                           */
+#define BW_F_NO_DEDUP 2u       /* skip the index (is_dup left 0); digests still logged     */
+#define BW_F_SERIAL_RESOLVE 4u /* force the serial boundary walker (test/diagnostic path)  */
+
+void bw_params_default(bw_params* p);
+const char* bw_strerror(int rc);
+
+int bw_create(int device, bw_ctx** out);
+void bw_destroy(bw_ctx* ctx);
+const char* bw_last_error(const bw_ctx* ctx);
+/* Run on a caller stream (hipStream_t as void*); NULL selects the context's own stream. */
+int bw_set_stream(bw_ctx* ctx, void* hip_stream);
+void* bw_get_stream(bw_ctx* ctx);
+
+/* FastCDC::new(src, min, avg, max).collect::<Vec<Chunk>>() over a host buffer. */
+int bw_fastcdc_chunks(bw_ctx* ctx, const uint8_t* src, uint64_t len, uint32_t min_size,
+                      uint32_t avg_size, uint32_t max_size, bw_chunk* out, uint64_t cap,
+                      uint64_t* n_out);
+
+/* blake3::hash(data) -> 32 bytes, host buffer. */
+int bw_blake3_hash(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
+/* n independent messages data[offsets[i] .. offsets[i]+lengths[i]) -> out[32*i..] */
+int bw_blake3_hash_many(bw_ctx* ctx, const uint8_t* data, uint64_t data_len,
+                        const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
+                        uint8_t* out);
+
+/* BlobIndex: empty the in-HBM index (capacity_hint = expected entries, 0 = default). */
+int bw_index_reset(bw_ctx* ctx, uint64_t capacity_hint);
+/* BlobIndex::load: seed with prior backups' sorted digests (n x 32 bytes). */
+int bw_index_seed(bw_ctx* ctx, const uint8_t* sorted_digests, uint64_t n);
+/* n digests in canonical order: is_dup[i] = is_blob_duplicate(d_i) at its turn, and every
+ * non-duplicate is then inserted (pack.rs:37 + blob_index.rs:109).  Host buffers. */
+int bw_index_check_insert(bw_ctx* ctx, const uint8_t* digests, uint64_t n, uint8_t* is_dup);
+/* number of distinct digests currently in the index */
+int bw_index_size(bw_ctx* ctx, uint64_t* n);
+
+/* Whole front end for a batch of files stored back to back in a host buffer: chunk -> hash
+ * -> dedup; synchronous; results in canonical order. */
+int bw_process_files(bw_ctx* ctx, const uint8_t* data, uint64_t data_len,
+                     const uint64_t* file_off, const uint64_t* file_len, uint64_t n_files,
+                     const bw_params* params, bw_blob* out, uint64_t cap, uint64_t* n_out);
+
+/* Same with the bytes already resident in HBM (d_data = device pointer, 16-byte aligned).
+ * File tables are host arrays.  Asynchronous on the context stream: nothing is copied back
+ * until bw_results(). */
+int bw_process_files_device(bw_ctx* ctx, const uint8_t* d_data, uint64_t data_len,
+                            const uint64_t* file_off, const uint64_t* file_len, uint64_t n_files,
+                            const bw_params* params);
+/* Wait for the last submitted batch and copy its blobs out. */
+int bw_results(bw_ctx* ctx, bw_blob* out, uint64_t cap, uint64_t* n_out);
+/* Device views of the last batch (valid until the next submit): n blobs (synchronizes),
+ * digests (n x 32 B, canonical order) and is_dup bytes. */
+int bw_batch_device_views(bw_ctx* ctx, uint64_t* n_blobs, const uint8_t** d_digests,
+                          uint8_t** d_is_dup);
+
+/* ---- multi-GPU digest exchange (index partitioned by digest prefix, RCCL all-to-all) ----
+ * owner(d) = d[0] >> (8 - log2(n_owners)), n_owners a power of two <= 256.
+ * Stable partition of n device digests by owner: d_out (n x 32 B, grouped by owner, canonical
+ * order kept inside each group), d_perm[n] = source index of each output digest,
+ * h_counts[n_owners] (host) = digests per owner.  Synchronizes (the counts size the exchange). */
+int bw_partition_by_owner(bw_ctx* ctx, const uint8_t* d_digests, uint64_t n, uint32_t n_owners,
+                          uint8_t* d_out, uint64_t* d_perm, uint64_t* h_counts);
+/* Owner side: n device digests in canonical order (an all-to-all output is source-rank-major,
+ * which is canonical when files are sharded rank-major) -> d_is_dup[n] (device). */
+int bw_index_check_insert_device(bw_ctx* ctx, const uint8_t* d_digests, uint64_t n,
+                                 uint8_t* d_is_dup);
+/* Scatter owner verdicts back to source order: d_is_dup[d_perm[i]] = d_verdict[i]. */
+int bw_scatter_verdicts(bw_ctx* ctx, const uint8_t* d_verdict, const uint64_t* d_perm,
+                        uint64_t n, uint8_t* d_is_dup);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BACKUWUP_GPU_H */

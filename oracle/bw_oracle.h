@@ -1,0 +1,70 @@
+/*
+ * bw_oracle.h -- CPU restatement of backuwup's dedup front end.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.  The
+ * product path (backuwup_amd/, libbackuwup_amd.so) never links, imports or calls it.
+ *
+ * PARITY STATUS: the reference's arithmetic lives in two third-party Rust crates that are
+ * absent from /root/reference and unbuildable here (no cargo/rustc, no network):
+ *   - fastcdc 3.0.3 (Cargo.lock:557-560), module v2020, Normalization::Level1
+ *   - blake3  1.3.3 (Cargo.lock:149-159), blake3::hash()
+ * The reference's own tests pin none of this path, so parity is UNPINNED BY THE
+ * REFERENCE.  This restatement is pinned instead by: the published BLAKE3 known answers
+ * (SURVEY.md A.4), the GEAR derivation rule + sha256 (A.2), the MASKS popcount identity (A.3),
+ * an independent pure-Python BLAKE3/FastCDC restatement (tests/golden/make_golden.py), and the
+ * cross-check vector of A.5.
+ */
+#ifndef BW_ORACLE_H
+#define BW_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same layout as bw_blob in include/backuwup_gpu.h (checked by tests). */
+typedef struct orc_blob {
+    uint64_t file;      /* index of the file in the batch (canonical order)             */
+    uint64_t offset;    /* byte offset of the blob inside its file                       */
+    uint64_t length;    /* blob length in bytes                                          */
+    uint64_t gear_hash; /* fastcdc Chunk.hash for CDC chunks, 0 for whole-file blobs     */
+    uint8_t digest[32]; /* blake3::hash(blob)                                            */
+    uint8_t is_dup;     /* 1 if Manager::add_blob would return Ok(None) (dedup hit)       */
+    uint8_t pad[7];
+} orc_blob;
+
+typedef struct orc_index orc_index;
+
+void orc_gear_table(uint64_t out[256]);
+/* FastCDC::with_level(.., Level1) parameter validation + mask selection.  0 ok, -1 = the crate
+ * would panic on an assert. */
+int orc_fastcdc_masks(uint32_t min, uint32_t avg, uint32_t max, uint64_t* mask_s, uint64_t* mask_l);
+/* fastcdc::v2020::cut() on src[0..len): returns the cut length, writes the gear hash. */
+size_t orc_fastcdc_cut(const uint8_t* src, size_t len, uint32_t min, uint32_t avg, uint32_t max,
+                       uint64_t mask_s, uint64_t mask_l, uint64_t* hash);
+/* FastCDC::new(src, min, avg, max).collect(): chunks as (hash, offset, length) triples. */
+int orc_fastcdc_chunks(const uint8_t* src, size_t len, uint32_t min, uint32_t avg, uint32_t max,
+                       uint64_t* out_hash, uint64_t* out_off, uint64_t* out_len, size_t cap,
+                       size_t* n_out);
+void orc_blake3(const uint8_t* data, size_t len, uint8_t out[32]);
+
+orc_index* orc_index_new(const uint8_t* sorted_digests, size_t n);
+void orc_index_free(orc_index* ix);
+int orc_index_is_duplicate(orc_index* ix, const uint8_t digest[32]);
+int orc_index_insert(orc_index* ix, const uint8_t digest[32]);
+
+/* The whole front end over a batch of files laid out back to back in `data`:
+ * process_file policy (dir_packer.rs:231-282) -> blake3 -> dedup gate in canonical order.
+ * Chunk + hash run on `threads` pthreads, parallel across files and serial within a file
+ * (the reference's task-per-file model, dir_packer.rs:148-166); dedup runs serially in
+ * canonical order on `ix` (may be NULL = empty index). */
+int orc_process_files(const uint8_t* data, const uint64_t* file_off, const uint64_t* file_len,
+                      size_t n_files, uint32_t min, uint32_t avg, uint32_t max,
+                      uint64_t small_file_threshold, orc_index* ix, int threads,
+                      orc_blob* out, size_t cap, size_t* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

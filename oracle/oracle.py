@@ -1,0 +1,147 @@
+"""ctypes loader for the CPU oracle (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY -- import from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never from the product package (backuwup_amd/).  Parity status: see
+oracle/bw_oracle.h (unpinned by the reference; pinned by spec KATs and derived constants).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liboracle.so")
+
+
+class OrcBlob(ctypes.Structure):
+    _fields_ = [("file", ctypes.c_uint64), ("offset", ctypes.c_uint64),
+                ("length", ctypes.c_uint64), ("gear_hash", ctypes.c_uint64),
+                ("digest", ctypes.c_uint8 * 32), ("is_dup", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 7)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.orc_gear_table.argtypes = [u64p]
+        L.orc_fastcdc_masks.argtypes = [ctypes.c_uint32] * 3 + [u64p, u64p]
+        L.orc_fastcdc_chunks.argtypes = [ctypes.c_void_p, ctypes.c_size_t] + [ctypes.c_uint32] * 3 + \
+            [u64p, u64p, u64p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        L.orc_blake3.argtypes = [ctypes.c_void_p, ctypes.c_size_t, u8p]
+        L.orc_index_new.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.orc_index_new.restype = ctypes.c_void_p
+        L.orc_index_free.argtypes = [ctypes.c_void_p]
+        L.orc_index_is_duplicate.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_index_insert.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_process_files.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_size_t,
+                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.POINTER(OrcBlob), ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.c_size_t)]
+        _lib = L
+    return _lib
+
+
+def _u64p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def _buf(data):
+    if isinstance(data, np.ndarray):
+        return data.ctypes.data, data.nbytes, data
+    b = bytes(data)
+    return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value, len(b), b
+
+
+def gear_table():
+    out = np.zeros(256, dtype=np.uint64)
+    lib().orc_gear_table(_u64p(out))
+    return out
+
+
+def masks(min_size, avg_size, max_size):
+    s, l = ctypes.c_uint64(), ctypes.c_uint64()
+    if lib().orc_fastcdc_masks(min_size, avg_size, max_size, ctypes.byref(s), ctypes.byref(l)):
+        raise ValueError("fastcdc parameter out of range")
+    return s.value, l.value
+
+
+def fastcdc(data, min_size, avg_size, max_size):
+    """FastCDC::new(data, min, avg, max).collect() -> list of (hash, offset, length)."""
+    ptr, n, keep = _buf(data)
+    cap = n // max(min_size, 1) + 2
+    h, o, l = (np.zeros(cap, dtype=np.uint64) for _ in range(3))
+    cnt = ctypes.c_size_t()
+    rc = lib().orc_fastcdc_chunks(ptr, n, min_size, avg_size, max_size, _u64p(h), _u64p(o),
+                                  _u64p(l), cap, ctypes.byref(cnt))
+    if rc:
+        raise ValueError("orc_fastcdc_chunks rc=%d" % rc)
+    k = cnt.value
+    return [(int(h[i]), int(o[i]), int(l[i])) for i in range(k)]
+
+
+def blake3(data):
+    ptr, n, keep = _buf(data)
+    out = (ctypes.c_uint8 * 32)()
+    lib().orc_blake3(ptr, n, out)
+    return bytes(out)
+
+
+class Index:
+    """BlobIndex restatement: sorted prior items + blobs_queued set (blob_index.rs:44-148)."""
+
+    def __init__(self, sorted_digests=b""):
+        arr = np.frombuffer(bytes(sorted_digests), dtype=np.uint8)
+        self._keep = arr
+        self.h = lib().orc_index_new(arr.ctypes.data if arr.size else None, arr.size // 32)
+
+    def is_blob_duplicate(self, d):
+        return bool(lib().orc_index_is_duplicate(self.h, bytes(d)))
+
+    def insert(self, d):
+        return lib().orc_index_insert(self.h, bytes(d))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_index_free(self.h)
+            self.h = None
+
+
+def process_files(data, file_off, file_len, min_size=262144, avg_size=1048576,
+                  max_size=3145728, small_threshold=None, index=None, threads=1):
+    """Batch front end -> structured numpy array of blobs (file, offset, length, gear_hash,
+    digest, is_dup) in canonical order."""
+    if small_threshold is None:
+        small_threshold = avg_size
+    ptr, n, keep = _buf(data)
+    fo = np.ascontiguousarray(file_off, dtype=np.uint64)
+    fl = np.ascontiguousarray(file_len, dtype=np.uint64)
+    cap = int(sum(int(x) // min_size + 2 for x in fl)) + 1
+    out = (OrcBlob * cap)()
+    cnt = ctypes.c_size_t()
+    rc = lib().orc_process_files(ptr, _u64p(fo), _u64p(fl), len(fo), min_size, avg_size, max_size,
+                                 small_threshold, index.h if index else None, threads, out, cap,
+                                 ctypes.byref(cnt))
+    if rc:
+        raise RuntimeError("orc_process_files rc=%d" % rc)
+    arr = np.frombuffer(out, dtype=BLOB_DTYPE, count=cnt.value).copy()
+    return arr
+
+
+BLOB_DTYPE = np.dtype([("file", "<u8"), ("offset", "<u8"), ("length", "<u8"),
+                       ("gear_hash", "<u8"), ("digest", "u1", (32,)), ("is_dup", "u1"),
+                       ("pad", "u1", (7,))])
+assert BLOB_DTYPE.itemsize == ctypes.sizeof(OrcBlob) == 72

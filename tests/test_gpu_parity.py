@@ -1,0 +1,223 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit for bit.
+
+Integer/byte work only, so every comparison is exact.  Inputs are seeded; sizes stay where the
+oracle finishes in seconds.  Edge cases follow SURVEY.md §4 item 4: odd tails, lengths at
+min/avg/max +-1, all-zero data (every chunk = max), byte-shifted copies, empty inputs.
+"""
+import numpy as np
+import pytest
+
+from backuwup_amd import make_params
+from backuwup_amd._lib import BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE, BwError
+from backuwup_amd.synth import splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+BK = (262144, 1048576, 3145728)  # backuwup: defaults.rs:61-68
+SMALL = (64, 256, 1024)           # tiny sizes: thousands of chunks in a few MiB
+MID = (4096, 16384, 65536)
+
+
+def chunks_oracle(oracle, data, p):
+    return oracle.fastcdc(data, *p)
+
+
+# ------------------------------------------------------------------ BLAKE3
+
+KAT = {
+    b"": "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262",
+    b"abc": "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85",
+    b"\x00": "2d3adedff11b61f14c886e35afa036736dcd87a74d27b5c1510225d0f592e213",
+}
+
+
+def test_blake3_kat(ctx):
+    for msg, hexd in KAT.items():
+        assert ctx.blake3(msg).hex() == hexd
+
+
+# the official test-vector lengths (input byte i = i % 251) plus the tree-shape edges
+TV_LENS = [0, 1, 63, 64, 65, 127, 128, 1023, 1024, 1025, 2048, 2049, 3072, 3073, 4096, 4097, 5120, 5121,
+           6144, 6145, 7168, 7169, 8192, 8193, 16384, 31744, 102400, 12288, 12289, 65536, 65537, 1048575,
+           1048576, 1048577, 3145728]
+
+
+def test_blake3_lengths(ctx, oracle):
+    for n in TV_LENS:
+        msg = (np.arange(n) % 251).astype(np.uint8)
+        assert ctx.blake3(msg) == oracle.blake3(msg), n
+
+
+def test_blake3_many_unaligned(ctx, oracle):
+    rng = np.random.default_rng(7)
+    data = splitmix_bytes(11, 6 << 20)
+    n = 400
+    lens = rng.integers(0, 70000, n)
+    lens[:40] = rng.integers(0, 9000, 40)
+    offs = np.array([rng.integers(0, data.size - l) for l in lens], dtype=np.uint64)
+    got = ctx.blake3_many(data, offs, lens)
+    for i in range(n):
+        o, l = int(offs[i]), int(lens[i])
+        assert bytes(got[i]) == oracle.blake3(data[o:o + l]), (o, l)
+
+
+def test_blake3_message_at_buffer_end(ctx, oracle):
+    # last message ends exactly at the caller's buffer end (bounds-safe tail loads)
+    for n in [1, 3, 67, 1021, 4099, 70001]:
+        data = splitmix_bytes(n, n + 5)
+        got = ctx.blake3_many(data, [5], [n])
+        assert bytes(got[0]) == oracle.blake3(data[5:]), n
+
+
+# ------------------------------------------------------------------ FastCDC
+
+
+@pytest.mark.parametrize("p", [SMALL, MID])
+def test_fastcdc_random_small_params(ctx, oracle, p):
+    for seed, n in [(1, 100_000), (2, 1_000_003), (3, 4_000_001), (4, p[0]), (5, p[0] + 1), (6, p[1] - 1),
+                    (7, p[1] + 1), (8, p[2] - 1), (9, p[2]), (10, p[2] + 1), (11, 2 * p[2] + 17), (12, 1)]:
+        data = splitmix_bytes(seed, n)
+        assert ctx.fastcdc_chunks(data, *p) == chunks_oracle(oracle, data, p), (seed, n)
+
+
+def test_fastcdc_backuwup_params(ctx, oracle):
+    for seed, n in [(0, 8_400_953), (21, 40 << 20), (22, (17 << 20) + 3), (23, BK[2] + 1), (24, BK[0] + 1),
+                    (25, BK[1] - 1), (26, BK[1] + 1)]:
+        data = splitmix_bytes(seed, n)
+        assert ctx.fastcdc_chunks(data, *BK) == chunks_oracle(oracle, data, BK), (seed, n)
+
+
+def test_fastcdc_a5_vector(ctx):
+    data = splitmix_bytes(0, 8_400_953)
+    lens = [c[2] for c in ctx.fastcdc_chunks(data, *BK)]
+    assert lens == [1560056, 791747, 1444242, 1177622, 806036, 2266142, 355108]
+
+
+def test_fastcdc_zeros_and_patterns(ctx, oracle):
+    cases = [np.zeros((8 << 20) + 5, dtype=np.uint8), np.full(5 << 20, 0xAB, dtype=np.uint8),
+             np.tile(np.arange(256, dtype=np.uint8), 20000), np.tile(splitmix_bytes(3, 4096), 1200)]
+    for data in cases:
+        for p in (BK, SMALL, MID):
+            assert ctx.fastcdc_chunks(data, *p) == chunks_oracle(oracle, data, p)
+    z = ctx.fastcdc_chunks(np.zeros((8 << 20) + 5, dtype=np.uint8), *BK)
+    assert [c[2] for c in z] == [3145728, 3145728, 2097157]
+
+
+def test_fastcdc_odd_params(ctx, oracle):
+    data = splitmix_bytes(44, 3_000_001)
+    for p in [(65, 300, 1100), (1001, 4000, 9999), (64, 256, 1024), (4095, 4096, 4097), (8191, 2048, 4096)]:
+        assert ctx.fastcdc_chunks(data, *p) == chunks_oracle(oracle, data, p), p
+
+
+def test_fastcdc_shifted_copies_resync(ctx, oracle):
+    base = splitmix_bytes(31, 6 << 20)
+    for shift in [1, 7, 63, 4097]:
+        data = np.concatenate([splitmix_bytes(32, shift), base])
+        assert ctx.fastcdc_chunks(data, *MID) == chunks_oracle(oracle, data, MID)
+
+
+def test_fastcdc_empty_and_invalid(ctx):
+    assert ctx.fastcdc_chunks(b"", *BK) == []
+    for bad in [(63, 256, 1024), (64, 255, 1024), (64, 256, 1023), (64, 256, 16777217), (1048577, 4096, 8192)]:
+        with pytest.raises(BwError):
+            ctx.fastcdc_chunks(b"x" * 5000, *bad)
+
+
+def test_serial_resolve_matches_parallel(ctx, oracle):
+    data = splitmix_bytes(77, 12 << 20)
+    for p in (SMALL, MID, BK):
+        par = make_params(*p, small_file_threshold=0, flags=BW_F_NO_DEDUP)
+        ser = make_params(*p, small_file_threshold=0, flags=BW_F_NO_DEDUP | BW_F_SERIAL_RESOLVE)
+        a = ctx.process_files(data, [0], [data.size], par)
+        b = ctx.process_files(data, [0], [data.size], ser)
+        assert np.array_equal(a, b)
+        assert [(int(x["gear_hash"]), int(x["offset"]), int(x["length"])) for x in a] == \
+            chunks_oracle(oracle, data, p)
+
+
+# ------------------------------------------------------------------ whole front end
+
+
+def blobs_equal(a, b):
+    assert a.shape == b.shape, (a.shape, b.shape)
+    for f in ("file", "offset", "length", "gear_hash", "is_dup"):
+        assert np.array_equal(a[f], b[f]), f
+    assert np.array_equal(a["digest"], b["digest"])
+
+
+def test_process_files_mixed(ctx, oracle):
+    from backuwup_amd.synth import tree_corpus
+    data, offs, lens = tree_corpus(48 << 20, seed=5, max_file=12 << 20)
+    lens[3] = 0  # an empty file is one empty blob
+    ctx.index_reset()
+    got = ctx.process_files(data, offs, lens)
+    want = oracle.process_files(data, offs, lens)
+    blobs_equal(got, want)
+    assert got["is_dup"].sum() > 0
+
+
+def test_process_files_small_params_many_files(ctx, oracle):
+    rng = np.random.default_rng(9)
+    lens = rng.integers(0, 300_000, 120).astype(np.uint64)
+    data = splitmix_bytes(90, int(lens.sum()) + 100)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    ctx.index_reset()
+    got = ctx.process_files(data, offs, lens, make_params(*SMALL))
+    want = oracle.process_files(data, offs, lens, *SMALL)
+    blobs_equal(got, want)
+
+
+def test_dedup_seeded_and_cross_batch(ctx, oracle):
+    from backuwup_amd.synth import small_files
+    data, offs, lens = small_files(3000, seed=4)
+    seed_digests = np.array(sorted(oracle.blake3(data[int(offs[i]):int(offs[i] + lens[i])]) for i in range(0, 3000, 7)))
+    seed_arr = np.frombuffer(b"".join(seed_digests), dtype=np.uint8).reshape(-1, 32)
+    ctx.index_reset()
+    ctx.index_seed(seed_arr)
+    half = 1500
+    got1 = ctx.process_files(data, offs[:half], lens[:half])
+    got2 = ctx.process_files(data, offs[half:], lens[half:])
+    ix = oracle.Index(b"".join(seed_digests))
+    want = oracle.process_files(data, offs, lens, index=ix)
+    assert np.array_equal(np.concatenate([got1["is_dup"], got2["is_dup"]]), want["is_dup"])
+    assert ctx.index_size() == len(set(bytes(d) for d in want["digest"]) | set(seed_digests))
+
+
+def test_index_check_insert_random(ctx, oracle):
+    rng = np.random.default_rng(3)
+    pool = rng.integers(0, 256, (5000, 32), dtype=np.uint8)
+    seq = pool[rng.integers(0, 5000, 20000)]
+    ctx.index_reset()
+    got = ctx.index_check_insert(seq)
+    ix = oracle.Index()
+    want = []
+    for d in seq:
+        dup = ix.is_blob_duplicate(d.tobytes())
+        if not dup:
+            ix.insert(d.tobytes())
+        want.append(int(dup))
+    assert got.tolist() == want
+    assert ctx.index_size() == len({d.tobytes() for d in seq})
+
+
+def test_index_growth(ctx):
+    rng = np.random.default_rng(5)
+    ctx.index_reset(16)
+    a = rng.integers(0, 256, (200_000, 32), dtype=np.uint8)
+    assert ctx.index_check_insert(a).sum() == 0
+    assert ctx.index_check_insert(a[::3]).all()
+    assert ctx.index_size() == 200_000
+
+
+def test_device_resident_batch(ctx, oracle):
+    import torch
+    from backuwup_amd.synth import splitmix_torch
+    n = (64 << 20) + 12345
+    t = splitmix_torch(123, n, "cuda")
+    torch.cuda.synchronize()
+    ctx.index_reset()
+    ctx.submit_device(t.data_ptr(), n, [0, 1000, 20 << 20], [1000, (20 << 20) - 1000, n - (20 << 20)])
+    got = ctx.results()
+    host = t.cpu().numpy()
+    want = oracle.process_files(host, [0, 1000, 20 << 20], [1000, (20 << 20) - 1000, n - (20 << 20)])
+    blobs_equal(got, want)
