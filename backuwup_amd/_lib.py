@@ -60,7 +60,13 @@ SIGNATURES = [
     ("bw_partition_by_owner", ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, u64p]),
     ("bw_index_check_insert_device", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),
     ("bw_scatter_verdicts", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, vp]),
+    ("bw_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
+    ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
 ]
+
+STAGES = ["scan", "compact", "resolve", "assemble", "b3_leaf", "b3_tree", "dedup", "pack"]
+# the kernel each stage's events bracket (names as rocprofv3 reports them)
+STAGE_KERNELS = {"scan": "k_scan", "b3_leaf": "k_b3_groups", "b3_tree": "k_b3_tree"}
 
 _lib = None
 

@@ -71,7 +71,7 @@ class Context:
     # -------------------------------------------------------------- chunk / hash
     def fastcdc_chunks(self, data, min_size, avg_size, max_size):
         buf = _as_u8(data)
-        cap = buf.size // max(min_size, 1) + 2
+        cap = buf.size // max(min(2 * (min_size // 2), max_size), 1) + 2
         out = (_lib.BwChunk * cap)()
         n = ctypes.c_uint64()
         check(self._L.bw_fastcdc_chunks(self.h, _ptr(buf), buf.size, min_size, avg_size, max_size, out, cap,
@@ -122,7 +122,8 @@ class Context:
         fo = np.ascontiguousarray(file_off, dtype=np.uint64)
         fl = np.ascontiguousarray(file_len, dtype=np.uint64)
         p = params or make_params()
-        cap = int(sum(int(x) // max(p.min_size - 1, 1) + 2 for x in fl)) + 1
+        mc = max(min(2 * (p.min_size // 2), p.max_size), 1)
+        cap = int(sum(int(x) // mc + 2 for x in fl)) + 1
         out = np.zeros(cap, dtype=BLOB_DTYPE)
         n = ctypes.c_uint64()
         check(self._L.bw_process_files(self.h, _ptr(buf), buf.size, fo.ctypes.data_as(_lib.u64p),
@@ -156,6 +157,17 @@ class Context:
         d, dup = ctypes.c_void_p(), ctypes.c_void_p()
         check(self._L.bw_batch_device_views(self.h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(dup)), self.h)
         return n.value, d.value, dup.value
+
+    # -------------------------------------------------------------- stage timing
+    def profile_enable(self, on=True):
+        check(self._L.bw_profile_enable(self.h, 1 if on else 0), self.h)
+
+    def profile_read(self):
+        """{stage: summed ms}, n_batches -- HIP events on the context stream."""
+        ms = (ctypes.c_double * len(_lib.STAGES))()
+        n = ctypes.c_uint64()
+        check(self._L.bw_profile_read(self.h, ms, ctypes.byref(n)), self.h)
+        return {s: ms[i] for i, s in enumerate(_lib.STAGES)}, n.value
 
     # -------------------------------------------------------------- multi-GPU helpers (device pointers)
     def partition_by_owner(self, d_digests, n, n_owners, d_out, d_perm):

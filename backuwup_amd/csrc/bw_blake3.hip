@@ -170,10 +170,11 @@ __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays
 }
 
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
-                   uint64_t max_groups, uint32_t* cv_buf, uint8_t* digests, int max_leaves) {
+                   uint64_t max_groups, uint32_t* cv_buf, uint8_t* digests, int max_leaves, hipEvent_t between) {
     if (!max_blobs) return;
     hipLaunchKernelGGL(k_b3_groups, dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data, ctr, b,
                        cv_buf, digests);
+    if (between) hipEventRecord(between, st);
     if (max_leaves > 4) {
         const size_t lds = (size_t)((max_leaves / 4) / 2 + 1) * 32;
         hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)max_blobs), dim3(256), lds, st, ctr, b, cv_buf, digests);

@@ -50,6 +50,14 @@ struct bw_ctx {
     DevBuf table, log, dstate;
     uint64_t table_cap = 0, log_cap = 0, log_hi = 0;  // log_hi: host upper bound of log length
 
+    // stage timing: two event sets, alternated per batch so recording never waits on the GPU
+    bool prof = false;
+    hipEvent_t ev[2][BW_N_STAGES + 1] = {};
+    bool ev_pending[2] = {false, false};
+    int ev_set = 0;
+    double stage_ms[BW_N_STAGES] = {};
+    uint64_t prof_batches = 0;
+
     // last batch (kept so a batch whose candidate array overflowed can be re-run exactly)
     uint64_t cand_override = 0;
     const uint8_t* last_data = nullptr;
@@ -133,10 +141,27 @@ static uint64_t seg_len_for(const Masks& mk) {
     // Segments are a multiple of max_size so that chains through data without candidates
     // (e.g. zeros: every chunk is exactly max) stay phase-aligned and merge immediately; the
     // multiple keeps a segment's own cuts within CHAIN_CAP / 2.
-    uint64_t k = (uint64_t)(CHAIN_CAP / 2) * mk.s0 / mk.max;
+    uint64_t k = (uint64_t)(CHAIN_CAP / 2) * std::min<uint64_t>(mk.s0, mk.max) / mk.max;
     if (k < 1) k = 1;
     if (k > 8) k = 8;
     return k * mk.max;
+}
+
+// ------------------------------------------------------------------ stage timing
+
+static void prof_collect(bw_ctx* c, int set) {
+    if (!c->ev_pending[set]) return;
+    hipEventSynchronize(c->ev[set][BW_N_STAGES]);
+    for (int i = 0; i < BW_N_STAGES; i++) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, c->ev[set][i], c->ev[set][i + 1]) == hipSuccess) c->stage_ms[i] += ms;
+    }
+    c->prof_batches++;
+    c->ev_pending[set] = false;
+}
+
+static void prof_mark(bw_ctx* c, int stage) {
+    if (c->prof) hipEventRecord(c->ev[c->ev_set][stage], c->stream);
 }
 
 // ------------------------------------------------------------------ C ABI: basics
@@ -196,6 +221,9 @@ extern "C" void bw_destroy(bw_ctx* c) {
         if (b->p) hipFree(b->p);
     if (c->stage.p) hipHostFree(c->stage.p);
     if (c->meta_done) hipEventDestroy(c->meta_done);
+    for (int k = 0; k < 2; k++)
+        for (int i = 0; i <= BW_N_STAGES; i++)
+            if (c->ev[k][i]) hipEventDestroy(c->ev[k][i]);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
 }
@@ -349,6 +377,8 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
 
     // ---- host metadata: CDC files, segments, canonical units
     const uint64_t L = seg_len_for(mk);
+    // every chunk but a file's last is >= min(2*(min/2), max) bytes (max < min is legal in the crate)
+    const uint64_t min_chunk = std::min<uint64_t>(mk.s0, mk.max);
     std::vector<SegDesc> segs;
     std::vector<CFileDesc> cfs;
     std::vector<UnitDesc> units;
@@ -381,7 +411,7 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
                 units.push_back(u);
                 segs.push_back(sd);
             }
-            const uint64_t nb = flen[f] / mk.s0 + 2;
+            const uint64_t nb = flen[f] / min_chunk + 2;
             fb_total += nb;
             max_blobs += nb;
             cfs.push_back(cf);
@@ -464,6 +494,11 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     c->meta_pending = true;
     HIPCHK(c, hipMemsetAsync(c->ctr.p, 0, C_COUNT * 8, c->stream));
 
+    if (c->prof) {
+        c->ev_set ^= 1;
+        prof_collect(c, c->ev_set);  // the set about to be reused belongs to batch k-2
+    }
+    prof_mark(c, BW_STAGE_SCAN);
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash)};
     uint64_t* ctr = P<uint64_t>(c->ctr);
@@ -472,8 +507,10 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     // ---- chunking
     if (ncf) {
         launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots));
+        prof_mark(c, BW_STAGE_COMPACT);
         launch_compact(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
                        P<uint64_t>(c->tile_off), P<uint64_t>(c->cand), cand_cap, P<uint32_t>(c->ovf), ctr);
+        prof_mark(c, BW_STAGE_RESOLVE);
         launch_chains(st, d_data, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs), nseg,
                       P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->chain_cptr),
                       P<uint64_t>(c->merge), force_serial);
@@ -481,7 +518,11 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
                        P<CFileDesc>(c->cfiles), ncf, P<uint64_t>(c->chains), P<uint32_t>(c->chain_n),
                        P<uint64_t>(c->merge), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
                        P<uint32_t>(c->cf_invalid), P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), force_serial);
+    } else {
+        prof_mark(c, BW_STAGE_COMPACT);
+        prof_mark(c, BW_STAGE_RESOLVE);
     }
+    prof_mark(c, BW_STAGE_ASSEMBLE);
     launch_assemble(st, ctr, P<UnitDesc>(c->units), nunits, P<SegDesc>(c->segs), P<CFileDesc>(c->cfiles),
                     P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
                     P<uint32_t>(c->cf_invalid), P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), b, max_blobs);
@@ -489,18 +530,24 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, st));
 
     // ---- hashing + dedup
+    prof_mark(c, BW_STAGE_B3LEAF);
     if (do_hash) {
         launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint8_t>(c->digests),
-                      max_leaves);
+                      max_leaves, c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : nullptr);
     } else {
+        prof_mark(c, BW_STAGE_B3TREE);
         HIPCHK(c, hipMemsetAsync(c->digests.p, 0, max_blobs * 32, st));
     }
+    prof_mark(c, BW_STAGE_DEDUP);
     if (do_dedup) {
         if (int r4 = dedup_device(c, P<uint8_t>(c->digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(c->is_dup)))
             return r4;
     }
+    prof_mark(c, BW_STAGE_PACK);
     launch_pack(st, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(c->digests), do_dedup ? P<uint8_t>(c->is_dup) : nullptr,
                 P<uint8_t>(c->packed), max_blobs);
+    prof_mark(c, BW_N_STAGES);
+    if (c->prof) c->ev_pending[c->ev_set] = true;
     HIPCHK(c, hipGetLastError());
     c->pending = true;
     c->last_data = d_data;
@@ -591,7 +638,7 @@ extern "C" int bw_fastcdc_chunks(bw_ctx* c, const uint8_t* src, uint64_t len, ui
     p.flags = BW_F_NO_HASH;
     p.small_file_threshold = 0;
     const uint64_t off = 0;
-    std::vector<bw_blob> tmp(len / mk.s0 + 2);
+    std::vector<bw_blob> tmp(len / std::min<uint64_t>(mk.s0, mk.max) + 2);
     uint64_t n = 0;
     if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
     *n_out = n;
@@ -646,5 +693,32 @@ extern "C" int bw_scatter_verdicts(bw_ctx* c, const uint8_t* d_verdict, const ui
     hipSetDevice(c->device);
     launch_scatter(c->stream, d_verdict, d_perm, n, d_is_dup);
     HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+// ------------------------------------------------------------------ stage timing API
+
+extern "C" int bw_profile_enable(bw_ctx* c, int on) {
+    if (!c) return BW_EINVAL;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (int k = 0; k < 2; k++) {
+        c->ev_pending[k] = false;
+        for (int i = 0; i <= BW_N_STAGES; i++)
+            if (!c->ev[k][i]) HIPCHK(c, hipEventCreate(&c->ev[k][i]));
+    }
+    c->prof = on != 0;
+    for (int i = 0; i < BW_N_STAGES; i++) c->stage_ms[i] = 0;
+    c->prof_batches = 0;
+    return BW_OK;
+}
+
+extern "C" int bw_profile_read(bw_ctx* c, double* stage_ms, uint64_t* n_batches) {
+    if (!c) return BW_EINVAL;
+    prof_collect(c, 0);
+    prof_collect(c, 1);
+    if (stage_ms)
+        for (int i = 0; i < BW_N_STAGES; i++) stage_ms[i] = c->stage_ms[i];
+    if (n_batches) *n_batches = c->prof_batches;
     return BW_OK;
 }

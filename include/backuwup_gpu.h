@@ -162,6 +162,22 @@ int bw_index_check_insert_device(bw_ctx* ctx, const uint8_t* d_digests, uint64_t
 int bw_scatter_verdicts(bw_ctx* ctx, const uint8_t* d_verdict, const uint64_t* d_perm,
                         uint64_t n, uint8_t* d_is_dup);
 
+/* ---- stage timing (HIP events on the context stream, accumulated over profiled batches) ---- */
+enum {
+    BW_STAGE_SCAN = 0,     /* gear candidate scan (k_scan)                                 */
+    BW_STAGE_COMPACT = 1,  /* candidate compaction                                          */
+    BW_STAGE_RESOLVE = 2,  /* speculative chains + merge resolution + serial walker         */
+    BW_STAGE_ASSEMBLE = 3, /* blob table + Chunk.hash                                       */
+    BW_STAGE_B3LEAF = 4,   /* BLAKE3 4-leaf groups (k_b3_groups)                            */
+    BW_STAGE_B3TREE = 5,   /* BLAKE3 upper tree levels (k_b3_tree)                          */
+    BW_STAGE_DEDUP = 6,    /* index append/claim/verdict                                    */
+    BW_STAGE_PACK = 7,     /* result records                                                */
+    BW_N_STAGES = 8
+};
+int bw_profile_enable(bw_ctx* ctx, int on); /* also clears the accumulators */
+/* stage_ms[BW_N_STAGES] = summed milliseconds; *n_batches = batches accumulated.  Syncs. */
+int bw_profile_read(bw_ctx* ctx, double* stage_ms, uint64_t* n_batches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -389,7 +389,8 @@ static int process_one_file(orc_job* j, size_t f) {
     const uint8_t* src = j->data + j->foff[f];
     size_t len = j->flen[f];
     if ((uint64_t)len > j->small) {  /* dir_packer.rs:246: len > BLOB_DESIRED_TARGET_SIZE */
-        size_t cap = len / j->min + 2, n = 0;
+        size_t mc = 2 * (j->min / 2) < j->max ? 2 * (j->min / 2) : j->max;
+        size_t cap = len / mc + 2, n = 0;
         uint64_t* h = (uint64_t*)malloc(cap * 8 * 3);
         if (!h) return -4;
         if (orc_fastcdc_chunks(src, len, j->min, j->avg, j->max, h, h + cap, h + 2 * cap, cap, &n)) {

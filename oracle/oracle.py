@@ -82,7 +82,7 @@ def masks(min_size, avg_size, max_size):
 def fastcdc(data, min_size, avg_size, max_size):
     """FastCDC::new(data, min, avg, max).collect() -> list of (hash, offset, length)."""
     ptr, n, keep = _buf(data)
-    cap = n // max(min_size, 1) + 2
+    cap = n // max(min(2 * (min_size // 2), max_size), 1) + 2
     h, o, l = (np.zeros(cap, dtype=np.uint64) for _ in range(3))
     cnt = ctypes.c_size_t()
     rc = lib().orc_fastcdc_chunks(ptr, n, min_size, avg_size, max_size, _u64p(h), _u64p(o),
@@ -129,7 +129,7 @@ def process_files(data, file_off, file_len, min_size=262144, avg_size=1048576,
     ptr, n, keep = _buf(data)
     fo = np.ascontiguousarray(file_off, dtype=np.uint64)
     fl = np.ascontiguousarray(file_len, dtype=np.uint64)
-    cap = int(sum(int(x) // min_size + 2 for x in fl)) + 1
+    cap = int(sum(int(x) // max(min(2 * (min_size // 2), max_size), 1) + 2 for x in fl)) + 1
     out = (OrcBlob * cap)()
     cnt = ctypes.c_size_t()
     rc = lib().orc_process_files(ptr, _u64p(fo), _u64p(fl), len(fo), min_size, avg_size, max_size,

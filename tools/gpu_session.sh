@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel trace.  Each GPU step runs under
+# its own time limit and the chain stops at the first failure.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT="$GRAFT_REPO_ROOT/gpurun_out"
+mkdir -p "$OUT"
+MODE="${1:-all}"
+run() { local name=$1 t=$2; shift 2; echo "== $name" >&2; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc" | tee -a "$OUT/summary.txt"; return $rc; }
+: > "$OUT/summary.txt"
+if [[ "$MODE" == *tests* || "$MODE" == all ]]; then
+  run pytest_gpu 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider || exit 1
+fi
+if [[ "$MODE" == *smoke* || "$MODE" == all ]]; then
+  run smoke 300 python __graft_entry__.py || exit 1
+fi
+if [[ "$MODE" == *bench* || "$MODE" == all ]]; then
+  run bench 600 python bench.py || exit 1
+fi
+if [[ "$MODE" == *prof* || "$MODE" == all ]]; then
+  cd /tmp && export TMPDIR=/tmp
+  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-check || exit 1
+fi
