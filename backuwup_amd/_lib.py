@@ -7,7 +7,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbackuwup_amd.so")
+LIB_PATH = os.environ.get("BW_LIB") or os.path.join(HERE, "libbackuwup_amd.so")
 
 BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -1, -2, -3, -4, -5, -6
 BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4

@@ -23,6 +23,18 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Chaining value of one leaf (<= 1024 bytes at global position `ls`), chunk counter `t`.
 // `bend` is the end of the blob: loads never touch bytes at or beyond it except through the
 // byte-exact tail path, so a blob at the very end of the caller's buffer is safe.
+__device__ __forceinline__ void load_words(const uint32_t* wb, uint32_t blk, uint32_t w[17]) {
+    const u32x4_a4* q = (const u32x4_a4*)(wb + blk * 16);
+    const u32x4_a4 a = q[0], b = q[1], c = q[2], d = q[3];
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w; w[12] = d.x; w[13] = d.y; w[14] = d.z; w[15] = d.w;
+    w[16] = wb[blk * 16 + 16];
+}
+
+// Chaining value of one leaf (<= 1024 bytes at global position `ls`), chunk counter `t`.
+// `bend` is the end of the blob: the 16-byte loads never touch bytes at or beyond it (a block
+// within 68 bytes of the end goes through the byte-exact path), so a blob at the very end of
+// the caller's buffer is safe.  Block b+1 is loaded before block b is compressed.
 __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64_t ls, uint32_t ll, uint64_t bend,
                                         uint64_t t, uint32_t root, uint32_t cv[8]) {
     b3_iv(cv);
@@ -30,15 +42,13 @@ __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64
     const uint8_t* base = data + ls;
     const uint32_t sh = (uint32_t)((uintptr_t)base & 3);
     const uint32_t* wb = (const uint32_t*)(base - sh);
+    uint32_t w[17];
+    if (ls + 68 <= bend) load_words(wb, 0, w);
     for (uint32_t blk = 0; blk < nblk; blk++) {
         uint32_t m[16];
         const uint32_t left = ll - blk * 64;
         const uint32_t blen = ll == 0 ? 0 : (left < 64 ? left : 64);
         if (ls + blk * 64 + 68 <= bend) {
-            const u32x4_a4* q = (const u32x4_a4*)(wb + blk * 16);
-            const u32x4_a4 a = q[0], b = q[1], c = q[2], d = q[3];
-            const uint32_t e = wb[blk * 16 + 16];
-            const uint32_t w[17] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e};
 #pragma unroll
             for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
         } else {
@@ -52,6 +62,7 @@ __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64
                 m[i] = v;
             }
         }
+        if (blk + 1 < nblk && ls + (blk + 1) * 64 + 68 <= bend) load_words(wb, blk + 1, w);
         uint32_t flags = 0;
         if (blk == 0) flags |= B3_CHUNK_START;
         if (blk == nblk - 1) flags |= B3_CHUNK_END | root;
@@ -83,26 +94,43 @@ __global__ __launch_bounds__(256) void k_b3_groups(const uint8_t* __restrict__ d
     const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
     const uint64_t first = gi * 4;
     const uint32_t k = (uint32_t)(n - first < 4 ? n - first : 4);
-    uint32_t acc[8], sv[8], cv[8];
+    // Pending subtree nodes wait in LDS (word-major, conflict-free) instead of registers, so the
+    // leaf loop keeps its VGPRs for the prefetched block.
+    __shared__ uint32_t s_acc[8][256], s_sv[8][256];
+    const int me = threadIdx.x;
+    uint32_t cv[8];
     for (uint32_t t = 0; t < k; t++) {
         const uint64_t li = first + t, ls = start + li * B3_LEAF_BYTES;
         const uint64_t rest = len - li * B3_LEAF_BYTES;
         const uint32_t ll = len == 0 ? 0 : (uint32_t)(rest < B3_LEAF_BYTES ? rest : B3_LEAF_BYTES);
         b3_leaf(data, ls, ll, bend, li, n == 1 ? B3_ROOT : 0, cv);
-        if (t == 0) {
+        if (t == 0 || t == 2) {
+            uint32_t (*dst)[256] = t == 0 ? s_acc : s_sv;
 #pragma unroll
-            for (int i = 0; i < 8; i++) acc[i] = cv[i];
-        } else if (t == 1) {
-            b3_parent(acc, cv, n == 2 ? B3_ROOT : 0, acc);
-        } else if (t == 2) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) sv[i] = cv[i];
+            for (int i = 0; i < 8; i++) dst[i][me] = cv[i];
         } else {
-            b3_parent(sv, cv, 0, sv);
-            b3_parent(acc, sv, n == 4 ? B3_ROOT : 0, acc);
+            uint32_t l[8];
+            if (t == 3) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) l[i] = s_sv[i][me];
+                b3_parent(l, cv, 0, cv);  // P(leaf2, leaf3)
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) l[i] = s_acc[i][me];
+            b3_parent(l, cv, (n == 2 && t == 1) || (n == 4 && t == 3) ? B3_ROOT : 0, cv);
+#pragma unroll
+            for (int i = 0; i < 8; i++) s_acc[i][me] = cv[i];
         }
     }
-    if (k == 3) b3_parent(acc, sv, n == 3 ? B3_ROOT : 0, acc);
+    uint32_t acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc[i] = s_acc[i][me];
+    if (k == 3) {
+        uint32_t r[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) r[i] = s_sv[i][me];
+        b3_parent(acc, r, n == 3 ? B3_ROOT : 0, acc);
+    }
     if (n <= 4) store_digest(digests + blob * 32, acc);
     else {
         uint32_t* o = cv_buf + g * 8;
@@ -117,56 +145,58 @@ __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays
                                                  const uint32_t* __restrict__ cv_buf,
                                                  uint8_t* __restrict__ digests) {
     extern __shared__ __attribute__((aligned(16))) uint32_t nodes[];  // [cap][8]
-    const uint64_t blob = blockIdx.x;
-    if (blob >= ctr[C_NBLOBS]) return;
-    const uint64_t len = b.len[blob];
-    const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
-    if (n <= 4) return;
-    const uint32_t* lvl2 = cv_buf + b.goff[blob] * 8;
-    uint64_t cnt = n / 4;
-    uint32_t acc[8];
-    bool have = false;
-    if (threadIdx.x == 0 && (n & 3)) {
+    const uint64_t nblobs = ctr[C_NBLOBS];
+    for (uint64_t blob = blockIdx.x; blob < nblobs; blob += gridDim.x) {  // persistent over blobs
+        const uint64_t len = b.len[blob];
+        const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
+        if (n <= 4) continue;
+        const uint32_t* lvl2 = cv_buf + b.goff[blob] * 8;
+        uint64_t cnt = n / 4;
+        uint32_t acc[8];
+        bool have = false;
+        if (threadIdx.x == 0 && (n & 3)) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) acc[i] = lvl2[cnt * 8 + i];
-        have = true;
-    }
-    const uint32_t* src = lvl2;
-    for (int l = 2;; l++) {
-        if (threadIdx.x == 0 && ((n >> l) & 1)) {
-            uint32_t T[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) T[i] = src[(cnt - 1) * 8 + i];
-            if (!have) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] = T[i];
-                have = true;
-            } else {
-                b3_parent(T, acc, (n >> (l + 1)) == 0 ? B3_ROOT : 0, acc);
-            }
+            for (int i = 0; i < 8; i++) acc[i] = lvl2[cnt * 8 + i];
+            have = true;
         }
-        const uint64_t next = cnt / 2;
-        if (next == 0) break;
-        const uint32_t root = (n == (1ull << (l + 1))) ? B3_ROOT : 0;
-        for (uint64_t c0 = 0; c0 < next; c0 += blockDim.x) {
-            const uint64_t i = c0 + threadIdx.x;
-            uint32_t L[8], R[8], P[8];
-            if (i < next) {
+        const uint32_t* src = lvl2;
+        for (int l = 2;; l++) {
+            if (threadIdx.x == 0 && ((n >> l) & 1)) {
+                uint32_t T[8];
 #pragma unroll
-                for (int w = 0; w < 8; w++) { L[w] = src[(2 * i) * 8 + w]; R[w] = src[(2 * i + 1) * 8 + w]; }
-            }
-            __syncthreads();
-            if (i < next) {
-                b3_parent(L, R, root, P);
+                for (int i = 0; i < 8; i++) T[i] = src[(cnt - 1) * 8 + i];
+                if (!have) {
 #pragma unroll
-                for (int w = 0; w < 8; w++) nodes[i * 8 + w] = P[w];
+                    for (int i = 0; i < 8; i++) acc[i] = T[i];
+                    have = true;
+                } else {
+                    b3_parent(T, acc, (n >> (l + 1)) == 0 ? B3_ROOT : 0, acc);
+                }
             }
-            __syncthreads();
+            const uint64_t next = cnt / 2;
+            if (next == 0) break;
+            const uint32_t root = (n == (1ull << (l + 1))) ? B3_ROOT : 0;
+            for (uint64_t c0 = 0; c0 < next; c0 += blockDim.x) {
+                const uint64_t i = c0 + threadIdx.x;
+                uint32_t L[8], R[8], P[8];
+                if (i < next) {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) { L[w] = src[(2 * i) * 8 + w]; R[w] = src[(2 * i + 1) * 8 + w]; }
+                }
+                __syncthreads();
+                if (i < next) {
+                    b3_parent(L, R, root, P);
+#pragma unroll
+                    for (int w = 0; w < 8; w++) nodes[i * 8 + w] = P[w];
+                }
+                __syncthreads();
+            }
+            src = nodes;
+            cnt = next;
         }
-        src = nodes;
-        cnt = next;
+        if (threadIdx.x == 0) store_digest(digests + blob * 32, acc);
+        __syncthreads();  // the next blob reuses `nodes`
     }
-    if (threadIdx.x == 0) store_digest(digests + blob * 32, acc);
 }
 
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
@@ -177,7 +207,8 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     if (between) hipEventRecord(between, st);
     if (max_leaves > 4) {
         const size_t lds = (size_t)((max_leaves / 4) / 2 + 1) * 32;
-        hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)max_blobs), dim3(256), lds, st, ctr, b, cv_buf, digests);
+        const uint64_t grid = max_blobs < 2048 ? max_blobs : 2048;
+        hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)grid), dim3(256), lds, st, ctr, b, cv_buf, digests);
     }
 }
 

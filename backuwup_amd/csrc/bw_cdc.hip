@@ -99,11 +99,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_scan(const uint8_t* __restr
                 }
             }
             uint64_t p = ss;
-            for (; p + 128 <= se; p += 128) {
-                const uint4* wp = (const uint4*)(data + p);
-                uint4 w[8];
+            uint4 w[8];
+            if (p + 128 <= se) {
 #pragma unroll
-                for (int i = 0; i < 8; i++) w[i] = wp[i];
+                for (int i = 0; i < 8; i++) w[i] = ((const uint4*)(data + p))[i];
+            }
+            for (; p + 128 <= se; p += 128) {
+                uint4 nx[8];  // next line in flight while this one is hashed
+                const bool more = p + 256 <= se;
+                if (more) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) nx[i] = ((const uint4*)(data + p + 128))[i];
+                }
                 const uint64_t h0 = h;
                 uint32_t acc = 0xffffffffu;
 #pragma unroll
@@ -132,6 +139,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_scan(const uint8_t* __restr
                         hh = (hh << 1) + s_gear[(uint32_t)data[p + i] * GEAR_REP];
                         if (mask_test(hh, mlo, mhi) == 0) record_hit(p + i, hh, mk, s_cnt, s_slots);
                     }
+                }
+                if (more) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) w[i] = nx[i];
                 }
             }
             for (; p < se; p++) {  // ragged end of the buffer only

@@ -1,0 +1,165 @@
+// backuwup.hpp -- C++ host-side mirror of the reference's call sites, over the C ABI.
+//
+// The reference is Rust; there is no Rust toolchain in this image, so the host side of the
+// boundary is written in C++ (the reference is compiled code) with the reference's names,
+// argument meaning and error behaviour.  A Rust maintainer binds the same C ABI instead
+// (INTEGRATION.md).  Header-only; link with -lbackuwup_amd.
+//
+//   fastcdc::v2020::FastCDC / Chunk    client/src/backup/filesystem/dir_packer.rs:254-266
+//   blake3::hash                       dir_packer.rs:286
+//   packfile::BlobIndex                packfile/blob_index.rs:44-148
+//   packfile::Manager::add_blob gate   packfile/pack.rs:31-39
+//   dir_packer::process_file           dir_packer.rs:231-282 (batched over many files)
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/backuwup_gpu.h"
+
+namespace backuwup {
+
+using BlobHash = std::array<uint8_t, 32>;  // shared/src/types.rs:31
+
+struct Error : std::runtime_error {
+    int rc;
+    Error(int r, const std::string& m) : std::runtime_error(m), rc(r) {}
+};
+
+inline void check(int rc, bw_ctx* ctx = nullptr) {
+    if (rc != BW_OK) {
+        std::string m = bw_strerror(rc);
+        if (ctx) m += std::string(": ") + bw_last_error(ctx);
+        throw Error(rc, m);
+    }
+}
+
+// One GPU context: stream, workspaces, the in-HBM index.  Not thread-safe (the reference
+// serialises index access under the packer mutex, packfile/mod.rs:77).
+class Context {
+public:
+    explicit Context(int device = 0) { check(bw_create(device, &h_)); }
+    ~Context() { bw_destroy(h_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    bw_ctx* get() const { return h_; }
+
+private:
+    bw_ctx* h_ = nullptr;
+};
+
+namespace fastcdc {
+namespace v2020 {
+
+constexpr uint32_t MINIMUM_MIN = BW_MINIMUM_MIN, MINIMUM_MAX = BW_MINIMUM_MAX;
+constexpr uint32_t AVERAGE_MIN = BW_AVERAGE_MIN, AVERAGE_MAX = BW_AVERAGE_MAX;
+constexpr uint32_t MAXIMUM_MIN = BW_MAXIMUM_MIN, MAXIMUM_MAX = BW_MAXIMUM_MAX;
+
+struct Chunk {
+    uint64_t hash;
+    size_t offset;
+    size_t length;
+};
+
+// FastCDC::new(source, min_size, avg_size, max_size): the crate panics on out-of-range sizes;
+// here the constructor throws Error(BW_EINVAL).  Iterating yields the chunks in order.
+class FastCDC {
+public:
+    FastCDC(Context& ctx, const uint8_t* source, size_t len, uint32_t min_size, uint32_t avg_size,
+            uint32_t max_size) {
+        const uint32_t s0 = 2 * (min_size / 2);
+        const uint32_t mc = s0 < max_size ? s0 : max_size;
+        std::vector<bw_chunk> out(len / (mc ? mc : 1) + 2);
+        uint64_t n = 0;
+        check(bw_fastcdc_chunks(ctx.get(), source, len, min_size, avg_size, max_size, out.data(), out.size(), &n),
+              ctx.get());
+        chunks_.reserve(n);
+        for (uint64_t i = 0; i < n; i++) chunks_.push_back({out[i].hash, out[i].offset, out[i].length});
+    }
+    std::vector<Chunk>::const_iterator begin() const { return chunks_.begin(); }
+    std::vector<Chunk>::const_iterator end() const { return chunks_.end(); }
+    size_t size() const { return chunks_.size(); }
+
+private:
+    std::vector<Chunk> chunks_;
+};
+
+}  // namespace v2020
+}  // namespace fastcdc
+
+namespace blake3 {
+inline BlobHash hash(Context& ctx, const uint8_t* data, size_t len) {
+    BlobHash h{};
+    check(bw_blake3_hash(ctx.get(), data, len, h.data()), ctx.get());
+    return h;
+}
+}  // namespace blake3
+
+// packfile::blob_index::BlobIndex -- lives in HBM; `load` seeds it with the prior backups'
+// sorted items (blob_index.rs:167-200); `is_blob_duplicate` answers in canonical order and
+// inserts a new blob (the blobs_queued insert of blob_index.rs:109).
+class BlobIndex {
+public:
+    explicit BlobIndex(Context& ctx, uint64_t capacity_hint = 0) : ctx_(ctx) {
+        check(bw_index_reset(ctx.get(), capacity_hint), ctx.get());
+    }
+    void load(const std::vector<BlobHash>& sorted_items) {
+        check(bw_index_seed(ctx_.get(), sorted_items.empty() ? nullptr : sorted_items[0].data(), sorted_items.size()),
+              ctx_.get());
+    }
+    bool is_blob_duplicate(const BlobHash& h) {
+        uint8_t dup = 0;
+        check(bw_index_check_insert(ctx_.get(), h.data(), 1, &dup), ctx_.get());
+        return dup != 0;
+    }
+    std::vector<uint8_t> is_blob_duplicate_many(const std::vector<BlobHash>& hs) {
+        std::vector<uint8_t> dup(hs.size());
+        if (!hs.empty()) check(bw_index_check_insert(ctx_.get(), hs[0].data(), hs.size(), dup.data()), ctx_.get());
+        return dup;
+    }
+    uint64_t size() {
+        uint64_t n = 0;
+        check(bw_index_size(ctx_.get(), &n), ctx_.get());
+        return n;
+    }
+
+private:
+    Context& ctx_;
+};
+
+struct BlobTooLarge : Error {
+    BlobTooLarge() : Error(BW_EINVAL, "Blob too large") {}
+};
+
+// The dedup gate of packfile::Manager::add_blob (pack.rs:31-39): BlobTooLarge above 3 MiB,
+// nullopt-like `false` for a duplicate (Ok(None)), `true` when the blob goes on to be packed.
+inline bool add_blob_gate(BlobIndex& index, const BlobHash& h, size_t len) {
+    if (len > BW_BLOB_MAX_UNCOMPRESSED_SIZE) throw BlobTooLarge();
+    return !index.is_blob_duplicate(h);
+}
+
+// process_file for a batch of files laid out back to back: CDC for files > 1 MiB, one blob per
+// smaller (or empty) file, blake3 per blob, dedup verdict per blob -- canonical order.
+inline std::vector<bw_blob> process_files(Context& ctx, const uint8_t* data, size_t data_len,
+                                          const std::vector<uint64_t>& file_off,
+                                          const std::vector<uint64_t>& file_len, const bw_params* params = nullptr) {
+    bw_params p;
+    if (params) p = *params;
+    else bw_params_default(&p);
+    const uint32_t s0 = 2 * (p.min_size / 2);
+    const uint64_t mc = s0 < p.max_size ? s0 : p.max_size;
+    uint64_t cap = 1;
+    for (uint64_t l : file_len) cap += l / (mc ? mc : 1) + 2;
+    std::vector<bw_blob> out(cap);
+    uint64_t n = 0;
+    check(bw_process_files(ctx.get(), data, data_len, file_off.data(), file_len.data(), file_off.size(), &p,
+                           out.data(), cap, &n),
+          ctx.get());
+    out.resize(n);
+    return out;
+}
+
+}  // namespace backuwup

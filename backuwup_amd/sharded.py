@@ -1,0 +1,66 @@
+"""Multi-GPU dedup: the seen-chunk index partitioned by digest prefix across ranks.
+
+One process per GPU.  Files are sharded rank-major (rank r holds canonical files
+[F_r, F_{r+1})), so (rank, local blob index) order IS the canonical order.  Each step:
+
+  1. every rank chunks + hashes its own files (no collective on the data path);
+  2. its digests are stably partitioned by owner = digest[0] >> (8 - log2 N);
+  3. one all-to-all of the per-owner counts, one all-to-all of the 32-byte digests (RCCL over
+     xGMI on MI355X; ~13.5k digests = 432 KiB per 16 GiB stream, latency-bound);
+  4. each owner decides its slice against its shard of the index -- the received buffer is
+     source-rank-major, i.e. canonical, so first occurrence = first position;
+  5. one all-to-all returns the verdict bytes, scattered back to local blob order.
+
+This replaces the reference's single in-process BlobIndex (blob_index.rs:44-148), whose
+`blobs_queued` HashSet and sorted `items` become the union of the N shards.
+
+The collective sequence is written once against a small ops interface so the same code runs
+on the GPU (DeviceShardOps, backed by libbackuwup_amd.so) and in the world-size-2 gloo tests.
+"""
+import torch
+import torch.distributed as dist
+
+
+def owner_of(first_byte, world):
+    bits = world.bit_length() - 1
+    return first_byte >> (8 - bits) if bits else 0
+
+
+class DeviceShardOps:
+    """GPU implementation of the three local steps (all device-resident)."""
+
+    def __init__(self, ctx, device):
+        self.ctx, self.device = ctx, device
+
+    def partition(self, digests_ptr, n, world):
+        out = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=self.device)
+        perm = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        counts = self.ctx.partition_by_owner(digests_ptr, n, world, out.data_ptr(), perm.data_ptr())
+        return out, perm, [int(c) for c in counts]
+
+    def decide(self, recv, n):
+        verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
+        if n:
+            self.ctx.index_check_insert_device(recv.data_ptr(), n, verdict.data_ptr())
+        return verdict
+
+    def scatter(self, back, perm, n, is_dup_ptr):
+        if n:
+            self.ctx.scatter_verdicts(back.data_ptr(), perm.data_ptr(), n, is_dup_ptr)
+
+
+def exchange_dedup(ops, digests_ptr, n, is_dup_ptr, world, device, group=None):
+    """Steps 2-5 above for one batch; returns (sent per owner, received per source)."""
+    out, perm, sc = ops.partition(digests_ptr, n, world)
+    send_counts = torch.tensor(sc, dtype=torch.int64, device=device)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    rc = [int(x) for x in recv_counts.cpu().tolist()]
+    nr = sum(rc)
+    recv = torch.empty(max(nr, 1) * 32, dtype=torch.uint8, device=device)
+    dist.all_to_all_single(recv[:nr * 32], out[:n * 32], [x * 32 for x in rc], [x * 32 for x in sc], group=group)
+    verdict = ops.decide(recv, nr)
+    back = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+    dist.all_to_all_single(back[:n], verdict[:nr], sc, rc, group=group)
+    ops.scatter(back, perm, n, is_dup_ptr)
+    return sc, rc

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="batches in flight: consecutive steps alternate between this many contexts/streams")
     args = ap.parse_args()
 
     import numpy as np
@@ -62,39 +64,35 @@ def main():
     torch.cuda.synchronize()
     log("rank %d: generated %.1f GiB in %.1f s" % (rank, n / 2**30, time.time() - t0))
 
-    ctx = Context(local)
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)
+    ctxs, streams = [], []
+    for k in range(max(1, args.streams)):
+        c = Context(local)
+        st = torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)
+        c.set_stream(st.cuda_stream)
+        ctxs.append(c)
+        streams.append(st)
+    ctx = ctxs[0]
+    stream = streams[0]
     flags = BW_F_NO_DEDUP if world > 1 else 0
     params = make_params(flags=flags)
     index_hint = 2 * (n // (256 << 10)) + 1024
     owner_bits = world.bit_length() - 1
     assert world == 1 << owner_bits, "world size must be a power of two (digest-prefix owners)"
 
-    def exchange():
-        """Digest all-to-all by owner = digest[0] >> (8 - log2 N); verdicts come back."""
-        nb, d_dig, d_dup = ctx.device_views()
-        out = torch.empty(max(nb, 1) * 32, dtype=torch.uint8, device=dev)
-        perm = torch.empty(max(nb, 1), dtype=torch.int64, device=dev)
-        counts = ctx.partition_by_owner(d_dig, nb, world, out.data_ptr(), perm.data_ptr())
-        send_counts = torch.tensor(counts.astype(np.int64), device=dev)
-        recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts)
-        rc = recv_counts.cpu().tolist()
-        sc = [int(x) for x in counts]
-        recv = torch.empty(max(sum(rc), 1) * 32, dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(recv[:sum(rc) * 32], out[:nb * 32], [x * 32 for x in rc], [x * 32 for x in sc])
-        verdict = torch.empty(max(sum(rc), 1), dtype=torch.uint8, device=dev)
-        ctx.index_check_insert_device(recv.data_ptr(), sum(rc), verdict.data_ptr())
-        back = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(back[:nb], verdict[:sum(rc)], sc, rc)
-        ctx.scatter_verdicts(back.data_ptr(), perm.data_ptr(), nb, d_dup)
+    from backuwup_amd.sharded import DeviceShardOps, exchange_dedup
+    step_no = [0]
 
     def step():
-        ctx.index_reset(index_hint)
-        ctx.submit_device(data.data_ptr(), n, [0], [n], params)
-        if world > 1:
-            exchange()
+        k = step_no[0] % len(ctxs)
+        step_no[0] += 1
+        c = ctxs[k]
+        with torch.cuda.stream(streams[k]):
+            c.index_reset(index_hint)
+            c.submit_device(data.data_ptr(), n, [0], [n], params)
+            if world > 1:
+                # digest all-to-all by owner = digest[0] >> (8 - log2 N); verdicts come back
+                nb, d_dig, d_dup = c.device_views()
+                exchange_dedup(DeviceShardOps(c, dev), d_dig, nb, d_dup, world, dev)
 
     for _ in range(args.warmup):
         step()
@@ -120,7 +118,8 @@ def main():
         if not ok:
             raise SystemExit("parity check failed")
 
-    ctx.profile_enable(True)
+    for c in ctxs:
+        c.profile_enable(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -183,7 +182,8 @@ def main():
                 "config": {"workload": "C2: single %.0f GiB splitmix64 stream per GPU (seed 42+rank), "
                                        "device-resident; FastCDC v2020 256K/1M/3M -> BLAKE3 -> index" % args.gib,
                            "bytes_per_gpu": n, "blobs_per_gpu": int(len(res)),
-                           "parallelism": "dp%d (files sharded, index by digest prefix)" % world},
+                           "parallelism": "dp%d (files sharded, index by digest prefix)" % world,
+                           "batches_in_flight": len(ctxs)},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": check}
         print(json.dumps(line), flush=True)
     if world > 1:

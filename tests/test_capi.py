@@ -1,0 +1,85 @@
+"""The C ABI boundary without a GPU: the library loads, exports every function that
+include/*.h declares, and the ctypes/Python mirrors agree with the C struct layouts."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?(?:int|void|char|uint\w+)\s*\*?\s*(bw_\w+)\s*\(", txt, re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ["bw_fastcdc_chunks", "bw_blake3_hash", "bw_blake3_hash_many", "bw_index_seed",
+                     "bw_index_check_insert", "bw_process_files", "bw_process_files_device", "bw_results",
+                     "bw_partition_by_owner", "bw_index_check_insert_device", "bw_scatter_verdicts"]:
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from backuwup_amd import _lib
+    lib = _lib.load()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert declared_functions() == bound
+
+
+def test_host_only_entry_points():
+    from backuwup_amd import _lib
+    lib = _lib.load()
+    p = _lib.BwParams()
+    lib.bw_params_default(ctypes.byref(p))
+    assert (p.min_size, p.avg_size, p.max_size, p.small_file_threshold) == (262144, 1048576, 3145728, 1048576)
+    assert lib.bw_strerror(-2) == b"output capacity too small"
+    assert lib.bw_create(0, None) == _lib.BW_EINVAL
+
+
+def test_struct_layout_matches_header(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "backuwup_gpu.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(bw_blob), offsetof(bw_blob, digest),'
+                   ' offsetof(bw_blob, is_dup), sizeof(bw_chunk), sizeof(bw_params),'
+                   ' offsetof(bw_params, small_file_threshold)); return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    vals = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    from backuwup_amd import _lib
+    from backuwup_amd.context import BLOB_DTYPE
+    assert vals == [ctypes.sizeof(_lib.BwBlob), _lib.BwBlob.digest.offset, _lib.BwBlob.is_dup.offset,
+                    ctypes.sizeof(_lib.BwChunk), ctypes.sizeof(_lib.BwParams), _lib.BwParams.small_file_threshold.offset]
+    assert BLOB_DTYPE.itemsize == vals[0] and BLOB_DTYPE.fields["digest"][1] == vals[1]
+
+
+def test_oracle_is_not_linked_by_the_product():
+    """The product library must not reference the oracle (it is test infrastructure only)."""
+    from backuwup_amd import _lib
+    out = subprocess.check_output(["nm", "-D", _lib.LIB_PATH]).decode()
+    assert "orc_" not in out
+    for py in glob.glob(os.path.join(ROOT, "backuwup_amd", "*.py")):
+        assert "oracle" not in open(py).read().replace("# oracle", ""), py
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    import importlib
+    from backuwup_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libbackuwup_amd.so")
+    with pytest.raises(RuntimeError):
+        _lib.load()
+    monkeypatch.undo()
+    importlib.reload(_lib)

@@ -1,0 +1,155 @@
+// tools/ablate.hip -- microbenchmarks that take the gear scan and BLAKE3 leaf kernels apart
+// (diagnostic only; not part of the product).  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17
+// -I backuwup_amd/csrc tools/ablate.hip -o build_ab/ablate ; run on an MI355X.
+//
+// For a 4 GiB random buffer it times:
+//   copy_strided   every lane reads its own 2 KiB strip in 128 B lines (the scan's pattern)
+//   copy_coalesced every lane reads 16 B at consecutive addresses (the HBM ceiling)
+//   scan_full      bw::k_scan exactly as shipped
+//   scan_noload    the scan's arithmetic + LDS lookups on register-resident bytes (no HBM)
+//   scan_nolds     the scan with the LDS gear lookup replaced by arithmetic on the byte
+//   b3_noload      BLAKE3 compressions on register data (pure VALU rate)
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "bw_cdc.hip"
+#include "bw_blake3.hip"
+
+using namespace bw;
+
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e = (x);                                                               \
+        if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } \
+    } while (0)
+
+__global__ __launch_bounds__(512) void copy_strided(const uint8_t* __restrict__ data, uint64_t n, uint32_t* out) {
+    uint32_t acc = 0;
+    for (uint64_t tile = blockIdx.x; tile * SCAN_TILE < n; tile += gridDim.x) {
+        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_STRIP;
+        for (uint64_t p = ss; p < ss + SCAN_STRIP; p += 128) {
+            const uint4* wp = (const uint4*)(data + p);
+#pragma unroll
+            for (int i = 0; i < 8; i++) { uint4 w = wp[i]; acc ^= w.x ^ w.y ^ w.z ^ w.w; }
+        }
+    }
+    if (acc == 0x12345678) out[0] = acc;
+}
+
+__global__ __launch_bounds__(512) void copy_coalesced(const uint8_t* __restrict__ data, uint64_t n, uint32_t* out) {
+    uint32_t acc = 0;
+    const uint4* wp = (const uint4*)data;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 16; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 w = wp[i];
+        acc ^= w.x ^ w.y ^ w.z ^ w.w;
+    }
+    if (acc == 0x12345678) out[0] = acc;
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(512, 4) void scan_noload(uint64_t n, Masks mk, uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_REP];
+    for (int i = threadIdx.x; i < 256 * GEAR_REP; i += blockDim.x) s_gear[i] = c_gear[i / GEAR_REP];
+    __syncthreads();
+    const uint32_t lane_off = (threadIdx.x & 31) * 8;
+    const uint32_t mlo = (uint32_t)mk.mask_pre, mhi = (uint32_t)(mk.mask_pre >> 32);
+    uint32_t hits = 0;
+    uint64_t h = 0;
+    uint32_t seed = threadIdx.x * 0x9E3779B9u + blockIdx.x;
+    const uint64_t lines = n / 128 / ((uint64_t)gridDim.x * blockDim.x);
+    for (uint64_t line = 0; line < lines; line++) {
+        uint32_t ww[32];
+#pragma unroll
+        for (int i = 0; i < 32; i++) { seed = seed * 1664525u + 1013904223u; ww[i] = seed; }
+        uint32_t acc = 0xffffffffu;
+#pragma unroll
+        for (int i = 0; i < 32; i += 2) {
+            uint64_t g[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t word = ww[i + q / 4];
+                if (LDS) g[q] = gear_fetch(word, BW_SEL(q % 4), lane_off, s_gear);
+                else g[q] = (uint64_t)((word >> (8 * (q % 4))) & 0xff) * 0x9E3779B97F4A7C15ull;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+                h = (h << 1) + g[q];
+                const uint32_t t0 = mask_test(h, mlo, mhi);
+                h = (h << 1) + g[q + 1];
+                const uint32_t t1 = mask_test(h, mlo, mhi);
+                acc = min(acc, min(t0, t1));
+            }
+        }
+        hits += acc == 0;
+    }
+    if (hits == 0x7fffffff) out[0] = hits + (uint32_t)h;
+}
+
+__global__ __launch_bounds__(256) void b3_noload(uint64_t blocks_per_lane, uint32_t* out) {
+    uint32_t cv[8];
+    b3_iv(cv);
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = threadIdx.x * 16 + i;
+    for (uint64_t b = 0; b < blocks_per_lane; b++) {
+        m[0] ^= (uint32_t)b;
+        b3_compress(cv, m, 64, b, 0);
+    }
+    if (cv[0] == 0x12345678) out[0] = cv[1];
+}
+
+template <typename F>
+static float timeit(F f, int reps = 5) {
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    f();
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a));
+    for (int i = 0; i < reps; i++) f();
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main() {
+    const uint64_t n = 4ull << 30;
+    uint8_t* d;
+    uint32_t *out, *tc;
+    uint64_t* ts;
+    CHECK(hipMalloc(&d, n));
+    CHECK(hipMalloc(&out, 64));
+    const uint64_t tiles = n / SCAN_TILE;
+    CHECK(hipMalloc(&tc, tiles * 4));
+    CHECK(hipMalloc(&ts, tiles * SCAN_CAP * 8));
+    {
+        uint32_t* h = (uint32_t*)malloc(1 << 26);
+        for (int i = 0; i < (1 << 24); i++) h[i] = (uint32_t)rand() * 2654435761u ^ (uint32_t)rand();
+        for (uint64_t o = 0; o < n; o += 1 << 26) CHECK(hipMemcpy(d + o, h, 1 << 26, hipMemcpyHostToDevice));
+        free(h);
+    }
+    Masks mk;
+    mk.min = 262144; mk.avg = 1048576; mk.max = 3145728; mk.s0 = 262144;
+    mk.mask_s = 0x0000d91767537000ull; mk.mask_l = 0x0000d91707537000ull; mk.mask_pre = mk.mask_l;
+    const double gb = n / 1e9;
+    float t;
+    t = timeit([&] { hipLaunchKernelGGL(copy_strided, dim3(1024), dim3(512), 0, 0, d, n, out); });
+    printf("copy_strided   %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { hipLaunchKernelGGL(copy_coalesced, dim3(4096), dim3(512), 0, 0, d, n, out); });
+    printf("copy_coalesced %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { launch_scan(0, d, n, tiles, mk, tc, ts); });
+    printf("scan_full      %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { hipLaunchKernelGGL(scan_noload<true>, dim3(512), dim3(512), 0, 0, n, mk, out); });
+    printf("scan_noload    %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { hipLaunchKernelGGL(scan_noload<false>, dim3(512), dim3(512), 0, 0, n, mk, out); });
+    printf("scan_nolds     %8.3f ms %8.1f GB/s (no LDS, no HBM)\n", t, gb / t * 1e3);
+    const uint64_t lanes = 256ull * 4096;
+    const uint64_t bpl = n / 64 / lanes;
+    t = timeit([&] { hipLaunchKernelGGL(b3_noload, dim3(4096), dim3(256), 0, 0, bpl, out); });
+    printf("b3_noload      %8.3f ms %8.1f GB/s (compressions on registers, %llu blocks/lane)\n", t, gb / t * 1e3,
+           (unsigned long long)bpl);
+    return 0;
+}
