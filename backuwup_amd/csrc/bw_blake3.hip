@@ -23,18 +23,22 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Chaining value of one leaf (<= 1024 bytes at global position `ls`), chunk counter `t`.
 // `bend` is the end of the blob: loads never touch bytes at or beyond it except through the
 // byte-exact tail path, so a blob at the very end of the caller's buffer is safe.
-__device__ __forceinline__ void load_words(const uint32_t* wb, uint32_t blk, uint32_t w[17]) {
-    const u32x4_a4* q = (const u32x4_a4*)(wb + blk * 16);
+__device__ uint32_t g_b3_dummy[20];  // target of clamped (never consumed) prefetches
+
+__device__ __forceinline__ void load_words(const uint32_t* src, uint32_t w[17]) {
+    const u32x4_a4* q = (const u32x4_a4*)src;
     const u32x4_a4 a = q[0], b = q[1], c = q[2], d = q[3];
     w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
     w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w; w[12] = d.x; w[13] = d.y; w[14] = d.z; w[15] = d.w;
-    w[16] = wb[blk * 16 + 16];
+    w[16] = src[16];
 }
 
 // Chaining value of one leaf (<= 1024 bytes at global position `ls`), chunk counter `t`.
 // `bend` is the end of the blob: the 16-byte loads never touch bytes at or beyond it (a block
 // within 68 bytes of the end goes through the byte-exact path), so a blob at the very end of
-// the caller's buffer is safe.  Block b+1 is loaded before block b is compressed.
+// the caller's buffer is safe.  Block b+1 is loaded before block b is compressed; the loads are
+// unconditional (a block that will take the byte path prefetches a dummy line instead) so the
+// compiler's vmcnt waits stay exact.
 __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64_t ls, uint32_t ll, uint64_t bend,
                                         uint64_t t, uint32_t root, uint32_t cv[8]) {
     b3_iv(cv);
@@ -43,7 +47,7 @@ __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64
     const uint32_t sh = (uint32_t)((uintptr_t)base & 3);
     const uint32_t* wb = (const uint32_t*)(base - sh);
     uint32_t w[17];
-    if (ls + 68 <= bend) load_words(wb, 0, w);
+    load_words(ls + 68 <= bend ? wb : g_b3_dummy, w);
     for (uint32_t blk = 0; blk < nblk; blk++) {
         uint32_t m[16];
         const uint32_t left = ll - blk * 64;
@@ -62,7 +66,8 @@ __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64
                 m[i] = v;
             }
         }
-        if (blk + 1 < nblk && ls + (blk + 1) * 64 + 68 <= bend) load_words(wb, blk + 1, w);
+        const bool nfast = blk + 1 < nblk && ls + (blk + 1) * 64 + 68 <= bend;
+        load_words(nfast ? wb + (blk + 1) * 16 : g_b3_dummy, w);
         uint32_t flags = 0;
         if (blk == 0) flags |= B3_CHUNK_START;
         if (blk == nblk - 1) flags |= B3_CHUNK_END | root;

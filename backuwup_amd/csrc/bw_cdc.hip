@@ -62,29 +62,90 @@ __device__ __forceinline__ void record_hit(uint64_t pos, uint64_t h, const Masks
     }
 }
 
-// Every thread owns a 2 KiB strip of the tile, warms the 64-bit gear state up on the 64 bytes
-// before it (the state after 64 steps is exactly the windowed hash), then tests every byte.
-// The test folds 128 positions into one min() and takes the slow recording path only when some
-// position passes the prefilter mask (~2.4e-4 per line at backuwup's parameters).
-__global__ __launch_bounds__(SCAN_THREADS, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
-                                                         uint64_t n_tiles, Masks mk,
-                                                         uint32_t* __restrict__ tile_count,
-                                                         uint64_t* __restrict__ tile_slots) {
-    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_REP];  // 64 KiB at LDS offset 0
-    __shared__ uint64_t s_slots[SCAN_CAP];
-    __shared__ uint32_t s_cnt[1];
-    for (int i = threadIdx.x; i < 256 * GEAR_REP; i += blockDim.x) s_gear[i] = c_gear[i / GEAR_REP];
-    const uint32_t lane_off = (threadIdx.x & 31) * 8;
-    const uint32_t mlo = (uint32_t)mk.mask_pre, mhi = (uint32_t)(mk.mask_pre >> 32);
+// Gear scan.  Each wavefront owns a 128 KiB sub-tile = 64 strips of 2 KiB, one per lane.  The
+// gear state is warmed up on the 64 bytes before the strip (after 64 steps it IS the windowed
+// hash), then every byte is tested.  Bytes reach the lanes coalesced: per 64-byte step, four
+// global_load_dwordx4 fetch 16 strips x 64 B each (4 lanes per half line), the wave stages them
+// in its own padded LDS rows and every lane reads back its strip's 64 bytes (16 B per
+// ds_read_b128, conflict-free with 80-byte rows).  The next step's loads are in flight while
+// the current step is hashed (two register sets, unconditional loads so the vmcnt waits are
+// exact).  128 positions fold into one min() of the prefilter test; only a step with a hit in
+// some lane replays bytes to record it (~1e-4 per lane-step at backuwup's parameters).  No
+// block barrier after the table fill: candidates are collected per wave in LDS and published
+// by lane 0.
+__device__ __forceinline__ void hash_words(uint64_t& h, uint32_t& acc, const uint32_t (&ww)[16], uint32_t lane_off,
+                                           const uint64_t* s_gear, uint32_t mlo, uint32_t mhi) {
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+        uint64_t g[8];  // 8 independent LDS reads ahead of the serial recurrence
+#pragma unroll
+        for (int q = 0; q < 8; q++) g[q] = gear_fetch(ww[i + q / 4], BW_SEL(q % 4), lane_off, s_gear);
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) {
+            h = (h << 1) + g[q];
+            const uint32_t t0 = mask_test(h, mlo, mhi);
+            h = (h << 1) + g[q + 1];
+            const uint32_t t1 = mask_test(h, mlo, mhi);
+            acc = min(acc, min(t0, t1));
+        }
+    }
+}
 
-    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        if (threadIdx.x == 0) *s_cnt = 0;
-        __syncthreads();
-        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_STRIP;
-        if (ss < n_bytes) {
-            const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
-            uint64_t h = 0;
-            if (ss >= 64) {
+// One 64-byte step of one lane: stage the wave's four coalesced loads, read back this lane's
+// strip bytes, hash them; on a prefilter hit replay the step byte by byte and record.
+__device__ __forceinline__ void stage_hash_step(uint4 r0, uint4 r1, uint4 r2, uint4 r3, uint8_t* wr,
+                                                const uint8_t* rd, uint64_t& h, uint64_t at,
+                                                const uint8_t* __restrict__ data, uint32_t lane_off,
+                                                const uint64_t* s_gear, uint32_t mlo, uint32_t mhi, const Masks& mk,
+                                                uint32_t* cnt, uint64_t* slots) {
+    *(uint4*)(wr) = r0;
+    *(uint4*)(wr + 16 * STAGE_ROW) = r1;
+    *(uint4*)(wr + 32 * STAGE_ROW) = r2;
+    *(uint4*)(wr + 48 * STAGE_ROW) = r3;
+    __builtin_amdgcn_wave_barrier();
+    const uint4 v0 = *(const uint4*)(rd), v1 = *(const uint4*)(rd + 16), v2 = *(const uint4*)(rd + 32),
+                v3 = *(const uint4*)(rd + 48);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t ww[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                             v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+    const uint64_t h0 = h;
+    uint32_t acc = 0xffffffffu;
+    hash_words(h, acc, ww, lane_off, s_gear, mlo, mhi);
+    if (__builtin_expect(acc == 0, 0)) {
+        uint64_t hh = h0;
+        for (int i = 0; i < SCAN_STEP; i++) {
+            hh = (hh << 1) + s_gear[(uint32_t)data[at + i] * GEAR_REP];
+            if (mask_test(hh, mlo, mhi) == 0) record_hit(at + i, hh, mk, cnt, slots);
+        }
+    }
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
+                                                       uint64_t n_tiles, Masks mk,
+                                                       uint32_t* __restrict__ tile_count,
+                                                       uint64_t* __restrict__ tile_slots) {
+    constexpr int WAVES = SCAN_BLOCK / 64;
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_REP];  // 64 KiB at LDS offset 0
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES][64 * STAGE_ROW];
+    __shared__ uint64_t s_slots[WAVES][SCAN_CAP];
+    __shared__ uint32_t s_cnt[WAVES];
+    for (int i = threadIdx.x; i < 256 * GEAR_REP; i += blockDim.x) s_gear[i] = c_gear[i / GEAR_REP];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t lane_off = (lane & 31) * 8;
+    const uint32_t mlo = (uint32_t)mk.mask_pre, mhi = (uint32_t)(mk.mask_pre >> 32);
+    uint8_t* stage = s_stage[wid];
+    uint32_t* cnt = &s_cnt[wid];
+    uint64_t* slots = s_slots[wid];
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+
+    for (uint64_t tile = (uint64_t)blockIdx.x * WAVES + wid; tile < n_tiles; tile += nw) {
+        if (lane == 0) *cnt = 0;
+        const uint64_t base = tile * SCAN_TILE;
+        const uint64_t ss = base + (uint64_t)lane * SCAN_STRIP;
+        uint64_t h = 0;
+        if (base + SCAN_TILE <= n_bytes) {
+            if (ss >= 64) {  // warm-up on the 64 bytes before the strip
                 const uint4* wp = (const uint4*)(data + ss - 64);
                 uint4 w[4];
 #pragma unroll
@@ -98,85 +159,66 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_scan(const uint8_t* __restr
                         for (int k = 0; k < 4; k++) gear_step(h, ww[j], BW_SEL(k), lane_off, s_gear);
                 }
             }
-            uint64_t p = ss;
-            uint4 w[8];
-            if (p + 128 <= se) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) w[i] = ((const uint4*)(data + p))[i];
+            // lane L loads piece (L & 3) of strip 16 j + (L >> 2) for j = 0..3
+            const uint8_t* src = data + base + (uint64_t)(lane >> 2) * SCAN_STRIP + (lane & 3) * 16;
+            uint8_t* wr = stage + (lane >> 2) * STAGE_ROW + (lane & 3) * 16;
+            const uint8_t* rd = stage + lane * STAGE_ROW;
+            constexpr int STEPS = SCAN_STRIP / SCAN_STEP;
+            constexpr uint64_t JS = 16ull * SCAN_STRIP;
+#define BW_LOAD4(r0, r1, r2, r3, step)                                   \
+    do {                                                                 \
+        const uint8_t* s_ = src + (uint64_t)(step) * SCAN_STEP;          \
+        r0 = *(const uint4*)(s_);                                        \
+        r1 = *(const uint4*)(s_ + JS);                                   \
+        r2 = *(const uint4*)(s_ + 2 * JS);                               \
+        r3 = *(const uint4*)(s_ + 3 * JS);                               \
+    } while (0)
+            uint4 a0, a1, a2, a3, b0, b1, b2, b3;
+            BW_LOAD4(a0, a1, a2, a3, 0);
+#pragma unroll 1
+            for (int step = 0; step < STEPS; step += 2) {
+                BW_LOAD4(b0, b1, b2, b3, step + 1);
+                stage_hash_step(a0, a1, a2, a3, wr, rd, h, ss + (uint64_t)step * SCAN_STEP, data, lane_off, s_gear,
+                                mlo, mhi, mk, cnt, slots);
+                BW_LOAD4(a0, a1, a2, a3, step + 2 < STEPS ? step + 2 : STEPS - 1);  // clamped, unused at the end
+                stage_hash_step(b0, b1, b2, b3, wr, rd, h, ss + (uint64_t)(step + 1) * SCAN_STEP, data, lane_off,
+                                s_gear, mlo, mhi, mk, cnt, slots);
             }
-            for (; p + 128 <= se; p += 128) {
-                uint4 nx[8];  // next line in flight while this one is hashed
-                const bool more = p + 256 <= se;
-                if (more) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) nx[i] = ((const uint4*)(data + p + 128))[i];
-                }
-                const uint64_t h0 = h;
-                uint32_t acc = 0xffffffffu;
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const uint32_t ww[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
-#pragma unroll
-                    for (int half = 0; half < 2; half++) {
-                        uint64_t g[8];  // issue 8 independent LDS reads before the serial chain
-#pragma unroll
-                        for (int q = 0; q < 8; q++)
-                            g[q] = gear_fetch(ww[half * 2 + q / 4], BW_SEL(q % 4), lane_off, s_gear);
-#pragma unroll
-                        for (int q = 0; q < 8; q += 2) {
-                            h = (h << 1) + g[q];
-                            const uint32_t t0 = mask_test(h, mlo, mhi);
-                            h = (h << 1) + g[q + 1];
-                            const uint32_t t1 = mask_test(h, mlo, mhi);
-                            acc = min(acc, min(t0, t1));
-                        }
-                    }
-                }
-                if (__builtin_expect(acc == 0, 0)) {
-                    // rare: replay the line byte by byte (L1/L2-hot) and record the hits
-                    uint64_t hh = h0;
-                    for (int i = 0; i < 128; i++) {
-                        hh = (hh << 1) + s_gear[(uint32_t)data[p + i] * GEAR_REP];
-                        if (mask_test(hh, mlo, mhi) == 0) record_hit(p + i, hh, mk, s_cnt, s_slots);
-                    }
-                }
-                if (more) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) w[i] = nx[i];
-                }
-            }
-            for (; p < se; p++) {  // ragged end of the buffer only
-                const uint64_t g = s_gear[(uint32_t)data[p] * GEAR_REP];
-                h = (h << 1) + g;
-                if (mask_test(h, mlo, mhi) == 0) record_hit(p, h, mk, s_cnt, s_slots);
+#undef BW_LOAD4
+        } else if (ss < n_bytes) {  // ragged last sub-tile: byte path
+            const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
+            for (uint64_t p = ss >= 64 ? ss - 64 : 0; p < se; p++) {
+                h = (h << 1) + s_gear[(uint32_t)data[p] * GEAR_REP];
+                if (p >= ss && mask_test(h, mlo, mhi) == 0) record_hit(p, h, mk, cnt, slots);
             }
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t cnt = *s_cnt, n = cnt < (uint32_t)SCAN_CAP ? cnt : (uint32_t)SCAN_CAP;
-            for (uint32_t i = 1; i < n; i++) {  // insertion sort by position (n is ~1)
-                uint64_t v = s_slots[i];
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            const uint32_t c = *cnt, n = c < (uint32_t)SCAN_CAP ? c : (uint32_t)SCAN_CAP;
+            for (uint32_t i = 1; i < n; i++) {  // insertion sort by position (n is ~0)
+                uint64_t v = slots[i];
                 int k = (int)i - 1;
-                while (k >= 0 && BW_CAND_POS(s_slots[k]) > BW_CAND_POS(v)) {
-                    s_slots[k + 1] = s_slots[k];
+                while (k >= 0 && BW_CAND_POS(slots[k]) > BW_CAND_POS(v)) {
+                    slots[k + 1] = slots[k];
                     k--;
                 }
-                s_slots[k + 1] = v;
+                slots[k + 1] = v;
             }
-            tile_count[tile] = cnt;
-            for (uint32_t i = 0; i < n; i++) tile_slots[tile * SCAN_CAP + i] = s_slots[i];
+            tile_count[tile] = c;
+            for (uint32_t i = 0; i < n; i++) tile_slots[tile * SCAN_CAP + i] = slots[i];
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
 void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                  uint32_t* tile_count, uint64_t* tile_slots) {
     if (!n_tiles) return;
-    const size_t lds = 0;
-    const uint64_t grid = n_tiles < 1024 ? n_tiles : 1024;
-    hipLaunchKernelGGL(k_scan, dim3((unsigned)grid), dim3(SCAN_THREADS), lds, st, data, n_bytes, n_tiles, mk,
-                       tile_count, tile_slots);
+    const uint64_t waves = (n_tiles + 0) ;
+    uint64_t grid = (waves + SCAN_BLOCK / 64 - 1) / (SCAN_BLOCK / 64);
+    if (grid > 512) grid = 512;  // persistent: 2 rounds of 256 CUs x 1 block
+    hipLaunchKernelGGL(k_scan, dim3((unsigned)grid), dim3(SCAN_BLOCK), 0, st, data, n_bytes, n_tiles, mk, tile_count,
+                       tile_slots);
 }
 
 // ======================================================================== block scan helpers
@@ -256,24 +298,27 @@ __global__ void k_compact(const uint32_t* __restrict__ cnt, const uint64_t* __re
 }
 
 // Exact ordered re-scan of a tile whose candidates overflowed the slots (pathological data).
-__global__ __launch_bounds__(SCAN_THREADS) void k_rescan(const uint8_t* __restrict__ data, uint64_t n_bytes,
-                                                         Masks mk, const uint32_t* __restrict__ ovf,
-                                                         const uint64_t* __restrict__ off,
-                                                         uint64_t* __restrict__ cand, uint64_t cap,
-                                                         const uint64_t* ctr) {
+constexpr int RESCAN_THREADS = 256;
+constexpr uint64_t RESCAN_STRIP = SCAN_TILE / RESCAN_THREADS;
+
+__global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __restrict__ data, uint64_t n_bytes,
+                                                           Masks mk, const uint32_t* __restrict__ ovf,
+                                                           const uint64_t* __restrict__ off,
+                                                           uint64_t* __restrict__ cand, uint64_t cap,
+                                                           const uint64_t* ctr) {
     __shared__ uint64_t s_gear[256];
-    __shared__ uint64_t s_scan[SCAN_THREADS];
+    __shared__ uint64_t s_scan[RESCAN_THREADS];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) s_gear[i] = c_gear[i];
     __syncthreads();
     const uint64_t novf = ctr[C_NOVF];
     for (uint64_t k = blockIdx.x; k < novf; k += gridDim.x) {
         const uint64_t tile = ovf[k];
-        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_STRIP;
-        const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
+        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * RESCAN_STRIP;
+        const uint64_t se = ss + RESCAN_STRIP < n_bytes ? ss + RESCAN_STRIP : n_bytes;
         uint64_t mine = 0;
         for (int pass = 0; pass < 2; pass++) {
             uint64_t h = 0, w = 0;
-            if (pass == 1) w = off[tile] + block_excl_sum<SCAN_THREADS>(mine, s_scan, nullptr);
+            if (pass == 1) w = off[tile] + block_excl_sum<RESCAN_THREADS>(mine, s_scan, nullptr);
             if (ss < n_bytes) {
                 for (uint64_t p = ss >= 64 ? ss - 64 : 0; p < se; p++) {
                     h = (h << 1) + s_gear[data[p]];
@@ -297,7 +342,7 @@ void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint6
     if (!n_tiles) return;
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count,
                        tile_slots, tile_off, n_tiles, cand, cand_cap, ovf_list, ctr);
-    hipLaunchKernelGGL(k_rescan, dim3(64), dim3(SCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
+    hipLaunchKernelGGL(k_rescan, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
                        cand, cand_cap, ctr);
 }
 

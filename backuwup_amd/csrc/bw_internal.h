@@ -6,10 +6,12 @@
 namespace bw {
 
 // ------------------------------------------------------------------ tunables
-constexpr int SCAN_THREADS = 512;
-constexpr int SCAN_STRIP = 2048;                                  // bytes per thread
-constexpr uint64_t SCAN_TILE = (uint64_t)SCAN_THREADS * SCAN_STRIP; // 1 MiB per tile
-constexpr int SCAN_CAP = 32;                                      // candidate slots per tile
+constexpr int SCAN_BLOCK = 1024;                                   // 16 waves, 1 block per CU (LDS)
+constexpr int SCAN_STRIP = 2048;                                   // bytes per lane
+constexpr uint64_t SCAN_TILE = 64ull * SCAN_STRIP;                 // one wave's 128 KiB sub-tile
+constexpr int SCAN_CAP = 16;                                       // candidate slots per tile
+constexpr int SCAN_STEP = 64;                                      // bytes per lane per staged step
+constexpr int STAGE_ROW = SCAN_STEP + 16;                          // padded LDS staging row
 constexpr int GEAR_REP = 32;                                      // LDS gear replicas
 constexpr int CHAIN_CAP = 128;                                    // cuts stored per segment
 

@@ -38,9 +38,11 @@ int main() {
     }
     BlobIndex index(ctx);
     BlobHash a = blake3::hash(ctx, data.data(), 100), b = blake3::hash(ctx, data.data(), 101);
-    index.load({std::min(a, b)});
-    printf("gate %d %d %d %d\n", (int)add_blob_gate(index, a, 100), (int)add_blob_gate(index, b, 101),
-           (int)add_blob_gate(index, b, 101), (int)index.size());
+    index.load({a});
+    const int g1 = add_blob_gate(index, a, 100);  // seeded -> duplicate (Ok(None))
+    const int g2 = add_blob_gate(index, b, 101);  // new
+    const int g3 = add_blob_gate(index, b, 101);  // now a duplicate
+    printf("gate %d %d %d %d\n", g1, g2, g3, (int)index.size());
     try {
         add_blob_gate(index, a, BW_BLOB_MAX_UNCOMPRESSED_SIZE + 1);
     } catch (const BlobTooLarge&) {

@@ -24,11 +24,13 @@ using namespace bw;
         if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } \
     } while (0)
 
+// 512 threads x 2 KiB strips = 1 MiB per block-tile; every byte read lies inside [0, n)
 __global__ __launch_bounds__(512) void copy_strided(const uint8_t* __restrict__ data, uint64_t n, uint32_t* out) {
     uint32_t acc = 0;
-    for (uint64_t tile = blockIdx.x; tile * SCAN_TILE < n; tile += gridDim.x) {
-        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_STRIP;
-        for (uint64_t p = ss; p < ss + SCAN_STRIP; p += 128) {
+    const uint64_t TILE = 512ull * 2048;
+    for (uint64_t tile = blockIdx.x; (tile + 1) * TILE <= n; tile += gridDim.x) {
+        const uint64_t ss = tile * TILE + (uint64_t)threadIdx.x * 2048;
+        for (uint64_t p = ss; p < ss + 2048; p += 128) {
             const uint4* wp = (const uint4*)(data + p);
 #pragma unroll
             for (int i = 0; i < 8; i++) { uint4 w = wp[i]; acc ^= w.x ^ w.y ^ w.z ^ w.w; }
@@ -146,6 +148,30 @@ int main() {
     printf("scan_noload    %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { hipLaunchKernelGGL(scan_noload<false>, dim3(512), dim3(512), 0, 0, n, mk, out); });
     printf("scan_nolds     %8.3f ms %8.1f GB/s (no LDS, no HBM)\n", t, gb / t * 1e3);
+    {  // the shipped BLAKE3 kernels on 4096 blobs of 1 MiB (one unaligned start per blob)
+        const uint64_t nb = 4096, blen = (1ull << 20) - 64;
+        uint64_t *ctr, *bs, *bl, *bg, *fe, *gh;
+        uint32_t *bf, *bk, *cv;
+        uint8_t* dig;
+        CHECK(hipMalloc(&ctr, 16 * 8)); CHECK(hipMalloc(&bs, nb * 8)); CHECK(hipMalloc(&bl, nb * 8));
+        CHECK(hipMalloc(&bg, nb * 8)); CHECK(hipMalloc(&fe, nb * 8)); CHECK(hipMalloc(&gh, nb * 8));
+        CHECK(hipMalloc(&bf, nb * 4)); CHECK(hipMalloc(&bk, nb * 4)); CHECK(hipMalloc(&dig, nb * 32));
+        const uint64_t groups_per = (blen / 1024 + 1 + 3) / 4;
+        CHECK(hipMalloc(&cv, nb * groups_per * 32));
+        uint64_t hc[16] = {0};
+        hc[C_NBLOBS] = nb; hc[C_NGROUPS] = nb * groups_per;
+        CHECK(hipMemcpy(ctr, hc, sizeof hc, hipMemcpyHostToDevice));
+        uint64_t* tmp = (uint64_t*)malloc(nb * 8 * 3);
+        for (uint64_t i = 0; i < nb; i++) { tmp[i] = i * (1ull << 20) + 17; tmp[nb + i] = blen; tmp[2 * nb + i] = i * groups_per; }
+        CHECK(hipMemcpy(bs, tmp, nb * 8, hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(bl, tmp + nb, nb * 8, hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(bg, tmp + 2 * nb, nb * 8, hipMemcpyHostToDevice));
+        free(tmp);
+        BlobArrays b{bs, bl, bg, bf, bk, fe, gh};
+        t = timeit([&] { launch_blake3(0, d, ctr, b, nb, nb * groups_per, cv, dig, (int)(blen / 1024 + 1), nullptr); });
+        printf("b3_full        %8.3f ms %8.1f GB/s (k_b3_groups + k_b3_tree, 4096 x 1 MiB blobs)\n", t,
+               nb * blen / 1e9 / t * 1e3);
+    }
     const uint64_t lanes = 256ull * 4096;
     const uint64_t bpl = n / 64 / lanes;
     t = timeit([&] { hipLaunchKernelGGL(b3_noload, dim3(4096), dim3(256), 0, 0, bpl, out); });
