@@ -144,14 +144,21 @@ __global__ __launch_bounds__(256) void k_b3_groups(const uint8_t* __restrict__ d
     }
 }
 
-// Upper levels of one blob (n > 4 leaves).  Level-2 nodes come from k_b3_groups; level l+1 is
-// built in LDS from level l; thread 0 folds the right spine as each level becomes available.
+// Upper levels of one blob (n > 4 leaves), one wavefront per blob.  Level-2 nodes come from
+// k_b3_groups (global); level 3 is built into the wave's LDS region, later levels in place, 64
+// parents per pass (a wave's LDS accesses execute in order, and pass p reads nodes
+// [128p, 128p+128) while writing [64p, 64p+64), so the in-place update is safe).  Lane 0 folds
+// the right spine as each level becomes available.  Many blobs are in flight per CU, so the
+// kernel is throughput- rather than barrier-latency-bound.
 __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays b,
                                                  const uint32_t* __restrict__ cv_buf,
-                                                 uint8_t* __restrict__ digests) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t nodes[];  // [cap][8]
+                                                 uint8_t* __restrict__ digests, uint32_t node_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t wpb = blockDim.x / 64, wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    uint32_t* nodes = smem + (uint64_t)wave * node_cap * 8;
     const uint64_t nblobs = ctr[C_NBLOBS];
-    for (uint64_t blob = blockIdx.x; blob < nblobs; blob += gridDim.x) {  // persistent over blobs
+    const uint64_t stride = (uint64_t)gridDim.x * wpb;
+    for (uint64_t blob = (uint64_t)blockIdx.x * wpb + wave; blob < nblobs; blob += stride) {
         const uint64_t len = b.len[blob];
         const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
         if (n <= 4) continue;
@@ -159,14 +166,14 @@ __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays
         uint64_t cnt = n / 4;
         uint32_t acc[8];
         bool have = false;
-        if (threadIdx.x == 0 && (n & 3)) {
+        if (lane == 0 && (n & 3)) {
 #pragma unroll
             for (int i = 0; i < 8; i++) acc[i] = lvl2[cnt * 8 + i];
             have = true;
         }
         const uint32_t* src = lvl2;
         for (int l = 2;; l++) {
-            if (threadIdx.x == 0 && ((n >> l) & 1)) {
+            if (lane == 0 && ((n >> l) & 1)) {
                 uint32_t T[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) T[i] = src[(cnt - 1) * 8 + i];
@@ -181,26 +188,23 @@ __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays
             const uint64_t next = cnt / 2;
             if (next == 0) break;
             const uint32_t root = (n == (1ull << (l + 1))) ? B3_ROOT : 0;
-            for (uint64_t c0 = 0; c0 < next; c0 += blockDim.x) {
-                const uint64_t i = c0 + threadIdx.x;
-                uint32_t L[8], R[8], P[8];
+            for (uint64_t i0 = 0; i0 < next; i0 += 64) {
+                const uint64_t i = i0 + lane;
                 if (i < next) {
+                    uint32_t L[8], R[8], P[8];
 #pragma unroll
                     for (int w = 0; w < 8; w++) { L[w] = src[(2 * i) * 8 + w]; R[w] = src[(2 * i + 1) * 8 + w]; }
-                }
-                __syncthreads();
-                if (i < next) {
                     b3_parent(L, R, root, P);
 #pragma unroll
                     for (int w = 0; w < 8; w++) nodes[i * 8 + w] = P[w];
                 }
-                __syncthreads();
+                __builtin_amdgcn_wave_barrier();
             }
             src = nodes;
             cnt = next;
         }
-        if (threadIdx.x == 0) store_digest(digests + blob * 32, acc);
-        __syncthreads();  // the next blob reuses `nodes`
+        if (lane == 0) store_digest(digests + blob * 32, acc);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -211,9 +215,13 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
                        cv_buf, digests);
     if (between) hipEventRecord(between, st);
     if (max_leaves > 4) {
-        const size_t lds = (size_t)((max_leaves / 4) / 2 + 1) * 32;
-        const uint64_t grid = max_blobs < 2048 ? max_blobs : 2048;
-        hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)grid), dim3(256), lds, st, ctr, b, cv_buf, digests);
+        const uint32_t node_cap = (uint32_t)((max_leaves / 4) / 2 + 1);
+        uint32_t wpb = (48u << 10) / (node_cap * 32);
+        wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
+        const size_t lds = (size_t)wpb * node_cap * 32;
+        uint64_t grid = (max_blobs + wpb - 1) / wpb;
+        if (grid > 8192) grid = 8192;
+        hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)grid), dim3(64 * wpb), lds, st, ctr, b, cv_buf, digests, node_cap);
     }
 }
 

@@ -40,7 +40,7 @@ struct bw_ctx {
     bool meta_pending = false;
 
     // per-batch device buffers
-    DevBuf tile_count, tile_slots, tile_off, cand, ovf, ctr;
+    DevBuf tile_count, tile_slots, tile_off, tile_btot, cand, ovf, ctr;
     DevBuf segs, cfiles, units, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
     DevBuf cv, digests, is_dup, packed, fstart, data, scratch;
@@ -212,7 +212,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->cand, &c->ovf, &c->ctr, &c->segs,
+    DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->ctr, &c->segs,
                      &c->cfiles, &c->units, &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->digests,
@@ -438,6 +438,7 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     rc |= ensure(c, c->tile_count, n_tiles * 4);
     rc |= ensure(c, c->tile_slots, n_tiles * SCAN_CAP * 8);
     rc |= ensure(c, c->tile_off, (n_tiles + 1) * 8);
+    rc |= ensure(c, c->tile_btot, (n_tiles / 1024 + 2) * 8);
     rc |= ensure(c, c->ovf, n_tiles * 4);
     rc |= ensure(c, c->segs, nseg * sizeof(SegDesc));
     rc |= ensure(c, c->cfiles, ncf * sizeof(CFileDesc));
@@ -509,7 +510,8 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
         launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots));
         prof_mark(c, BW_STAGE_COMPACT);
         launch_compact(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
-                       P<uint64_t>(c->tile_off), P<uint64_t>(c->cand), cand_cap, P<uint32_t>(c->ovf), ctr);
+                       P<uint64_t>(c->tile_off), P<uint64_t>(c->cand), cand_cap, P<uint32_t>(c->ovf), ctr,
+                       P<uint64_t>(c->tile_btot));
         prof_mark(c, BW_STAGE_RESOLVE);
         launch_chains(st, d_data, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs), nseg,
                       P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->chain_cptr),

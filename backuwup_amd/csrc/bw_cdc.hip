@@ -13,7 +13,7 @@
 //
 // Pipeline (all on the stream, no host round trip):
 //   k_scan      gear hash at every byte, LDS lane-replicated table, per-tile candidate slots
-//   k_tilescan  exclusive scan of per-tile counts -> sorted global candidate array offsets
+//   k_tile_partial/k_tile_top  exclusive scan of per-tile counts -> candidate array offsets
 //   k_compact   copy slots; k_rescan handles (rare) overflowing tiles exactly
 //   k_chains    one wave per segment: speculative boundary chain from the segment start
 //   k_extend    continue each chain until it merges with the next segment's chain (CDC resync)
@@ -125,10 +125,19 @@ __global__ __launch_bounds__(SCAN_BLOCK, 4) void k_scan(const uint8_t* __restric
                                                        uint32_t* __restrict__ tile_count,
                                                        uint64_t* __restrict__ tile_slots) {
     constexpr int WAVES = SCAN_BLOCK / 64;
-    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_REP];  // 64 KiB at LDS offset 0
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[WAVES][64 * STAGE_ROW];
-    __shared__ uint64_t s_slots[WAVES][SCAN_CAP];
-    __shared__ uint32_t s_cnt[WAVES];
+    // one LDS object so the gear table sits at LDS address 0 and every lookup address is the
+    // v_perm result itself (a table at a non-zero base costs one v_add per byte)
+    struct ScanLds {
+        uint64_t gear[256 * GEAR_REP];        // 64 KiB, 32 lane replicas
+        uint8_t stage[WAVES][64 * STAGE_ROW]; // per-wave staging rows
+        uint64_t slots[WAVES][SCAN_CAP];
+        uint32_t cnt[WAVES];
+    };
+    __shared__ __attribute__((aligned(16))) ScanLds lds;
+    uint64_t* s_gear = lds.gear;
+    uint8_t (*s_stage)[64 * STAGE_ROW] = lds.stage;
+    uint64_t (*s_slots)[SCAN_CAP] = lds.slots;
+    uint32_t* s_cnt = lds.cnt;
     for (int i = threadIdx.x; i < 256 * GEAR_REP; i += blockDim.x) s_gear[i] = c_gear[i / GEAR_REP];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -264,18 +273,42 @@ __device__ __forceinline__ uint64_t block_excl_segmax(uint32_t f, uint64_t v, ui
 
 constexpr int BLK = 1024;
 
-__global__ __launch_bounds__(BLK) void k_tilescan(const uint32_t* __restrict__ cnt, uint64_t n,
+// Candidate offsets: a three-kernel scan over the per-tile counts (tiles are 128 KiB, so a
+// 16 GiB batch has 131072 of them): block-local scans of 1024 counts, one block over the block
+// totals, then compaction adds the block base and copies the slots.
+constexpr int TS_BLOCK = 256;  // threads per block, 4 counts each
+
+__global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint32_t* __restrict__ cnt, uint64_t n,
+                                                           uint64_t* __restrict__ off, uint64_t* __restrict__ btot) {
+    __shared__ uint64_t s[TS_BLOCK];
+    const uint64_t i0 = ((uint64_t)blockIdx.x * TS_BLOCK + threadIdx.x) * 4;
+    uint32_t c[4] = {0, 0, 0, 0};
+    if (i0 + 4 <= n) {
+        const uint4 v = *(const uint4*)(cnt + i0);
+        c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+    } else {
+        for (int k = 0; k < 4; k++) c[k] = i0 + k < n ? cnt[i0 + k] : 0;
+    }
+    const uint64_t sum = (uint64_t)c[0] + c[1] + c[2] + c[3];
+    uint64_t total;
+    uint64_t run = block_excl_sum<TS_BLOCK>(sum, s, &total);
+    for (int k = 0; k < 4; k++)
+        if (i0 + k < n) { off[i0 + k] = run; run += c[k]; }
+    if (threadIdx.x == 0) btot[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(BLK) void k_tile_top(uint64_t* __restrict__ btot, uint64_t nb, uint64_t n_tiles,
                                                   uint64_t* __restrict__ off, uint64_t cap, uint64_t* ctr) {
     __shared__ uint64_t s[BLK];
-    const uint64_t per = (n + BLK - 1) / BLK, lo = threadIdx.x * per;
-    const uint64_t hi = lo + per < n ? lo + per : n;
+    const uint64_t per = (nb + BLK - 1) / BLK, lo = threadIdx.x * per;
+    const uint64_t hi = lo + per < nb ? lo + per : nb;
     uint64_t sum = 0;
-    for (uint64_t i = lo; i < hi; i++) sum += cnt[i];
+    for (uint64_t i = lo; i < hi; i++) sum += btot[i];
     uint64_t total;
     uint64_t run = block_excl_sum<BLK>(sum, s, &total);
-    for (uint64_t i = lo; i < hi; i++) { off[i] = run; run += cnt[i]; }
+    for (uint64_t i = lo; i < hi; i++) { const uint64_t t = btot[i]; btot[i] = run; run += t; }
     if (threadIdx.x == 0) {
-        off[n] = total;
+        off[n_tiles] = total;
         ctr[C_NCAND] = total < cap ? total : cap;
         ctr[C_CANDTOTAL] = total;
         ctr[C_NOVF] = 0;
@@ -283,14 +316,16 @@ __global__ __launch_bounds__(BLK) void k_tilescan(const uint32_t* __restrict__ c
 }
 
 __global__ void k_compact(const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ slots,
-                          const uint64_t* __restrict__ off, uint64_t n_tiles, uint64_t* __restrict__ cand,
-                          uint64_t cap, uint32_t* __restrict__ ovf, uint64_t* ctr) {
+                          uint64_t* __restrict__ off, const uint64_t* __restrict__ bbase, uint64_t n_tiles,
+                          uint64_t* __restrict__ cand, uint64_t cap, uint32_t* __restrict__ ovf, uint64_t* ctr) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
+    const uint64_t o = off[t] + bbase[t / (4 * TS_BLOCK)];
+    off[t] = o;  // final offset: the walkers start their candidate cursor here
     const uint32_t c = cnt[t];
     if (c <= (uint32_t)SCAN_CAP) {
         for (uint32_t i = 0; i < c; i++)
-            if (off[t] + i < cap) cand[off[t] + i] = slots[t * SCAN_CAP + i];
+            if (o + i < cap) cand[o + i] = slots[t * SCAN_CAP + i];
     } else {
         const uint64_t k = atomicAdd((unsigned long long*)&ctr[C_NOVF], 1ull);
         ovf[k] = (uint32_t)t;
@@ -337,11 +372,13 @@ __global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __rest
 
 void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                     const uint32_t* tile_count, const uint64_t* tile_slots, uint64_t* tile_off, uint64_t* cand,
-                    uint64_t cand_cap, uint32_t* ovf_list, uint64_t* ctr) {
-    hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(BLK), 0, st, tile_count, n_tiles, tile_off, cand_cap, ctr);
+                    uint64_t cand_cap, uint32_t* ovf_list, uint64_t* ctr, uint64_t* btot) {
     if (!n_tiles) return;
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count,
-                       tile_slots, tile_off, n_tiles, cand, cand_cap, ovf_list, ctr);
+    const uint64_t nb = (n_tiles + 4 * TS_BLOCK - 1) / (4 * TS_BLOCK);
+    hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, tile_count, n_tiles, tile_off, btot);
+    hipLaunchKernelGGL(k_tile_top, dim3(1), dim3(BLK), 0, st, btot, nb, n_tiles, tile_off, cand_cap, ctr);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count, tile_slots,
+                       tile_off, btot, n_tiles, cand, cand_cap, ovf_list, ctr);
     hipLaunchKernelGGL(k_rescan, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
                        cand, cand_cap, ctr);
 }

@@ -74,7 +74,7 @@ void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t
 void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
                     const Masks& mk, const uint32_t* tile_count, const uint64_t* tile_slots,
                     uint64_t* tile_off, uint64_t* cand, uint64_t cand_cap, uint32_t* ovf_list,
-                    uint64_t* ctr);
+                    uint64_t* ctr, uint64_t* scratch /* >= n_tiles / 1024 + 1 entries */);
 void launch_chains(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
                    const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg,
                    uint64_t* chains, uint32_t* chain_n, uint64_t* chain_cptr, uint64_t* merge,
