@@ -39,6 +39,7 @@ __device__ __forceinline__ void load_words(const uint32_t* src, uint32_t w[17]) 
 // the caller's buffer is safe.  Block b+1 is loaded before block b is compressed; the loads are
 // unconditional (a block that will take the byte path prefetches a dummy line instead) so the
 // compiler's vmcnt waits stay exact.
+template <bool PREFETCH>
 __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64_t ls, uint32_t ll, uint64_t bend,
                                         uint64_t t, uint32_t root, uint32_t cv[8]) {
     b3_iv(cv);
@@ -47,8 +48,9 @@ __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64
     const uint32_t sh = (uint32_t)((uintptr_t)base & 3);
     const uint32_t* wb = (const uint32_t*)(base - sh);
     uint32_t w[17];
-    load_words(ls + 68 <= bend ? wb : g_b3_dummy, w);
+    if (PREFETCH) load_words(ls + 68 <= bend ? wb : g_b3_dummy, w);
     for (uint32_t blk = 0; blk < nblk; blk++) {
+        if (!PREFETCH) load_words(ls + blk * 64 + 68 <= bend ? wb + blk * 16 : g_b3_dummy, w);
         uint32_t m[16];
         const uint32_t left = ll - blk * 64;
         const uint32_t blen = ll == 0 ? 0 : (left < 64 ? left : 64);
@@ -66,8 +68,10 @@ __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64
                 m[i] = v;
             }
         }
-        const bool nfast = blk + 1 < nblk && ls + (blk + 1) * 64 + 68 <= bend;
-        load_words(nfast ? wb + (blk + 1) * 16 : g_b3_dummy, w);
+        if (PREFETCH) {
+            const bool nfast = blk + 1 < nblk && ls + (blk + 1) * 64 + 68 <= bend;
+            load_words(nfast ? wb + (blk + 1) * 16 : g_b3_dummy, w);
+        }
         uint32_t flags = 0;
         if (blk == 0) flags |= B3_CHUNK_START;
         if (blk == nblk - 1) flags |= B3_CHUNK_END | root;
@@ -81,7 +85,9 @@ __device__ __forceinline__ void store_digest(uint8_t* out, const uint32_t cv[8])
     for (int i = 0; i < 8; i++) o[i] = cv[i];  // little-endian words = the digest bytes
 }
 
-__global__ __launch_bounds__(256) void k_b3_groups(const uint8_t* __restrict__ data, const uint64_t* ctr,
+// PREFETCH: block b+1's words are loaded before block b is compressed (17 more VGPRs).
+template <bool PREFETCH, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_b3_groups(const uint8_t* __restrict__ data, const uint64_t* ctr,
                                                    BlobArrays b, uint32_t* __restrict__ cv_buf,
                                                    uint8_t* __restrict__ digests) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(256) void k_b3_groups(const uint8_t* __restrict__ d
         const uint64_t li = first + t, ls = start + li * B3_LEAF_BYTES;
         const uint64_t rest = len - li * B3_LEAF_BYTES;
         const uint32_t ll = len == 0 ? 0 : (uint32_t)(rest < B3_LEAF_BYTES ? rest : B3_LEAF_BYTES);
-        b3_leaf(data, ls, ll, bend, li, n == 1 ? B3_ROOT : 0, cv);
+        b3_leaf<PREFETCH>(data, ls, ll, bend, li, n == 1 ? B3_ROOT : 0, cv);
         if (t == 0 || t == 2) {
             uint32_t (*dst)[256] = t == 0 ? s_acc : s_sv;
 #pragma unroll
@@ -211,8 +217,8 @@ __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
                    uint64_t max_groups, uint32_t* cv_buf, uint8_t* digests, int max_leaves, hipEvent_t between) {
     if (!max_blobs) return;
-    hipLaunchKernelGGL(k_b3_groups, dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data, ctr, b,
-                       cv_buf, digests);
+    hipLaunchKernelGGL((k_b3_groups<true, 1>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data,
+                       ctr, b, cv_buf, digests);
     if (between) hipEventRecord(between, st);
     if (max_leaves > 4) {
         const uint32_t node_cap = (uint32_t)((max_leaves / 4) / 2 + 1);

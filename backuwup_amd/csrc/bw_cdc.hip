@@ -120,11 +120,12 @@ __device__ __forceinline__ void stage_hash_step(uint4 r0, uint4 r1, uint4 r2, ui
     }
 }
 
-__global__ __launch_bounds__(SCAN_BLOCK, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
                                                        uint64_t n_tiles, Masks mk,
                                                        uint32_t* __restrict__ tile_count,
                                                        uint64_t* __restrict__ tile_slots) {
-    constexpr int WAVES = SCAN_BLOCK / 64;
+    constexpr int WAVES = BLOCK / 64;
     // one LDS object so the gear table sits at LDS address 0 and every lookup address is the
     // v_perm result itself (a table at a non-zero base costs one v_add per byte)
     struct ScanLds {
@@ -220,14 +221,19 @@ __global__ __launch_bounds__(SCAN_BLOCK, 4) void k_scan(const uint8_t* __restric
     }
 }
 
+template <int BLOCK>
+static void launch_scan_t(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
+                          uint32_t* tile_count, uint64_t* tile_slots) {
+    uint64_t grid = (n_tiles + BLOCK / 64 - 1) / (BLOCK / 64);
+    if (grid > 512) grid = 512;  // persistent: every CU holds one block (LDS), two rounds
+    hipLaunchKernelGGL(k_scan<BLOCK>, dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes, n_tiles, mk, tile_count,
+                       tile_slots);
+}
+
 void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                  uint32_t* tile_count, uint64_t* tile_slots) {
     if (!n_tiles) return;
-    const uint64_t waves = (n_tiles + 0) ;
-    uint64_t grid = (waves + SCAN_BLOCK / 64 - 1) / (SCAN_BLOCK / 64);
-    if (grid > 512) grid = 512;  // persistent: 2 rounds of 256 CUs x 1 block
-    hipLaunchKernelGGL(k_scan, dim3((unsigned)grid), dim3(SCAN_BLOCK), 0, st, data, n_bytes, n_tiles, mk, tile_count,
-                       tile_slots);
+    launch_scan_t<SCAN_BLOCK>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots);
 }
 
 // ======================================================================== block scan helpers

@@ -30,7 +30,10 @@ class DeviceShardOps:
     """GPU implementation of the three local steps (all device-resident)."""
 
     def __init__(self, ctx, device):
+        # the collectives run on torch's current stream; the library must use the same stream so
+        # its kernels and the all-to-alls are ordered
         self.ctx, self.device = ctx, device
+        ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
 
     def partition(self, digests_ptr, n, world):
         out = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=self.device)

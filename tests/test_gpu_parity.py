@@ -221,3 +221,66 @@ def test_device_resident_batch(ctx, oracle):
     host = t.cpu().numpy()
     want = oracle.process_files(host, [0, 1000, 20 << 20], [1000, (20 << 20) - 1000, n - (20 << 20)])
     blobs_equal(got, want)
+
+
+def test_unmerged_chains_fall_back_exactly(ctx, oracle):
+    """Random prefix then zeros: the true chain's max-size phase differs from every speculative
+    chain's, so chains never merge and the serial walker must take over -- exactly."""
+    for pre, zeros, p in [(5000, 200_000, SMALL), (300_000, 2_000_000, MID), (3 << 20, 40 << 20, BK)]:
+        data = np.concatenate([splitmix_bytes(pre, pre), np.zeros(zeros, dtype=np.uint8)])
+        assert ctx.fastcdc_chunks(data, *p) == chunks_oracle(oracle, data, p), (pre, zeros)
+
+
+def test_candidate_dense_input(ctx, oracle):
+    """A period whose every window passes the prefilter: tiles overflow their slots and the exact
+    rescan + candidate-capacity retry paths run."""
+    from oracle import oracle as o
+    g = [int(x) for x in o.gear_table()]
+    # find a byte b whose constant window hash -GEAR[b]*(2^64-1)... passes mask_l for SMALL params
+    ms, ml = o.masks(*SMALL)
+    for b in range(256):
+        h = 0
+        for _ in range(64):
+            h = ((h << 1) + g[b]) & ((1 << 64) - 1)
+        if h & ml == 0:
+            break
+    else:
+        pytest.skip("no constant byte passes the mask")
+    data = np.full(3 << 20, b, dtype=np.uint8)
+    data[:1000] = splitmix_bytes(1, 1000)
+    assert ctx.fastcdc_chunks(data, *SMALL) == chunks_oracle(oracle, data, SMALL)
+
+
+def test_exchange_dedup_rccl_world1(ctx, oracle):
+    """The multi-GPU exchange (partition -> RCCL all-to-all -> owner decides -> all-to-all back ->
+    scatter) on one rank equals the inline index."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    from backuwup_amd.sharded import DeviceShardOps, exchange_dedup
+    from backuwup_amd.synth import small_files
+    if not dist.is_initialized():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    data, offs, lens = small_files(4000, seed=8)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.index_reset()
+    want = ctx.process_files(data, offs, lens)
+    ctx.index_reset()
+    dev = torch.from_numpy(data).cuda()
+    torch.cuda.synchronize()
+    ctx.submit_device(dev.data_ptr(), data.size, offs, lens, make_params(flags=BW_F_NO_DEDUP))
+    nb, d_dig, _ = ctx.device_views()
+    is_dup = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    exchange_dedup(DeviceShardOps(ctx, torch.device("cuda", 0)), d_dig, nb, is_dup.data_ptr(), 1,
+                   torch.device("cuda", 0))
+    torch.cuda.synchronize()
+    host = is_dup.cpu().numpy()
+    ctx.set_stream(0)  # back to the context's own stream
+    assert np.array_equal(host, want["is_dup"])
+    assert host.sum() > 0

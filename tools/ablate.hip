@@ -144,6 +144,8 @@ int main() {
     printf("copy_coalesced %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { launch_scan(0, d, n, tiles, mk, tc, ts); });
     printf("scan_full      %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { launch_scan_t<512>(0, d, n, tiles, mk, tc, ts); });
+    printf("scan_b512      %8.3f ms %8.1f GB/s (8-wave blocks: leaves LDS for a co-resident kernel)\n", t, gb / t * 1e3);
     t = timeit([&] { hipLaunchKernelGGL(scan_noload<true>, dim3(512), dim3(512), 0, 0, n, mk, out); });
     printf("scan_noload    %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { hipLaunchKernelGGL(scan_noload<false>, dim3(512), dim3(512), 0, 0, n, mk, out); });
@@ -171,6 +173,29 @@ int main() {
         t = timeit([&] { launch_blake3(0, d, ctr, b, nb, nb * groups_per, cv, dig, (int)(blen / 1024 + 1), nullptr); });
         printf("b3_full        %8.3f ms %8.1f GB/s (k_b3_groups + k_b3_tree, 4096 x 1 MiB blobs)\n", t,
                nb * blen / 1e9 / t * 1e3);
+        const unsigned g = (unsigned)((nb * groups_per + 255) / 256);
+#define B3V(P, W, name)                                                                                   \
+        t = timeit([&] { hipLaunchKernelGGL((k_b3_groups<P, W>), dim3(g), dim3(256), 0, 0, d, ctr, b, cv, dig); }); \
+        printf("%-14s %8.3f ms %8.1f GB/s (k_b3_groups only)\n", name, t, nb * blen / 1e9 / t * 1e3);
+        B3V(true, 1, "b3g_pf")
+        B3V(false, 1, "b3g_nopf")
+        B3V(false, 6, "b3g_nopf_w6")
+        B3V(false, 7, "b3g_nopf_w7")
+        B3V(true, 6, "b3g_pf_w6")
+#undef B3V
+        hipStream_t s1, s2;
+        CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+        CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        for (int blk : {1024, 512}) {
+            t = timeit([&] {
+                if (blk == 1024) launch_scan_t<1024>(s1, d, n, tiles, mk, tc, ts);
+                else launch_scan_t<512>(s1, d, n, tiles, mk, tc, ts);
+                launch_blake3(s2, d, ctr, b, nb, nb * groups_per, cv, dig, (int)(blen / 1024 + 1), nullptr);
+                CHECK(hipStreamSynchronize(s1));
+                CHECK(hipStreamSynchronize(s2));
+            });
+            printf("scan%-4d||b3   %8.3f ms (scan of 4 GiB concurrently with b3 of 4 GiB on two streams)\n", blk, t);
+        }
     }
     const uint64_t lanes = 256ull * 4096;
     const uint64_t bpl = n / 64 / lanes;
