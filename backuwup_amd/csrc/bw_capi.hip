@@ -134,6 +134,8 @@ static int make_masks(uint32_t mn, uint32_t av, uint32_t mx, Masks* mk) {
     mk->mask_s = H_MASKS[bits + 1];  // Normalization::Level1
     mk->mask_l = H_MASKS[bits - 1];
     mk->mask_pre = mk->mask_s & mk->mask_l;
+    mk->pre_shift = (uint32_t)__builtin_clzll(mk->mask_s | mk->mask_l);  // 63 - top bit
+    mk->pre_hi = (uint32_t)((mk->mask_pre << mk->pre_shift) >> 32);
     return BW_OK;
 }
 

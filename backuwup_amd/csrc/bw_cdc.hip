@@ -12,9 +12,12 @@
 // chunk's start+min need the truncated (chunk-local) hash.
 //
 // Pipeline (all on the stream, no host round trip):
-//   k_scan      gear hash at every byte, LDS lane-replicated table, per-tile candidate slots
+//   k_scan      gear hash at every byte, LDS lane-replicated table, one-v_and prefilter per
+//               byte, flagged 64-byte blocks per tile
+//   k_refine    exact candidates (pos | S | L) for the flagged blocks, per-tile slots in place
 //   k_tile_partial/k_tile_top  exclusive scan of per-tile counts -> candidate array offsets
-//   k_compact   copy slots; k_rescan handles (rare) overflowing tiles exactly
+//   k_rescan<false> exact counts of overflowed tiles (candidate-dense data, small parameters)
+//   k_compact   copy slots; k_rescan<true> writes the overflowed tiles' candidates
 //   k_chains    one wave per segment: speculative boundary chain from the segment start
 //   k_extend    continue each chain until it merges with the next segment's chain (CDC resync)
 //   k_resolve   prefix-max of merge points -> true chain entry of every segment, validity
@@ -53,6 +56,8 @@ __device__ __forceinline__ uint32_t mask_test(uint64_t h, uint32_t mlo, uint32_t
     return r;
 }
 
+// Exact normalized-chunking test of the plain gear state h at `pos`; a hit is appended to the
+// wave's LDS slots as pos | S | L.
 __device__ __forceinline__ void record_hit(uint64_t pos, uint64_t h, const Masks& mk, uint32_t* s_cnt,
                                            uint64_t* s_slots) {
     const bool S = (h & mk.mask_s) == 0, L = (h & mk.mask_l) == 0;
@@ -62,19 +67,27 @@ __device__ __forceinline__ void record_hit(uint64_t pos, uint64_t h, const Masks
     }
 }
 
-// Gear scan.  Each wavefront owns a 128 KiB sub-tile = 64 strips of 2 KiB, one per lane.  The
-// gear state is warmed up on the 64 bytes before the strip (after 64 steps it IS the windowed
-// hash), then every byte is tested.  Bytes reach the lanes coalesced: per 64-byte step, four
+// Gear scan.  The lanes carry the SHIFTED state h' = h << pre_shift (the LDS table holds
+// GEAR[b] << pre_shift; pre_shift = 63 - top mask bit, 16 at backuwup's parameters), so the
+// high dword of h' is the 32-bit window of h that holds the top mask bits, and the per-byte
+// prefilter is ONE v_and on it: (hi(h') & pre_hi) == 0 is implied by a real candidate (pre_hi =
+// the intersection mask's bits inside the window: 16 of mask_l's 19 at backuwup's parameters).
+// 128 positions fold into one min() per step; a step whose fold hits records only its 64-byte
+// block (rate ~64 * 2^-16 per lane-step), and k_refine turns flagged blocks into exact
+// candidates afterwards with every lane busy, instead of the whole wave replaying inside the
+// hot loop.
+//
+// Each wavefront owns a 128 KiB sub-tile = 64 strips of 2 KiB, one per lane.  The gear state
+// is warmed up on the 64 bytes before the strip (after 64 steps it IS the windowed hash), then
+// every byte is tested.  Bytes reach the lanes coalesced: per 64-byte step, four
 // global_load_dwordx4 fetch 16 strips x 64 B each (4 lanes per half line), the wave stages them
 // in its own padded LDS rows and every lane reads back its strip's 64 bytes (16 B per
 // ds_read_b128, conflict-free with 80-byte rows).  The next step's loads are in flight while
 // the current step is hashed (two register sets, unconditional loads so the vmcnt waits are
-// exact).  128 positions fold into one min() of the prefilter test; only a step with a hit in
-// some lane replays bytes to record it (~1e-4 per lane-step at backuwup's parameters).  No
-// block barrier after the table fill: candidates are collected per wave in LDS and published
-// by lane 0.
+// exact).  No block barrier after the table fill: records are collected per wave in LDS and
+// published by lane 0.
 __device__ __forceinline__ void hash_words(uint64_t& h, uint32_t& acc, const uint32_t (&ww)[16], uint32_t lane_off,
-                                           const uint64_t* s_gear, uint32_t mlo, uint32_t mhi) {
+                                           const uint64_t* s_gear, uint32_t phi) {
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
         uint64_t g[8];  // 8 independent LDS reads ahead of the serial recurrence
@@ -83,21 +96,21 @@ __device__ __forceinline__ void hash_words(uint64_t& h, uint32_t& acc, const uin
 #pragma unroll
         for (int q = 0; q < 8; q += 2) {
             h = (h << 1) + g[q];
-            const uint32_t t0 = mask_test(h, mlo, mhi);
+            const uint32_t t0 = (uint32_t)(h >> 32) & phi;
             h = (h << 1) + g[q + 1];
-            const uint32_t t1 = mask_test(h, mlo, mhi);
-            acc = min(acc, min(t0, t1));
+            const uint32_t t1 = (uint32_t)(h >> 32) & phi;
+            // one v_min3 per two positions (left to itself the compiler builds a v_min tree)
+            asm("v_min3_u32 %0, %1, %2, %3" : "=v"(acc) : "v"(acc), "v"(t0), "v"(t1));
         }
     }
 }
 
 // One 64-byte step of one lane: stage the wave's four coalesced loads, read back this lane's
-// strip bytes, hash them; on a prefilter hit replay the step byte by byte and record.
+// strip bytes, hash them; a prefilter hit records the block at `at`.
 __device__ __forceinline__ void stage_hash_step(uint4 r0, uint4 r1, uint4 r2, uint4 r3, uint8_t* wr,
-                                                const uint8_t* rd, uint64_t& h, uint64_t at,
-                                                const uint8_t* __restrict__ data, uint32_t lane_off,
-                                                const uint64_t* s_gear, uint32_t mlo, uint32_t mhi, const Masks& mk,
-                                                uint32_t* cnt, uint64_t* slots) {
+                                                const uint8_t* rd, uint64_t& h, uint64_t at, uint32_t lane_off,
+                                                const uint64_t* s_gear, uint32_t phi, uint32_t* cnt,
+                                                uint64_t* slots) {
     *(uint4*)(wr) = r0;
     *(uint4*)(wr + 16 * STAGE_ROW) = r1;
     *(uint4*)(wr + 32 * STAGE_ROW) = r2;
@@ -108,15 +121,11 @@ __device__ __forceinline__ void stage_hash_step(uint4 r0, uint4 r1, uint4 r2, ui
     __builtin_amdgcn_wave_barrier();
     const uint32_t ww[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
                              v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
-    const uint64_t h0 = h;
     uint32_t acc = 0xffffffffu;
-    hash_words(h, acc, ww, lane_off, s_gear, mlo, mhi);
+    hash_words(h, acc, ww, lane_off, s_gear, phi);
     if (__builtin_expect(acc == 0, 0)) {
-        uint64_t hh = h0;
-        for (int i = 0; i < SCAN_STEP; i++) {
-            hh = (hh << 1) + s_gear[(uint32_t)data[at + i] * GEAR_REP];
-            if (mask_test(hh, mlo, mhi) == 0) record_hit(at + i, hh, mk, cnt, slots);
-        }
+        const uint32_t i = atomicAdd(cnt, 1u);
+        if (i < (uint32_t)SCAN_CAP) slots[i] = at | BW_CAND_BLK;
     }
 }
 
@@ -139,11 +148,11 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
     uint8_t (*s_stage)[64 * STAGE_ROW] = lds.stage;
     uint64_t (*s_slots)[SCAN_CAP] = lds.slots;
     uint32_t* s_cnt = lds.cnt;
-    for (int i = threadIdx.x; i < 256 * GEAR_REP; i += blockDim.x) s_gear[i] = c_gear[i / GEAR_REP];
+    for (int i = threadIdx.x; i < 256 * GEAR_REP; i += blockDim.x) s_gear[i] = c_gear[i / GEAR_REP] << mk.pre_shift;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t lane_off = (lane & 31) * 8;
-    const uint32_t mlo = (uint32_t)mk.mask_pre, mhi = (uint32_t)(mk.mask_pre >> 32);
+    const uint32_t phi = mk.pre_hi;
     uint8_t* stage = s_stage[wid];
     uint32_t* cnt = &s_cnt[wid];
     uint64_t* slots = s_slots[wid];
@@ -188,24 +197,25 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
 #pragma unroll 1
             for (int step = 0; step < STEPS; step += 2) {
                 BW_LOAD4(b0, b1, b2, b3, step + 1);
-                stage_hash_step(a0, a1, a2, a3, wr, rd, h, ss + (uint64_t)step * SCAN_STEP, data, lane_off, s_gear,
-                                mlo, mhi, mk, cnt, slots);
+                stage_hash_step(a0, a1, a2, a3, wr, rd, h, ss + (uint64_t)step * SCAN_STEP, lane_off, s_gear, phi,
+                                cnt, slots);
                 BW_LOAD4(a0, a1, a2, a3, step + 2 < STEPS ? step + 2 : STEPS - 1);  // clamped, unused at the end
-                stage_hash_step(b0, b1, b2, b3, wr, rd, h, ss + (uint64_t)(step + 1) * SCAN_STEP, data, lane_off,
-                                s_gear, mlo, mhi, mk, cnt, slots);
+                stage_hash_step(b0, b1, b2, b3, wr, rd, h, ss + (uint64_t)(step + 1) * SCAN_STEP, lane_off, s_gear,
+                                phi, cnt, slots);
             }
 #undef BW_LOAD4
-        } else if (ss < n_bytes) {  // ragged last sub-tile: byte path
+        } else if (ss < n_bytes) {  // ragged last sub-tile: exact byte path (h' >> pre_shift is h
+                                    // modulo 2^(64 - pre_shift), which holds every mask bit)
             const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
             for (uint64_t p = ss >= 64 ? ss - 64 : 0; p < se; p++) {
                 h = (h << 1) + s_gear[(uint32_t)data[p] * GEAR_REP];
-                if (p >= ss && mask_test(h, mlo, mhi) == 0) record_hit(p, h, mk, cnt, slots);
+                if (p >= ss) record_hit(p, h >> mk.pre_shift, mk, cnt, slots);
             }
         }
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
             const uint32_t c = *cnt, n = c < (uint32_t)SCAN_CAP ? c : (uint32_t)SCAN_CAP;
-            for (uint32_t i = 1; i < n; i++) {  // insertion sort by position (n is ~0)
+            for (uint32_t i = 1; i < n; i++) {  // insertion sort by position (n is ~2)
                 uint64_t v = slots[i];
                 int k = (int)i - 1;
                 while (k >= 0 && BW_CAND_POS(slots[k]) > BW_CAND_POS(v)) {
@@ -219,6 +229,67 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
         }
         __builtin_amdgcn_wave_barrier();
     }
+}
+
+// Exact candidates for the 64-byte blocks the scan's prefilter flagged: one lane per tile,
+// rewriting the tile's slots in place (sorted, exact pos | S | L records).  A block is re-hashed
+// from 64 bytes before it (from 0 at the buffer start), exactly the history the scan's lane had.
+// A tile whose flags or exact candidates exceed SCAN_CAP joins the overflow list: k_rescan
+// counts (before the offset scan) and writes (after it) its candidates exactly.  Work: ~2
+// flagged blocks per 128 KiB tile on random data at backuwup's parameters.
+constexpr int REFINE_THREADS = 256;
+constexpr uint32_t TILE_OVF = 0x80000000u;  // tile_count flag: candidates come from k_rescan
+
+__device__ __forceinline__ void ovf_push(uint64_t t, uint32_t* ovf, uint64_t* ctr) {
+    const uint64_t k = atomicAdd((unsigned long long*)&ctr[C_NOVF], 1ull);
+    ovf[k] = (uint32_t)t;
+}
+
+__global__ __launch_bounds__(REFINE_THREADS) void k_refine(const uint8_t* __restrict__ data, uint64_t n_tiles,
+                                                           Masks mk, uint32_t* __restrict__ tile_count,
+                                                           uint64_t* __restrict__ tile_slots,
+                                                           uint32_t* __restrict__ ovf, uint64_t* ctr) {
+    __shared__ uint64_t lg[256];
+    __shared__ uint64_t s_in[REFINE_THREADS][SCAN_CAP];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = c_gear[i];
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * REFINE_THREADS + threadIdx.x;
+    if (t >= n_tiles) return;
+    const uint32_t c = tile_count[t];
+    if (c == 0) return;
+    if (c > (uint32_t)SCAN_CAP) {
+        ovf_push(t, ovf, ctr);
+        return;
+    }
+    uint64_t* sl = tile_slots + t * SCAN_CAP;
+    uint64_t* in = s_in[threadIdx.x];
+    for (uint32_t k = 0; k < c; k++) in[k] = sl[k];
+    if (!(in[0] & BW_CAND_BLK)) return;  // ragged tile: the scan recorded exact candidates
+    uint32_t w = 0;
+    for (uint32_t k = 0; k < c; k++) {
+        const uint64_t b = BW_CAND_POS(in[k]);
+        const uint64_t s = b >= 64 ? b - 64 : 0;
+        const uint4* wp = (const uint4*)(data + s);
+        uint64_t h = 0;
+        for (int q = 0; q < (int)((b + 64 - s) / 16); q++) {
+            const uint4 v = wp[q];
+            const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                h = (h << 1) + lg[(ww[j >> 2] >> (8 * (j & 3))) & 0xff];
+                const uint64_t p = s + 16 * (uint64_t)q + j;
+                if (p >= b) {
+                    const bool S = (h & mk.mask_s) == 0, L = (h & mk.mask_l) == 0;
+                    if (S || L) {
+                        if (w < (uint32_t)SCAN_CAP) sl[w] = p | (S ? BW_CAND_S : 0) | (L ? BW_CAND_L : 0);
+                        w++;
+                    }
+                }
+            }
+        }
+    }
+    if (w > (uint32_t)SCAN_CAP) ovf_push(t, ovf, ctr);
+    else tile_count[t] = w;
 }
 
 template <int BLOCK>
@@ -295,6 +366,7 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint32_t* __res
     } else {
         for (int k = 0; k < 4; k++) c[k] = i0 + k < n ? cnt[i0 + k] : 0;
     }
+    for (int k = 0; k < 4; k++) c[k] &= ~TILE_OVF;
     const uint64_t sum = (uint64_t)c[0] + c[1] + c[2] + c[3];
     uint64_t total;
     uint64_t run = block_excl_sum<TS_BLOCK>(sum, s, &total);
@@ -317,36 +389,35 @@ __global__ __launch_bounds__(BLK) void k_tile_top(uint64_t* __restrict__ btot, u
         off[n_tiles] = total;
         ctr[C_NCAND] = total < cap ? total : cap;
         ctr[C_CANDTOTAL] = total;
-        ctr[C_NOVF] = 0;
     }
 }
 
 __global__ void k_compact(const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ slots,
                           uint64_t* __restrict__ off, const uint64_t* __restrict__ bbase, uint64_t n_tiles,
-                          uint64_t* __restrict__ cand, uint64_t cap, uint32_t* __restrict__ ovf, uint64_t* ctr) {
+                          uint64_t* __restrict__ cand, uint64_t cap) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
     const uint64_t o = off[t] + bbase[t / (4 * TS_BLOCK)];
     off[t] = o;  // final offset: the walkers start their candidate cursor here
     const uint32_t c = cnt[t];
-    if (c <= (uint32_t)SCAN_CAP) {
+    if (!(c & TILE_OVF)) {  // overflowed tiles are written by k_rescan<true>
         for (uint32_t i = 0; i < c; i++)
             if (o + i < cap) cand[o + i] = slots[t * SCAN_CAP + i];
-    } else {
-        const uint64_t k = atomicAdd((unsigned long long*)&ctr[C_NOVF], 1ull);
-        ovf[k] = (uint32_t)t;
     }
 }
 
-// Exact ordered re-scan of a tile whose candidates overflowed the slots (pathological data).
+// Exact ordered re-scan of the tiles on the overflow list (candidate-dense data or small
+// parameters): WRITE = false counts a tile's candidates before the offset scan (tile_count =
+// count | TILE_OVF), WRITE = true stores them at the tile's offset after it.
 constexpr int RESCAN_THREADS = 256;
 constexpr uint64_t RESCAN_STRIP = SCAN_TILE / RESCAN_THREADS;
 
+template <bool WRITE>
 __global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __restrict__ data, uint64_t n_bytes,
                                                            Masks mk, const uint32_t* __restrict__ ovf,
                                                            const uint64_t* __restrict__ off,
                                                            uint64_t* __restrict__ cand, uint64_t cap,
-                                                           const uint64_t* ctr) {
+                                                           uint32_t* __restrict__ tile_count, const uint64_t* ctr) {
     __shared__ uint64_t s_gear[256];
     __shared__ uint64_t s_scan[RESCAN_THREADS];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) s_gear[i] = c_gear[i];
@@ -357,7 +428,7 @@ __global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __rest
         const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * RESCAN_STRIP;
         const uint64_t se = ss + RESCAN_STRIP < n_bytes ? ss + RESCAN_STRIP : n_bytes;
         uint64_t mine = 0;
-        for (int pass = 0; pass < 2; pass++) {
+        for (int pass = 0; pass < (WRITE ? 2 : 1); pass++) {
             uint64_t h = 0, w = 0;
             if (pass == 1) w = off[tile] + block_excl_sum<RESCAN_THREADS>(mine, s_scan, nullptr);
             if (ss < n_bytes) {
@@ -372,21 +443,30 @@ __global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __rest
                 }
             }
         }
+        if (!WRITE) {
+            uint64_t total;
+            block_excl_sum<RESCAN_THREADS>(mine, s_scan, &total);
+            if (threadIdx.x == 0) tile_count[tile] = (uint32_t)total | TILE_OVF;
+        }
         __syncthreads();
     }
 }
 
 void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
-                    const uint32_t* tile_count, const uint64_t* tile_slots, uint64_t* tile_off, uint64_t* cand,
+                    uint32_t* tile_count, uint64_t* tile_slots, uint64_t* tile_off, uint64_t* cand,
                     uint64_t cand_cap, uint32_t* ovf_list, uint64_t* ctr, uint64_t* btot) {
     if (!n_tiles) return;
     const uint64_t nb = (n_tiles + 4 * TS_BLOCK - 1) / (4 * TS_BLOCK);
+    hipLaunchKernelGGL(k_refine, dim3((unsigned)((n_tiles + REFINE_THREADS - 1) / REFINE_THREADS)),
+                       dim3(REFINE_THREADS), 0, st, data, n_tiles, mk, tile_count, tile_slots, ovf_list, ctr);
+    hipLaunchKernelGGL(k_rescan<false>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
+                       cand, cand_cap, tile_count, ctr);
     hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, tile_count, n_tiles, tile_off, btot);
     hipLaunchKernelGGL(k_tile_top, dim3(1), dim3(BLK), 0, st, btot, nb, n_tiles, tile_off, cand_cap, ctr);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count, tile_slots,
-                       tile_off, btot, n_tiles, cand, cand_cap, ovf_list, ctr);
-    hipLaunchKernelGGL(k_rescan, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
-                       cand, cand_cap, ctr);
+                       tile_off, btot, n_tiles, cand, cand_cap);
+    hipLaunchKernelGGL(k_rescan<true>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
+                       cand, cand_cap, tile_count, ctr);
 }
 
 // ======================================================================== the boundary walker

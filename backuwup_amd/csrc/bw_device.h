@@ -17,7 +17,8 @@
 // two top bits: bit 63 = (g & mask_s) == 0, bit 62 = (g & mask_l) == 0.
 #define BW_CAND_S (1ull << 63)
 #define BW_CAND_L (1ull << 62)
-#define BW_CAND_POS(c) ((c) & ((1ull << 62) - 1))
+#define BW_CAND_BLK (1ull << 61)  // scan record: a flagged 64-byte block (k_refine makes it exact)
+#define BW_CAND_POS(c) ((c) & ((1ull << 61) - 1))
 #define BW_NONE (~0ull)
 
 // ---------------------------------------------------------------- wave primitives

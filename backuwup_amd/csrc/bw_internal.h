@@ -33,6 +33,8 @@ enum Ctr : int {
 struct Masks {
     uint32_t min, avg, max, s0;  // s0 = 2 * (min / 2): first position the crate hashes
     uint64_t mask_s, mask_l, mask_pre;  // mask_pre = mask_s & mask_l (scan prefilter)
+    uint32_t pre_shift;  // the scan carries h << pre_shift; 63 - top bit of (mask_s | mask_l)
+    uint32_t pre_hi;     // bits of mask_pre inside the high dword of h << pre_shift
 };
 
 // One boundary-resolution segment: a window [start, end) of one CDC file.
@@ -72,7 +74,7 @@ struct BlobArrays {
 void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
                  const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots);
 void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
-                    const Masks& mk, const uint32_t* tile_count, const uint64_t* tile_slots,
+                    const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots,
                     uint64_t* tile_off, uint64_t* cand, uint64_t cand_cap, uint32_t* ovf_list,
                     uint64_t* ctr, uint64_t* scratch /* >= n_tiles / 1024 + 1 entries */);
 void launch_chains(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
