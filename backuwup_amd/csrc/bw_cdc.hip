@@ -82,10 +82,10 @@ __device__ __forceinline__ void record_hit(uint64_t pos, uint64_t h, const Masks
 // every byte is tested.  Bytes reach the lanes coalesced: per 64-byte step, four
 // global_load_dwordx4 fetch 16 strips x 64 B each (4 lanes per half line), the wave stages them
 // in its own padded LDS rows and every lane reads back its strip's 64 bytes (16 B per
-// ds_read_b128, conflict-free with 80-byte rows).  The next step's loads are in flight while
-// the current step is hashed (two register sets, unconditional loads so the vmcnt waits are
-// exact).  No block barrier after the table fill: records are collected per wave in LDS and
-// published by lane 0.
+// ds_read_b128, conflict-free with 80-byte rows).  Loads run one double step (128 B per strip)
+// ahead, both halves of each 128-byte line back to back (two register sets, unconditional loads
+// so the vmcnt waits are exact).  No block barrier after the table fill: records are collected
+// per wave in LDS and published by lane 0.
 __device__ __forceinline__ void hash_words(uint64_t& h, uint32_t& acc, const uint32_t (&ww)[16], uint32_t lane_off,
                                            const uint64_t* s_gear, uint32_t phi) {
 #pragma unroll
@@ -178,32 +178,41 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
                         for (int k = 0; k < 4; k++) gear_step(h, ww[j], BW_SEL(k), lane_off, s_gear);
                 }
             }
-            // lane L loads piece (L & 3) of strip 16 j + (L >> 2) for j = 0..3
-            const uint8_t* src = data + base + (uint64_t)(lane >> 2) * SCAN_STRIP + (lane & 3) * 16;
-            uint8_t* wr = stage + (lane >> 2) * STAGE_ROW + (lane & 3) * 16;
-            const uint8_t* rd = stage + lane * STAGE_ROW;
-            constexpr int STEPS = SCAN_STRIP / SCAN_STEP;
-            constexpr uint64_t JS = 16ull * SCAN_STRIP;
-#define BW_LOAD4(r0, r1, r2, r3, step)                                   \
-    do {                                                                 \
-        const uint8_t* s_ = src + (uint64_t)(step) * SCAN_STEP;          \
-        r0 = *(const uint4*)(s_);                                        \
-        r1 = *(const uint4*)(s_ + JS);                                   \
-        r2 = *(const uint4*)(s_ + 2 * JS);                               \
-        r3 = *(const uint4*)(s_ + 3 * JS);                               \
+            {
+                // Both 64-byte halves of every 128-byte line are requested back to back: the
+                // loads run one double step (two 64-byte steps) ahead, so the second half of a
+                // line meets the first half's miss in L2 instead of arriving one step later,
+                // after ~4 MiB of other waves' half-open lines per XCD have evicted it.
+                const uint8_t* src = data + base + (uint64_t)(lane >> 2) * SCAN_STRIP + (lane & 3) * 16;
+                uint8_t* wr = stage + (lane >> 2) * STAGE_ROW + (lane & 3) * 16;
+                const uint8_t* rd = stage + lane * STAGE_ROW;
+                constexpr int STEPS = SCAN_STRIP / SCAN_STEP;
+                constexpr uint64_t JS = 16ull * SCAN_STRIP;
+#define BW_LOAD8(r, ds)                                                                          \
+    do {                                                                                         \
+        const uint8_t* s_ = src + (uint64_t)(ds) * (2 * SCAN_STEP);                              \
+        _Pragma("unroll") for (int j = 0; j < 4; j++) {                                          \
+            r[j] = *(const uint4*)(s_ + j * JS);                                                 \
+            r[4 + j] = *(const uint4*)(s_ + SCAN_STEP + j * JS);                                 \
+        }                                                                                        \
     } while (0)
-            uint4 a0, a1, a2, a3, b0, b1, b2, b3;
-            BW_LOAD4(a0, a1, a2, a3, 0);
+                uint4 a[8], b[8];
+                BW_LOAD8(a, 0);
 #pragma unroll 1
-            for (int step = 0; step < STEPS; step += 2) {
-                BW_LOAD4(b0, b1, b2, b3, step + 1);
-                stage_hash_step(a0, a1, a2, a3, wr, rd, h, ss + (uint64_t)step * SCAN_STEP, lane_off, s_gear, phi,
-                                cnt, slots);
-                BW_LOAD4(a0, a1, a2, a3, step + 2 < STEPS ? step + 2 : STEPS - 1);  // clamped, unused at the end
-                stage_hash_step(b0, b1, b2, b3, wr, rd, h, ss + (uint64_t)(step + 1) * SCAN_STEP, lane_off, s_gear,
-                                phi, cnt, slots);
+                for (int ds = 0; ds < STEPS / 2; ds += 2) {
+                    BW_LOAD8(b, ds + 1);
+                    stage_hash_step(a[0], a[1], a[2], a[3], wr, rd, h, ss + (uint64_t)(2 * ds) * SCAN_STEP, lane_off,
+                                    s_gear, phi, cnt, slots);
+                    stage_hash_step(a[4], a[5], a[6], a[7], wr, rd, h, ss + (uint64_t)(2 * ds + 1) * SCAN_STEP,
+                                    lane_off, s_gear, phi, cnt, slots);
+                    BW_LOAD8(a, ds + 2 < STEPS / 2 ? ds + 2 : STEPS / 2 - 1);  // clamped, unused at the end
+                    stage_hash_step(b[0], b[1], b[2], b[3], wr, rd, h, ss + (uint64_t)(2 * ds + 2) * SCAN_STEP,
+                                    lane_off, s_gear, phi, cnt, slots);
+                    stage_hash_step(b[4], b[5], b[6], b[7], wr, rd, h, ss + (uint64_t)(2 * ds + 3) * SCAN_STEP,
+                                    lane_off, s_gear, phi, cnt, slots);
+                }
+#undef BW_LOAD8
             }
-#undef BW_LOAD4
         } else if (ss < n_bytes) {  // ragged last sub-tile: exact byte path (h' >> pre_shift is h
                                     // modulo 2^(64 - pre_shift), which holds every mask bit)
             const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
@@ -297,8 +306,8 @@ static void launch_scan_t(hipStream_t st, const uint8_t* data, uint64_t n_bytes,
                           uint32_t* tile_count, uint64_t* tile_slots) {
     uint64_t grid = (n_tiles + BLOCK / 64 - 1) / (BLOCK / 64);
     if (grid > 512) grid = 512;  // persistent: every CU holds one block (LDS), two rounds
-    hipLaunchKernelGGL(k_scan<BLOCK>, dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes, n_tiles, mk, tile_count,
-                       tile_slots);
+    hipLaunchKernelGGL((k_scan<BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes,
+                       n_tiles, mk, tile_count, tile_slots);
 }
 
 void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
