@@ -98,34 +98,78 @@ def tree_corpus(total_bytes, seed=0x6261636B, dup_fraction=0.30, min_file=4096, 
     return data, offs, np.array(lens, dtype=np.uint64)
 
 
+def _variant_plan(base_size, v, seed, n_indels, n_overwrites, max_indel):
+    """Edits of C3 variant v: 4 KiB overwrites [(at, bytes)] applied first, then the image is
+    re-assembled from parts: ("keep", start, end) ranges of the overwritten image and ("ins",
+    bytes) insertions (a deletion is a skipped range)."""
+    r = np.random.default_rng(seed * 7919 + v)
+    over = []
+    for _ in range(n_overwrites):
+        at = int(r.integers(0, max(1, base_size - 4096)))
+        over.append((at, r.integers(0, 256, 4096, dtype=np.uint8)))
+    edits = sorted(int(x) for x in r.integers(0, base_size, n_indels))
+    parts = []
+    prev = 0
+    for at in edits:
+        if at > prev:
+            parts.append(("keep", prev, at))
+        k = int(r.integers(1, max_indel + 1))
+        if r.integers(2):
+            parts.append(("ins", r.integers(0, 256, k, dtype=np.uint8)))
+            prev = max(prev, at)
+        else:
+            prev = max(prev, min(base_size, at + k))
+    if prev < base_size:
+        parts.append(("keep", prev, base_size))
+    return over, parts
+
+
+def _part_len(p):
+    return p[2] - p[1] if p[0] == "keep" else p[1].size
+
+
 def vm_image_variants(base_bytes, n_variants, seed=1, n_indels=32, n_overwrites=16, max_indel=64):
     """C3: a random base image plus variants with small insertions/deletions (byte shifts) and
     4 KiB overwrites.  Returns (data, file_off, file_len) with the base as file 0."""
-    rng = np.random.default_rng(seed)
     base = splitmix_bytes(seed, base_bytes)
     images = [base]
     for v in range(1, n_variants):
-        r = np.random.default_rng(seed * 7919 + v)
+        over, parts = _variant_plan(base_bytes, v, seed, n_indels, n_overwrites, max_indel)
         img = base.copy()
-        for _ in range(n_overwrites):
-            at = int(r.integers(0, max(1, img.size - 4096)))
-            img[at:at + 4096] = r.integers(0, 256, 4096, dtype=np.uint8)
-        edits = sorted(int(x) for x in r.integers(0, img.size, n_indels))
-        parts = []
-        prev = 0
-        for at in edits:
-            parts.append(img[prev:at])
-            k = int(r.integers(1, max_indel + 1))
-            if r.integers(2):
-                parts.append(r.integers(0, 256, k, dtype=np.uint8))
-                prev = at
-            else:
-                prev = min(img.size, at + k)
-        parts.append(img[prev:])
-        images.append(np.concatenate(parts))
+        for at, b in over:
+            img[at:at + b.size] = b[:img.size - at]
+        images.append(np.concatenate([img[p[1]:p[2]] if p[0] == "keep" else p[1] for p in parts]))
     offs = np.cumsum([0] + [im.size for im in images[:-1]]).astype(np.uint64)
     lens = np.array([im.size for im in images], dtype=np.uint64)
     return np.concatenate(images), offs, lens
+
+
+def vm_image_variants_torch(base_bytes, n_variants, device, seed=1, n_indels=32, n_overwrites=16, max_indel=64):
+    """The same corpus as vm_image_variants, assembled in HBM with device copies (C3 at 4 GiB x
+    16 = 64 GiB never touches the host).  Returns (uint8 tensor, file_off, file_len)."""
+    import torch
+    plans = [_variant_plan(base_bytes, v, seed, n_indels, n_overwrites, max_indel) for v in range(1, n_variants)]
+    lens = [base_bytes] + [sum(_part_len(p) for p in parts) for _, parts in plans]
+    offs = np.cumsum([0] + lens[:-1]).astype(np.uint64)
+    total = int(sum(lens))
+    out = torch.empty(total + 16, dtype=torch.uint8, device=device)
+    base = out[:base_bytes]
+    base.copy_(splitmix_torch(seed, base_bytes, device))
+    img = torch.empty(base_bytes, dtype=torch.uint8, device=device)
+    for v, (over, parts) in enumerate(plans, start=1):
+        img.copy_(base)
+        for at, b in over:
+            n = min(b.size, base_bytes - at)
+            img[at:at + n] = torch.from_numpy(b[:n]).to(device)
+        pos = int(offs[v])
+        for p in parts:
+            if p[0] == "keep":
+                out[pos:pos + p[2] - p[1]] = img[p[1]:p[2]]
+            else:
+                out[pos:pos + p[1].size] = torch.from_numpy(p[1]).to(device)
+            pos += _part_len(p)
+    del img
+    return out[:total], offs, np.array(lens, dtype=np.uint64)
 
 
 def small_files(n_files, seed=3, lo=4096, hi=65536, dup_fraction=0.30):
@@ -143,3 +187,16 @@ def small_files(n_files, seed=3, lo=4096, hi=65536, dup_fraction=0.30):
     for k, s in enumerate(src):
         data[int(offs[k]):int(offs[k]) + int(lens[k])] = blob[int(uniq_off[s]):int(uniq_off[s]) + int(sizes[s])]
     return data, offs, lens
+
+
+def small_files_table(n_files, seed=3, lo=4096, hi=65536, dup_fraction=0.30):
+    """C4's file table over a buffer holding only the distinct files back to back: copies alias
+    the bytes of their source (same content, hence same digest and dedup verdict as the laid-out
+    corpus of small_files).  Returns (unique_bytes, file_off, file_len)."""
+    rng = np.random.default_rng(seed)
+    n_uniq = int(round(n_files * (1 - dup_fraction)))
+    sizes = rng.integers(lo, hi + 1, n_uniq)
+    src = np.array(list(range(n_uniq)) + [int(x) for x in rng.integers(0, n_uniq, n_files - n_uniq)])
+    rng.shuffle(src)
+    uniq_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    return int(sizes.sum()), uniq_off[src], sizes[src].astype(np.uint64)

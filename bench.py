@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark: GB/s chunked + hashed + deduped (BASELINE.json metric) on configuration C2.
+"""Benchmark: GB/s chunked + hashed + deduped (BASELINE.json metric).
 
-C2 = a single 16 GiB random stream, device-resident (BASELINE.json configs[1]).  One step = one
-pass of the hot path over the stream: FastCDC-v2020 (256 KiB / 1 MiB / 3 MiB) -> BLAKE3 of every
-chunk -> seen-chunk index (fresh index per step: one backup session).  Inputs are generated on
-the GPU (counter-based splitmix64, seed 42 + rank) before timing, so the timed region starts
-with the bytes resident in HBM.
+Default workload C2 = a single 16 GiB random stream per GPU, device-resident (BASELINE.json
+configs[1]).  One step = one pass of the hot path over the batch: FastCDC-v2020 (256 KiB / 1 MiB /
+3 MiB) -> BLAKE3 of every chunk -> seen-chunk index (fresh index per step: one backup session).
+Inputs are generated on the GPU (counter-based splitmix64, seed 42 + rank) before timing, so the
+timed region starts with the bytes resident in HBM.
 
-N GPUs (weak scaling): every rank owns its own 16 GiB stream; the index is partitioned by digest
-prefix and each step exchanges digests with one RCCL all-to-all (and verdicts back).
+N GPUs (weak scaling): every rank owns its own stream; the index is partitioned by digest prefix
+and each step exchanges digests with RCCL all-to-alls (and verdicts back).
+
+Other configurations, for DESIGN.md / profiles -- the driver's line is C2:
+  --workload c1   1 GiB directory tree, 30% whole-file copies (the reference's CPU config)
+  --workload c3   VM images: 4 GiB base + 15 byte-shifted variants = 64 GiB (--gib scales the base)
+  --workload c4   1M small files of 4-64 KiB, 30% copies (copies alias their source's bytes)
+  --host-stream   the batch starts in pinned host memory: H2D copy of batch k+1 overlaps the
+                  processing of batch k (PCIe-inclusive rate; never the headline value)
 
 Prints one JSON line (rank 0).  Extra diagnostics go to stderr.
 """
@@ -23,10 +30,38 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GB/s chunked+hashed+deduped (whole node, 1/2/4/8 GPU), bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: PCIe Gen5 x16, 63 GB/s (spec)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def make_workload(name, gib, rank, dev, n_files):
+    """-> (device uint8 tensor, file_off, file_len, description).  Bytes are generated in HBM."""
+    import numpy as np
+    import torch
+    from backuwup_amd import synth
+    if name == "c2":
+        n = int(gib * (1 << 30))
+        data = synth.splitmix_torch(42 + rank, n, dev)
+        return data, [0], [n], ("C2: single %.0f GiB splitmix64 stream per GPU (seed 42+rank), device-resident; "
+                                "FastCDC v2020 256K/1M/3M -> BLAKE3 -> index" % gib)
+    if name == "c1":
+        d, o, l = synth.tree_corpus(int(gib * (1 << 30)), seed=0x6261636B + rank)
+        return torch.from_numpy(d).to(dev), o, l, ("C1: %.0f GiB directory tree per GPU, %d files (log-uniform "
+                                                    "4 KiB-64 MiB, 30%% whole-file copies)" % (gib, len(l)))
+    if name == "c3":
+        base = int(gib * (1 << 30))
+        data, o, l = synth.vm_image_variants_torch(base, 16, dev, seed=1 + rank)
+        return data, o, l, ("C3: VM images per GPU, %.1f GiB base + 15 variants (32 byte indels + 16 x 4 KiB "
+                            "overwrites each) = %.1f GiB" % (gib, data.numel() / 2**30))
+    if name == "c4":
+        u, o, l = synth.small_files_table(n_files, seed=3 + rank)
+        data = synth.splitmix_torch(3 + rank, u, dev)
+        return data, o, l, ("C4: %d small files per GPU (4-64 KiB uniform, 30%% copies aliasing their source), "
+                            "%.1f GB of file bytes" % (n_files, float(np.sum(l)) / 1e9))
+    raise SystemExit("unknown workload " + name)
 
 
 def main():
@@ -34,13 +69,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--gib", type=float, default=16.0, help="stream size per GPU (GiB)")
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4"])
+    ap.add_argument("--gib", type=float, default=None,
+                    help="C2: stream size per GPU; C1: corpus size; C3: base image size (GiB)")
+    ap.add_argument("--files", type=int, default=1000000, help="C4: files per GPU")
     ap.add_argument("--cpu-sample-gib", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--streams", type=int, default=1,
                     help="batches in flight: consecutive steps alternate between this many contexts/streams")
+    ap.add_argument("--host-stream", action="store_true",
+                    help="batches start in pinned host memory (H2D copies overlapped with processing)")
     args = ap.parse_args()
+    if args.gib is None:
+        args.gib = {"c1": 1.0, "c2": 16.0, "c3": 4.0, "c4": 0.0}[args.workload]
 
     import numpy as np
     import torch
@@ -48,7 +90,6 @@ def main():
 
     from backuwup_amd import Context, make_params
     from backuwup_amd._lib import BW_F_NO_DEDUP, STAGES
-    from backuwup_amd.synth import splitmix_torch
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -58,41 +99,67 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    n = int(args.gib * (1 << 30))
     t0 = time.time()
-    data = splitmix_torch(42 + rank, n, dev)
+    data, file_off, file_len, desc = make_workload(args.workload, args.gib, rank, dev, args.files)
     torch.cuda.synchronize()
-    log("rank %d: generated %.1f GiB in %.1f s" % (rank, n / 2**30, time.time() - t0))
+    n = int(data.numel())
+    processed = int(np.sum(np.asarray(file_len, dtype=np.uint64)))  # file bytes per step (C4 copies alias)
+    log("rank %d: %s -- generated in %.1f s" % (rank, desc, time.time() - t0))
 
+    nctx = 2 if args.host_stream else max(1, args.streams)
     ctxs, streams = [], []
-    for k in range(max(1, args.streams)):
+    for k in range(nctx):
         c = Context(local)
         st = torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)
         c.set_stream(st.cuda_stream)
         ctxs.append(c)
         streams.append(st)
     ctx = ctxs[0]
-    stream = streams[0]
     flags = BW_F_NO_DEDUP if world > 1 else 0
     params = make_params(flags=flags)
-    index_hint = 2 * (n // (256 << 10)) + 1024
+    index_hint = 2 * (processed // (256 << 10)) + len(file_len) + 1024
     owner_bits = world.bit_length() - 1
     assert world == 1 << owner_bits, "world size must be a power of two (digest-prefix owners)"
 
     from backuwup_amd.sharded import DeviceShardOps, exchange_dedup
+
+    # host-streamed mode: the batch lives in pinned host memory; batch k+1's copy (copy stream)
+    # overlaps batch k's processing; the two contexts alternate between two HBM buffers
+    host = None
+    if args.host_stream:
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        host.copy_(data)
+        bufs = [data, torch.empty_like(data)]
+        copy_stream = torch.cuda.Stream(dev)
+        copied = [torch.cuda.Event() for _ in range(2)]
+        done = [torch.cuda.Event() for _ in range(2)]
+        for e in done:
+            e.record(torch.cuda.current_stream(dev))
+
     step_no = [0]
 
     def step():
         k = step_no[0] % len(ctxs)
         step_no[0] += 1
         c = ctxs[k]
+        src = data
+        if host is not None:
+            b = k
+            copy_stream.wait_event(done[b])
+            with torch.cuda.stream(copy_stream):
+                bufs[b].copy_(host, non_blocking=True)
+                copied[b].record(copy_stream)
+            streams[k].wait_event(copied[b])
+            src = bufs[b]
         with torch.cuda.stream(streams[k]):
             c.index_reset(index_hint)
-            c.submit_device(data.data_ptr(), n, [0], [n], params)
+            c.submit_device(src.data_ptr(), n, file_off, file_len, params)
             if world > 1:
                 # digest all-to-all by owner = digest[0] >> (8 - log2 N); verdicts come back
                 nb, d_dig, d_dup = c.device_views()
                 exchange_dedup(DeviceShardOps(c, dev), d_dig, nb, d_dup, world, dev)
+            if host is not None:
+                done[k].record(streams[k])
 
     for _ in range(args.warmup):
         step()
@@ -100,22 +167,9 @@ def main():
 
     check = None
     if not args.no_check:
-        # bit-exactness spot check against the CPU oracle on the first 64 MiB of chunks
-        from oracle import oracle
-        res = ctx.results()
-        ends = np.cumsum(res["length"].astype(np.int64))
-        assert int(ends[-1]) == n and int(res["offset"][0]) == 0
-        k = int(np.searchsorted(ends, 64 << 20)) + 1
-        upto = int(ends[k - 1])
-        host = data[:upto + (4 << 20)].cpu().numpy()
-        want = oracle.fastcdc(host[:upto + (4 << 20)], 262144, 1048576, 3145728)
-        ok = all(want[i][1] == int(res["offset"][i]) and want[i][2] == int(res["length"][i]) and
-                 want[i][0] == int(res["gear_hash"][i]) for i in range(k - 1))
-        ok = ok and all(oracle.blake3(host[int(res["offset"][i]):int(res["offset"][i] + res["length"][i])]) ==
-                        bytes(res["digest"][i]) for i in range(k - 1))
-        check = {"chunks_checked": k - 1, "bytes_checked": int(ends[k - 2]), "bit_exact": bool(ok)}
+        check = parity_spot_check(args.workload, ctx, data, file_off, file_len, rank)
         log("rank %d: parity spot check %s" % (rank, check))
-        if not ok:
+        if not check["bit_exact"]:
             raise SystemExit("parity check failed")
 
     for c in ctxs:
@@ -139,36 +193,30 @@ def main():
     res = ctx.results()
     log("rank %d: %d blobs/step, stage ms/step: %s" % (rank, len(res), {k: round(v, 3) for k, v in per.items()}))
 
-    total_bytes = n * world * args.steps
+    total_bytes = processed * world * args.steps
     value = total_bytes / el / 1e9
     ms_per_step = el / args.steps * 1e3
 
-    # roofline for the dominant kernel (largest stage time); algorithmic traffic = every input byte
-    # read once per launch, so bytes per launch = n
+    # roofline for the dominant kernel (largest stage time); algorithmic traffic = every input
+    # byte read once per launch, so bytes per launch = the batch's file bytes
     dom = max(["scan", "b3_leaf"], key=lambda s: per[s])
-    achieved = n / (per[dom] * 1e-3) / 1e9
+    algo = processed if dom == "b3_leaf" else n
+    achieved = algo / (per[dom] * 1e-3) / 1e9
     kernel = {"scan": "k_scan", "b3_leaf": "k_b3_groups"}[dom]
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("gib") == args.gib and kernel in pmc.get("kernels", {}):
-                traffic = pmc["kernels"][kernel]["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
-                "algorithmic_bytes_per_launch": n,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, kernel), "kernel": kernel,
+                "algorithmic_bytes_per_launch": algo,
                 "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
+    if host is not None:
+        roofline.update({"host_stream_pcie_frac": round(value / PCIE_PEAK_GBS, 4)})
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         from oracle import oracle
         m = int(args.cpu_sample_gib * (1 << 30))
-        host = data[:m].cpu().numpy()
+        hb = data[:m].cpu().numpy()
         t1 = time.perf_counter()
-        r = oracle.process_files(host, [0], [m], threads=1)
+        r = oracle.process_files(hb, [0], [m], threads=1)
         ct = time.perf_counter() - t1
         cpu = {"value": round(m / ct / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
                "sample": "first %.0f GiB of the C2 stream as one file (%d blobs), oracle/bw_oracle.c "
@@ -179,15 +227,80 @@ def main():
         line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-                "config": {"workload": "C2: single %.0f GiB splitmix64 stream per GPU (seed 42+rank), "
-                                       "device-resident; FastCDC v2020 256K/1M/3M -> BLAKE3 -> index" % args.gib,
-                           "bytes_per_gpu": n, "blobs_per_gpu": int(len(res)),
+                "config": {"workload": desc + (" -- streamed from pinned host memory" if host is not None else ""),
+                           "bytes_per_gpu": processed, "blobs_per_gpu": int(len(res)),
+                           "files_per_gpu": len(file_len),
                            "parallelism": "dp%d (files sharded, index by digest prefix)" % world,
                            "batches_in_flight": len(ctxs)},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": check}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the same workload
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if args.workload != "c2" or args.host_stream or not os.path.exists(path):
+        return None
+    try:
+        pmc = json.load(open(path))
+        if pmc.get("gib") == args.gib and kernel in pmc.get("kernels", {}):
+            return pmc["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def parity_spot_check(workload, ctx, data, file_off, file_len, rank):
+    """Bit-exactness against the CPU oracle on the first ~64 MiB of blobs (C2) or on a sample of
+    files (other workloads), from the last warm-up batch's results."""
+    import numpy as np
+    from oracle import oracle
+    res = ctx.results()
+    if workload == "c2":
+        n = int(file_len[0])
+        ends = np.cumsum(res["length"].astype(np.int64))
+        assert int(ends[-1]) == n and int(res["offset"][0]) == 0
+        k = int(np.searchsorted(ends, 64 << 20)) + 1
+        upto = int(ends[k - 1])
+        host = data[:upto + (4 << 20)].cpu().numpy()
+        want = oracle.fastcdc(host, 262144, 1048576, 3145728)
+        ok = all(want[i][1] == int(res["offset"][i]) and want[i][2] == int(res["length"][i]) and
+                 want[i][0] == int(res["gear_hash"][i]) for i in range(k - 1))
+        ok = ok and all(oracle.blake3(host[int(res["offset"][i]):int(res["offset"][i] + res["length"][i])]) ==
+                        bytes(res["digest"][i]) for i in range(k - 1))
+        return {"chunks_checked": k - 1, "bytes_checked": int(ends[k - 2]), "bit_exact": bool(ok)}
+    # sample files: each file's blobs re-derived by the oracle (chunking + digests; dedup verdicts
+    # need the whole batch and are covered by tests/test_gpu_configs.py)
+    rng = np.random.default_rng(rank)
+    nf = len(file_len)
+    pick = sorted(set(rng.integers(0, nf, min(nf, 64)).tolist()))
+    fo = np.asarray(file_off, dtype=np.uint64)
+    fl = np.asarray(file_len, dtype=np.uint64)
+    ok, nb, nbytes = True, 0, 0
+    for f in pick:
+        got = res[res["file"] == f]
+        if int(fl[f]) > (256 << 20):
+            # a large file: its blobs up to 64 MiB, from the file start (CDC restarts per file)
+            ends = np.cumsum(got["length"].astype(np.int64))
+            k = int(np.searchsorted(ends, 64 << 20)) + 1
+            host = data[int(fo[f]):int(fo[f]) + int(ends[k - 1]) + (4 << 20)].cpu().numpy()
+            want = oracle.fastcdc(host, 262144, 1048576, 3145728)[:k - 1]
+            got = got[:k - 1]
+            ok = ok and [(int(g["gear_hash"]), int(g["offset"]), int(g["length"])) for g in got] == want and \
+                all(oracle.blake3(host[int(g["offset"]):int(g["offset"] + g["length"])]) == bytes(g["digest"])
+                    for g in got)
+            nbytes += int(ends[k - 2])
+        else:
+            host = data[int(fo[f]):int(fo[f] + fl[f])].cpu().numpy()
+            want = oracle.process_files(host, [0], [int(fl[f])])
+            ok = ok and len(got) == len(want) and np.array_equal(got["length"], want["length"]) and \
+                np.array_equal(got["digest"], want["digest"]) and np.array_equal(got["gear_hash"], want["gear_hash"])
+            nbytes += int(fl[f])
+        nb += len(got)
+    return {"files_checked": len(pick), "blobs_checked": nb, "bytes_checked": nbytes, "bit_exact": bool(ok)}
 
 
 if __name__ == "__main__":

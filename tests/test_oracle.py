@@ -160,3 +160,4 @@ def test_golden_generator_agrees_on_small_cases():
         assert [list(c) for c in mg.fastcdc_py(d, v["min"], v["avg"], v["max"])] == v["chunks"]
     for v in VEC["blake3"][:12]:
         assert mg.blake3_py(bytes(i % 251 for i in range(v["len"]))).hex() == v["digest"]
+
