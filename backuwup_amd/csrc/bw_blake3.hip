@@ -12,7 +12,8 @@
 //                parents, all lanes busy).  Blobs of <= 4 leaves finish here (ROOT in-lane);
 //                otherwise the lane stores the level-2 node, or for a blob's ragged last group
 //                the merged tail of the spine (bits 0..1 of n).
-//   k_b3_tree    one workgroup per blob with n > 4: the remaining levels in LDS + the spine.
+//   k_b3_small   one lane per blob with 4 < n <= 64: the remaining levels on an in-place stack.
+//   k_b3_tree    one wave per blob with n > 64: the remaining levels in LDS + the spine.
 #include "bw_device.h"
 #include "bw_internal.h"
 
@@ -150,7 +151,64 @@ __global__ __launch_bounds__(256, MINW) void k_b3_groups(const uint8_t* __restri
     }
 }
 
-// Upper levels of one blob (n > 4 leaves), one wavefront per blob.  Level-2 nodes come from
+// Upper levels of a small blob (4 < n <= B3_SMALL_LEAVES leaves), one lane per blob: a batch of
+// many small files (C4) keeps every lane busy instead of one wave per blob with <= 8 lanes
+// active.  The level-2 nodes are merged left to right on a stack of complete subtrees that lives
+// in the blob's own cv_buf slots (slot d < node i, so it only overwrites consumed nodes); the
+// stack is then folded from the right onto the ragged tail (bits 0..1 of n).  The merge that
+// completes a power-of-two blob, or the last fold, carries ROOT.
+constexpr uint64_t B3_SMALL_LEAVES = 64;
+
+__global__ __launch_bounds__(256) void k_b3_small(const uint64_t* ctr, BlobArrays b, uint32_t* __restrict__ cv_buf,
+                                                  uint8_t* __restrict__ digests) {
+    const uint64_t blob = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blob >= ctr[C_NBLOBS]) return;
+    const uint64_t len = b.len[blob];
+    const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
+    if (n <= 4 || n > B3_SMALL_LEAVES) return;
+    uint32_t* g = cv_buf + b.goff[blob] * 8;
+    const uint32_t m2 = (uint32_t)(n / 4);
+    const bool tail = (n & 3) != 0;
+    uint32_t depth = 0;
+    for (uint32_t i = 0; i < m2; i++) {
+        uint32_t carry[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) carry[w] = g[i * 8 + w];
+        for (uint32_t c = i + 1; (c & 1) == 0; c >>= 1) {
+            uint32_t l[8];
+            depth--;
+#pragma unroll
+            for (int w = 0; w < 8; w++) l[w] = g[depth * 8 + w];
+            b3_parent(l, carry, (!tail && i + 1 == m2 && depth == 0) ? B3_ROOT : 0, carry);
+        }
+#pragma unroll
+        for (int w = 0; w < 8; w++) g[depth * 8 + w] = carry[w];
+        depth++;
+    }
+    uint32_t acc[8];
+    bool have = false;
+    if (tail) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) acc[w] = g[m2 * 8 + w];
+        have = true;
+    }
+    while (depth > 0) {
+        depth--;
+        uint32_t t[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) t[w] = g[depth * 8 + w];
+        if (!have) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) acc[w] = t[w];
+            have = true;
+        } else {
+            b3_parent(t, acc, depth == 0 ? B3_ROOT : 0, acc);
+        }
+    }
+    store_digest(digests + blob * 32, acc);
+}
+
+// Upper levels of one larger blob (n > B3_SMALL_LEAVES leaves), one wavefront per blob.  Level-2 nodes come from
 // k_b3_groups (global); level 3 is built into the wave's LDS region, later levels in place, 64
 // parents per pass (a wave's LDS accesses execute in order, and pass p reads nodes
 // [128p, 128p+128) while writing [64p, 64p+64), so the in-place update is safe).  Lane 0 folds
@@ -167,7 +225,7 @@ __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays
     for (uint64_t blob = (uint64_t)blockIdx.x * wpb + wave; blob < nblobs; blob += stride) {
         const uint64_t len = b.len[blob];
         const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
-        if (n <= 4) continue;
+        if (n <= B3_SMALL_LEAVES) continue;  // k_b3_small
         const uint32_t* lvl2 = cv_buf + b.goff[blob] * 8;
         uint64_t cnt = n / 4;
         uint32_t acc[8];
@@ -220,7 +278,10 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     hipLaunchKernelGGL((k_b3_groups<true, 1>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data,
                        ctr, b, cv_buf, digests);
     if (between) hipEventRecord(between, st);
-    if (max_leaves > 4) {
+    if (max_leaves > 4)
+        hipLaunchKernelGGL(k_b3_small, dim3((unsigned)((max_blobs + 255) / 256)), dim3(256), 0, st, ctr, b, cv_buf,
+                           digests);
+    if (max_leaves > (int)B3_SMALL_LEAVES) {
         const uint32_t node_cap = (uint32_t)((max_leaves / 4) / 2 + 1);
         uint32_t wpb = (48u << 10) / (node_cap * 32);
         wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);

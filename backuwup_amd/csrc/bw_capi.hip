@@ -43,7 +43,7 @@ struct bw_ctx {
     DevBuf tile_count, tile_slots, tile_off, tile_btot, cand, ovf, ctr;
     DevBuf segs, cfiles, units, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
-    DevBuf cv, digests, is_dup, packed, fstart, data, scratch;
+    DevBuf cv, digests, is_dup, packed, fstart, data, scratch, ucnt, ubtot;
     PinBuf stage;
 
     // persistent dedup index
@@ -218,7 +218,8 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->cfiles, &c->units, &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->digests,
-                     &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->table, &c->log, &c->dstate};
+                     &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->table,
+                     &c->log, &c->dstate};
     for (DevBuf* b : all)
         if (b->p) hipFree(b->p);
     if (c->stage.p) hipHostFree(c->stage.p);
@@ -466,6 +467,8 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     rc |= ensure(c, c->is_dup, max_blobs);
     rc |= ensure(c, c->packed, max_blobs * sizeof(bw_blob));
     rc |= ensure(c, c->fstart, nf * 8);
+    rc |= ensure(c, c->ucnt, 2 * nunits * 8);
+    rc |= ensure(c, c->ubtot, 2 * (nunits / 1024 + 2) * 8);
     if (rc) return BW_ENOMEM;
     // candidate array: 4x the expected count (2^-popcount(mask) per byte) plus slack; a batch
     // that finds more is re-run by bw_results with the exact count (pathological inputs only)
@@ -528,8 +531,9 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     }
     prof_mark(c, BW_STAGE_ASSEMBLE);
     launch_assemble(st, ctr, P<UnitDesc>(c->units), nunits, P<SegDesc>(c->segs), P<CFileDesc>(c->cfiles),
-                    P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
-                    P<uint32_t>(c->cf_invalid), P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), b, max_blobs);
+                    P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->seg_M), P<uint32_t>(c->cf_invalid),
+                    P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), b, P<uint64_t>(c->ucnt),
+                    P<uint64_t>(c->ubtot));
     if (ncf) launch_cut_hash(st, d_data, mk, ctr, b, max_blobs);
     else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, st));
 

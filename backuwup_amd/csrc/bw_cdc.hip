@@ -22,7 +22,7 @@
 //   k_extend    continue each chain until it merges with the next segment's chain (CDC resync)
 //   k_resolve   prefix-max of merge points -> true chain entry of every segment, validity
 //   k_fallback  serial wave walker for files whose chains did not merge (exact, slower)
-//   k_assemble  canonical-order blob table + BLAKE3 group offsets
+//   k_unit_*    canonical-order blob table + BLAKE3 group offsets (count, scan, emit)
 //   k_cut_hash  Chunk.hash (the crate's returned gear state) for every CDC chunk
 #include "bw_device.h"
 #include "bw_internal.h"
@@ -277,12 +277,18 @@ __global__ __launch_bounds__(REFINE_THREADS) void k_refine(const uint8_t* __rest
     uint32_t w = 0;
     for (uint32_t k = 0; k < c; k++) {
         const uint64_t b = BW_CAND_POS(in[k]);
+        // the block and the 64 bytes before it (from 0 at the buffer start, where b == 0): all
+        // eight loads in flight at once
         const uint64_t s = b >= 64 ? b - 64 : 0;
         const uint4* wp = (const uint4*)(data + s);
+        uint4 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = wp[b >= 64 ? q : (q & 3)];
         uint64_t h = 0;
-        for (int q = 0; q < (int)((b + 64 - s) / 16); q++) {
-            const uint4 v = wp[q];
-            const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            if (b < 64 && q >= 4) break;
+            const uint32_t ww[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
             for (int j = 0; j < 16; j++) {
                 h = (h << 1) + lg[(ww[j >> 2] >> (8 * (j & 3))) & 0xff];
@@ -778,35 +784,78 @@ __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDe
     if (prev != BW_NONE) emit(prev, R, 1, sd.file_end);
 }
 
-__global__ __launch_bounds__(BLK) void k_assemble(uint64_t* ctr, const UnitDesc* __restrict__ units, uint64_t nunits,
-                                                  const SegDesc* __restrict__ segs,
-                                                  const CFileDesc* __restrict__ cfiles,
-                                                  const uint64_t* __restrict__ chains,
-                                                  const uint32_t* __restrict__ chain_n,
-                                                  const uint64_t* __restrict__ seg_M,
-                                                  const uint32_t* __restrict__ cf_invalid,
-                                                  const uint64_t* __restrict__ fb_starts,
-                                                  const uint64_t* __restrict__ fb_count, BlobArrays b) {
+// Canonical blob table over all units, in three passes so a batch of a million small files
+// (C4) spreads over the chip: per-unit blob/group counts (one thread per unit), a two-level
+// exclusive scan of the counts (1024 units per block, then one block over the block totals),
+// and the emit pass writing each unit's blobs at its offsets.
+constexpr int AS_BLOCK = 256;                      // threads per block, 4 units each
+constexpr uint64_t AS_UNITS = 4ull * AS_BLOCK;     // units per partial-scan block
+
+__global__ __launch_bounds__(256) void k_unit_count(const UnitDesc* __restrict__ units, uint64_t nunits,
+                                                    const SegDesc* __restrict__ segs,
+                                                    const CFileDesc* __restrict__ cfiles,
+                                                    const uint64_t* __restrict__ chains,
+                                                    const uint32_t* __restrict__ chain_n,
+                                                    const uint64_t* __restrict__ seg_M,
+                                                    const uint32_t* __restrict__ cf_invalid,
+                                                    const uint64_t* __restrict__ fb_starts,
+                                                    const uint64_t* __restrict__ fb_count, BlobArrays b,
+                                                    uint64_t* __restrict__ ucb, uint64_t* __restrict__ ucg) {
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nunits) return;
+    uint64_t nb, ng;
+    unit_blobs<false>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, 0, 0, nb, ng);
+    ucb[u] = nb;
+    ucg[u] = ng;
+}
+
+__global__ __launch_bounds__(AS_BLOCK) void k_unit_partial(uint64_t* __restrict__ ucb, uint64_t* __restrict__ ucg,
+                                                           uint64_t n, uint64_t* __restrict__ bt_b,
+                                                           uint64_t* __restrict__ bt_g) {
+    __shared__ uint64_t s[AS_BLOCK];
+    const uint64_t i0 = ((uint64_t)blockIdx.x * AS_BLOCK + threadIdx.x) * 4;
+    uint64_t cb[4], cg[4], sb = 0, sg = 0;
+    for (int k = 0; k < 4; k++) {
+        cb[k] = i0 + k < n ? ucb[i0 + k] : 0;
+        cg[k] = i0 + k < n ? ucg[i0 + k] : 0;
+        sb += cb[k];
+        sg += cg[k];
+    }
+    uint64_t tb, tg;
+    uint64_t rb = block_excl_sum<AS_BLOCK>(sb, s, &tb);
+    uint64_t rg = block_excl_sum<AS_BLOCK>(sg, s, &tg);
+    for (int k = 0; k < 4; k++)
+        if (i0 + k < n) {
+            ucb[i0 + k] = rb;
+            ucg[i0 + k] = rg;
+            rb += cb[k];
+            rg += cg[k];
+        }
+    if (threadIdx.x == 0) {
+        bt_b[blockIdx.x] = tb;
+        bt_g[blockIdx.x] = tg;
+    }
+}
+
+__global__ __launch_bounds__(BLK) void k_unit_top(uint64_t* __restrict__ bt_b, uint64_t* __restrict__ bt_g,
+                                                  uint64_t nb, uint64_t* ctr) {
     __shared__ uint64_t s[BLK];
-    const uint64_t per = (nunits + BLK - 1) / BLK, lo = threadIdx.x * per;
-    const uint64_t hi = lo + per < nunits ? lo + per : nunits;
-    uint64_t tb = 0, tg = 0;
-    for (uint64_t u = lo; u < hi; u++) {
-        uint64_t nb, ng;
-        unit_blobs<false>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, 0, 0,
-                          nb, ng);
-        tb += nb;
-        tg += ng;
+    const uint64_t per = (nb + BLK - 1) / BLK, lo = threadIdx.x * per;
+    const uint64_t hi = lo + per < nb ? lo + per : nb;
+    uint64_t sb = 0, sg = 0;
+    for (uint64_t i = lo; i < hi; i++) {
+        sb += bt_b[i];
+        sg += bt_g[i];
     }
     uint64_t totb, totg;
-    uint64_t bb = block_excl_sum<BLK>(tb, s, &totb);
-    uint64_t gb = block_excl_sum<BLK>(tg, s, &totg);
-    for (uint64_t u = lo; u < hi; u++) {
-        uint64_t nb, ng;
-        unit_blobs<true>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, bb, gb,
-                         nb, ng);
-        bb += nb;
-        gb += ng;
+    uint64_t rb = block_excl_sum<BLK>(sb, s, &totb);
+    uint64_t rg = block_excl_sum<BLK>(sg, s, &totg);
+    for (uint64_t i = lo; i < hi; i++) {
+        const uint64_t tb = bt_b[i], tg = bt_g[i];
+        bt_b[i] = rb;
+        bt_g[i] = rg;
+        rb += tb;
+        rg += tg;
     }
     if (threadIdx.x == 0) {
         ctr[C_NBLOBS] = totb;
@@ -815,14 +864,42 @@ __global__ __launch_bounds__(BLK) void k_assemble(uint64_t* ctr, const UnitDesc*
     }
 }
 
+__global__ __launch_bounds__(256) void k_unit_emit(const UnitDesc* __restrict__ units, uint64_t nunits,
+                                                   const SegDesc* __restrict__ segs,
+                                                   const CFileDesc* __restrict__ cfiles,
+                                                   const uint64_t* __restrict__ chains,
+                                                   const uint32_t* __restrict__ chain_n,
+                                                   const uint64_t* __restrict__ seg_M,
+                                                   const uint32_t* __restrict__ cf_invalid,
+                                                   const uint64_t* __restrict__ fb_starts,
+                                                   const uint64_t* __restrict__ fb_count, BlobArrays b,
+                                                   const uint64_t* __restrict__ ucb, const uint64_t* __restrict__ ucg,
+                                                   const uint64_t* __restrict__ bt_b,
+                                                   const uint64_t* __restrict__ bt_g) {
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nunits) return;
+    const uint64_t bb = ucb[u] + bt_b[u / AS_UNITS], gb = ucg[u] + bt_g[u / AS_UNITS];
+    uint64_t nb, ng;
+    unit_blobs<true>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, bb, gb, nb,
+                     ng);
+}
+
 void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint64_t nunits, const SegDesc* segs,
                      const CFileDesc* cfiles, const uint64_t* chains, const uint32_t* chain_n, const uint64_t* seg_M,
-                     const uint32_t* seg_cnt, const uint32_t* cf_invalid, const uint64_t* fb_starts,
-                     const uint64_t* fb_count, BlobArrays b, uint64_t max_blobs) {
-    (void)seg_cnt;
-    (void)max_blobs;
-    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(BLK), 0, st, ctr, units, nunits, segs, cfiles, chains, chain_n,
-                       seg_M, cf_invalid, fb_starts, fb_count, b);
+                     const uint32_t* cf_invalid, const uint64_t* fb_starts, const uint64_t* fb_count, BlobArrays b,
+                     uint64_t* ucnt, uint64_t* ubtot) {
+    const uint64_t nblk = (nunits + AS_UNITS - 1) / AS_UNITS;
+    uint64_t *ucb = ucnt, *ucg = ucnt + nunits, *bt_b = ubtot, *bt_g = ubtot + nblk + 1;
+    const unsigned g = (unsigned)((nunits + 255) / 256);
+    if (nunits) {
+        hipLaunchKernelGGL(k_unit_count, dim3(g), dim3(256), 0, st, units, nunits, segs, cfiles, chains, chain_n, seg_M,
+                           cf_invalid, fb_starts, fb_count, b, ucb, ucg);
+        hipLaunchKernelGGL(k_unit_partial, dim3((unsigned)nblk), dim3(AS_BLOCK), 0, st, ucb, ucg, nunits, bt_b, bt_g);
+    }
+    hipLaunchKernelGGL(k_unit_top, dim3(1), dim3(BLK), 0, st, bt_b, bt_g, nblk, ctr);
+    if (nunits)
+        hipLaunchKernelGGL(k_unit_emit, dim3(g), dim3(256), 0, st, units, nunits, segs, cfiles, chains, chain_n, seg_M,
+                           cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g);
 }
 
 // ======================================================================== Chunk.hash

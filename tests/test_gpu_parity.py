@@ -48,6 +48,18 @@ def test_blake3_lengths(ctx, oracle):
         assert ctx.blake3(msg) == oracle.blake3(msg), n
 
 
+def test_blake3_tree_shapes_batched(ctx, oracle):
+    # every leaf count around the group (4 leaves), lane-per-blob (<= 64 leaves) and wave-per-blob
+    # tree paths, ragged and exact, hashed in one batch
+    lens = [k * 1024 + d for k in range(1, 140) for d in (-1, 0, 1)]
+    data = splitmix_bytes(17, sum(lens) + 64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) + 3
+    got = ctx.blake3_many(data, offs, lens)
+    for i, l in enumerate(lens):
+        o = int(offs[i])
+        assert bytes(got[i]) == oracle.blake3(data[o:o + l]), l
+
+
 def test_blake3_many_unaligned(ctx, oracle):
     rng = np.random.default_rng(7)
     data = splitmix_bytes(11, 6 << 20)
