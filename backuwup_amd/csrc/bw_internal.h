@@ -7,9 +7,15 @@ namespace bw {
 
 // ------------------------------------------------------------------ tunables
 constexpr int SCAN_BLOCK = 1024;                                   // 16 waves, 1 block per CU (LDS)
-constexpr int SCAN_STRIP = 2048;                                   // bytes per lane
-constexpr uint64_t SCAN_TILE = 64ull * SCAN_STRIP;                 // one wave's 128 KiB sub-tile
-constexpr int SCAN_CAP = 16;                                       // candidate slots per tile
+#ifndef BW_SCAN_STRIP
+#define BW_SCAN_STRIP 2048
+#endif
+#ifndef BW_SCAN_CAP
+#define BW_SCAN_CAP 16
+#endif
+constexpr int SCAN_STRIP = BW_SCAN_STRIP;                          // bytes per lane
+constexpr uint64_t SCAN_TILE = 64ull * SCAN_STRIP;                 // one wave's sub-tile (128 KiB)
+constexpr int SCAN_CAP = BW_SCAN_CAP;                              // candidate slots per tile
 constexpr int SCAN_STEP = 64;                                      // bytes per lane per staged step
 constexpr int STAGE_ROW = SCAN_STEP + 16;                          // padded LDS staging row
 constexpr int GEAR_REP = 32;                                      // LDS gear replicas
