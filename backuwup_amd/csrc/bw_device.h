@@ -79,16 +79,31 @@ __device__ __forceinline__ uint32_t b3_rotr(uint32_t x, int n) { return __builti
 #define B3_IV6 0x1F83D9ABu
 #define B3_IV7 0x5BE0CD19u
 
+// The two-operand xor / add of G are emitted in their VOP3 (e64) encodings: on gfx950 they issue
+// faster than the VOP2 (e32) forms the compiler picks (tools/op_rate.hip: 2.7 vs 3.2-3.6 SIMD
+// cycles per wave64 instruction at full occupancy; BLAKE3 from registers 4.05 vs 3.68 TB/s at 4
+// waves/SIMD, tools/valu_rate.hip).  Non-volatile asm: the compiler still schedules them.
+__device__ __forceinline__ uint32_t b3_xor(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_xor_b32_e64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t b3_add(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_add_u32_e64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 #define B3_G(a, b, c, d, x, y)            \
     do {                                  \
         a = a + b + (x);                  \
-        d = b3_rotr(d ^ a, 16);           \
-        c = c + d;                        \
-        b = b3_rotr(b ^ c, 12);           \
+        d = b3_rotr(b3_xor(d, a), 16);    \
+        c = b3_add(c, d);                 \
+        b = b3_rotr(b3_xor(b, c), 12);    \
         a = a + b + (y);                  \
-        d = b3_rotr(d ^ a, 8);            \
-        c = c + d;                        \
-        b = b3_rotr(b ^ c, 7);            \
+        d = b3_rotr(b3_xor(d, a), 8);     \
+        c = b3_add(c, d);                 \
+        b = b3_rotr(b3_xor(b, c), 7);     \
     } while (0)
 
 // One round on state v with the message words in schedule order s0..s15 (compile-time names).
@@ -119,8 +134,8 @@ __device__ __forceinline__ void b3_compress(uint32_t cv[8], const uint32_t m[16]
     B3_ROUND(m, 12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4);
     B3_ROUND(m, 9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7);
     B3_ROUND(m, 11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13);
-    cv[0] = v0 ^ v8; cv[1] = v1 ^ v9; cv[2] = v2 ^ v10; cv[3] = v3 ^ v11;
-    cv[4] = v4 ^ v12; cv[5] = v5 ^ v13; cv[6] = v6 ^ v14; cv[7] = v7 ^ v15;
+    cv[0] = b3_xor(v0, v8); cv[1] = b3_xor(v1, v9); cv[2] = b3_xor(v2, v10); cv[3] = b3_xor(v3, v11);
+    cv[4] = b3_xor(v4, v12); cv[5] = b3_xor(v5, v13); cv[6] = b3_xor(v6, v14); cv[7] = b3_xor(v7, v15);
 }
 
 __device__ __forceinline__ void b3_iv(uint32_t cv[8]) {
