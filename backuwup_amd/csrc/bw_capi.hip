@@ -512,7 +512,8 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
 
     // ---- chunking
     if (ncf) {
-        launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots));
+        launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
+                    P<uint32_t>(c->ovf), ctr);
         prof_mark(c, BW_STAGE_COMPACT);
         launch_compact(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
                        P<uint64_t>(c->tile_off), P<uint64_t>(c->cand), cand_cap, P<uint32_t>(c->ovf), ctr,

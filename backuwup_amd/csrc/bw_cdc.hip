@@ -13,8 +13,7 @@
 //
 // Pipeline (all on the stream, no host round trip):
 //   k_scan      gear hash at every byte, LDS lane-replicated table, one-v_and prefilter per
-//               byte, flagged 64-byte blocks per tile
-//   k_refine    exact candidates (pos | S | L) for the flagged blocks, per-tile slots in place
+//               byte; flagged 64-byte blocks made exact by the wave at the end of each tile
 //   k_tile_partial/k_tile_top  exclusive scan of per-tile counts -> candidate array offsets
 //   k_rescan<false> exact counts of overflowed tiles (candidate-dense data, small parameters)
 //   k_compact   copy slots; k_rescan<true> writes the overflowed tiles' candidates
@@ -73,9 +72,8 @@ __device__ __forceinline__ void record_hit(uint64_t pos, uint64_t h, const Masks
 // prefilter is ONE v_and on it: (hi(h') & pre_hi) == 0 is implied by a real candidate (pre_hi =
 // the intersection mask's bits inside the window: 16 of mask_l's 19 at backuwup's parameters).
 // 128 positions fold into one min() per step; a step whose fold hits records only its 64-byte
-// block (rate ~64 * 2^-16 per lane-step), and k_refine turns flagged blocks into exact
-// candidates afterwards with every lane busy, instead of the whole wave replaying inside the
-// hot loop.
+// block (rate ~64 * 2^-16 per lane-step), and at the end of the tile the wave makes each flagged
+// block exact with every lane busy (refine_block), instead of replaying it inside the hot loop.
 //
 // Each wavefront owns a 128 KiB sub-tile = 64 strips of 2 KiB, one per lane.  The gear state
 // is warmed up on the 64 bytes before the strip (after 64 steps it IS the windowed hash), then
@@ -129,19 +127,43 @@ __device__ __forceinline__ void stage_hash_step(uint4 r0, uint4 r1, uint4 r2, ui
     }
 }
 
+constexpr uint32_t TILE_OVF = 0x80000000u;  // tile_count flag: candidates come from k_rescan
+
+__device__ __forceinline__ void ovf_push(uint64_t t, uint32_t* ovf, uint64_t* ctr) {
+    const uint64_t k = atomicAdd((unsigned long long*)&ctr[C_NOVF], 1ull);
+    ovf[k] = (uint32_t)t;
+}
+
+// Exact candidates of one flagged 64-byte block at b, by the whole wave: lane j takes position
+// b + j.  Two wave shift-scans of the (shifted) gear recurrence give h'_{b-1} from the 64 bytes
+// before the block (from 0 at the buffer start, where b == 0: the history the scan's lane had)
+// and then h'_{b+j} = scan_j + (h'_{b-1} << (j + 1)).  ~2 flagged blocks per 128 KiB tile on
+// random data at backuwup's parameters; the bytes were just streamed by this wave (L2 hits).
+__device__ __forceinline__ void refine_block(const uint8_t* __restrict__ data, uint64_t b, const uint64_t* s_gear,
+                                             uint32_t lane, const Masks& mk, uint32_t* cnt, uint64_t* slots) {
+    const uint32_t rep = (lane & 31) * 8;
+    const uint64_t g0 = b >= 64 ? *(const uint64_t*)((const uint8_t*)s_gear + ((uint32_t)data[b - 64 + lane] << 8) + rep) : 0;
+    const uint64_t g1 = *(const uint64_t*)((const uint8_t*)s_gear + ((uint32_t)data[b + lane] << 8) + rep);
+    const uint64_t pre = bw_shfl64(bw_gear_scan(g0), 63);
+    const uint64_t h = bw_gear_scan(g1) + ((pre << lane) << 1);
+    record_hit(b + lane, h >> mk.pre_shift, mk, cnt, slots);
+}
+
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
                                                        uint64_t n_tiles, Masks mk,
                                                        uint32_t* __restrict__ tile_count,
-                                                       uint64_t* __restrict__ tile_slots) {
+                                                       uint64_t* __restrict__ tile_slots, uint32_t* __restrict__ ovf,
+                                                       uint64_t* ctr) {
     constexpr int WAVES = BLOCK / 64;
     // one LDS object so the gear table sits at LDS address 0 and every lookup address is the
     // v_perm result itself (a table at a non-zero base costs one v_add per byte)
     struct ScanLds {
         uint64_t gear[256 * GEAR_REP];        // 64 KiB, 32 lane replicas
         uint8_t stage[WAVES][64 * STAGE_ROW]; // per-wave staging rows
-        uint64_t slots[WAVES][SCAN_CAP];
-        uint32_t cnt[WAVES];
+        uint64_t slots[WAVES][SCAN_CAP];  // exact candidates pos | S | L
+        uint64_t flags[WAVES][SCAN_CAP];  // flagged 64-byte blocks
+        uint32_t cnt[WAVES], nflag[WAVES];
     };
     __shared__ __attribute__((aligned(16))) ScanLds lds;
     uint64_t* s_gear = lds.gear;
@@ -156,10 +178,12 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
     uint8_t* stage = s_stage[wid];
     uint32_t* cnt = &s_cnt[wid];
     uint64_t* slots = s_slots[wid];
+    uint32_t* fcnt = &lds.nflag[wid];
+    uint64_t* fslots = lds.flags[wid];
     const uint64_t nw = (uint64_t)gridDim.x * WAVES;
 
     for (uint64_t tile = (uint64_t)blockIdx.x * WAVES + wid; tile < n_tiles; tile += nw) {
-        if (lane == 0) *cnt = 0;
+        if (lane == 0) { *cnt = 0; *fcnt = 0; }
         const uint64_t base = tile * SCAN_TILE;
         const uint64_t ss = base + (uint64_t)lane * SCAN_STRIP;
         uint64_t h = 0;
@@ -202,14 +226,14 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
                 for (int ds = 0; ds < STEPS / 2; ds += 2) {
                     BW_LOAD8(b, ds + 1);
                     stage_hash_step(a[0], a[1], a[2], a[3], wr, rd, h, ss + (uint64_t)(2 * ds) * SCAN_STEP, lane_off,
-                                    s_gear, phi, cnt, slots);
+                                    s_gear, phi, fcnt, fslots);
                     stage_hash_step(a[4], a[5], a[6], a[7], wr, rd, h, ss + (uint64_t)(2 * ds + 1) * SCAN_STEP,
-                                    lane_off, s_gear, phi, cnt, slots);
+                                    lane_off, s_gear, phi, fcnt, fslots);
                     BW_LOAD8(a, ds + 2 < STEPS / 2 ? ds + 2 : STEPS / 2 - 1);  // clamped, unused at the end
                     stage_hash_step(b[0], b[1], b[2], b[3], wr, rd, h, ss + (uint64_t)(2 * ds + 2) * SCAN_STEP,
-                                    lane_off, s_gear, phi, cnt, slots);
+                                    lane_off, s_gear, phi, fcnt, fslots);
                     stage_hash_step(b[4], b[5], b[6], b[7], wr, rd, h, ss + (uint64_t)(2 * ds + 3) * SCAN_STEP,
-                                    lane_off, s_gear, phi, cnt, slots);
+                                    lane_off, s_gear, phi, fcnt, fslots);
                 }
 #undef BW_LOAD8
             }
@@ -222,9 +246,14 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
             }
         }
         __builtin_amdgcn_wave_barrier();
+        const uint32_t nf = __builtin_amdgcn_readfirstlane(*fcnt);
+        if (nf <= (uint32_t)SCAN_CAP)
+            for (uint32_t f = 0; f < nf; f++) refine_block(data, BW_CAND_POS(fslots[f]), s_gear, lane, mk, cnt, slots);
+        __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
             const uint32_t c = *cnt, n = c < (uint32_t)SCAN_CAP ? c : (uint32_t)SCAN_CAP;
-            for (uint32_t i = 1; i < n; i++) {  // insertion sort by position (n is ~2)
+            if (nf > (uint32_t)SCAN_CAP || c > (uint32_t)SCAN_CAP) ovf_push(tile, ovf, ctr);  // exact list from k_rescan
+            for (uint32_t i = 1; i < n; i++) {  // insertion sort by position (n is ~0.25)
                 uint64_t v = slots[i];
                 int k = (int)i - 1;
                 while (k >= 0 && BW_CAND_POS(slots[k]) > BW_CAND_POS(v)) {
@@ -240,86 +269,19 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
     }
 }
 
-// Exact candidates for the 64-byte blocks the scan's prefilter flagged: one lane per tile,
-// rewriting the tile's slots in place (sorted, exact pos | S | L records).  A block is re-hashed
-// from 64 bytes before it (from 0 at the buffer start), exactly the history the scan's lane had.
-// A tile whose flags or exact candidates exceed SCAN_CAP joins the overflow list: k_rescan
-// counts (before the offset scan) and writes (after it) its candidates exactly.  Work: ~2
-// flagged blocks per 128 KiB tile on random data at backuwup's parameters.
-constexpr int REFINE_THREADS = 256;
-constexpr uint32_t TILE_OVF = 0x80000000u;  // tile_count flag: candidates come from k_rescan
-
-__device__ __forceinline__ void ovf_push(uint64_t t, uint32_t* ovf, uint64_t* ctr) {
-    const uint64_t k = atomicAdd((unsigned long long*)&ctr[C_NOVF], 1ull);
-    ovf[k] = (uint32_t)t;
-}
-
-__global__ __launch_bounds__(REFINE_THREADS) void k_refine(const uint8_t* __restrict__ data, uint64_t n_tiles,
-                                                           Masks mk, uint32_t* __restrict__ tile_count,
-                                                           uint64_t* __restrict__ tile_slots,
-                                                           uint32_t* __restrict__ ovf, uint64_t* ctr) {
-    __shared__ uint64_t lg[256];
-    __shared__ uint64_t s_in[REFINE_THREADS][SCAN_CAP];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = c_gear[i];
-    __syncthreads();
-    const uint64_t t = (uint64_t)blockIdx.x * REFINE_THREADS + threadIdx.x;
-    if (t >= n_tiles) return;
-    const uint32_t c = tile_count[t];
-    if (c == 0) return;
-    if (c > (uint32_t)SCAN_CAP) {
-        ovf_push(t, ovf, ctr);
-        return;
-    }
-    uint64_t* sl = tile_slots + t * SCAN_CAP;
-    uint64_t* in = s_in[threadIdx.x];
-    for (uint32_t k = 0; k < c; k++) in[k] = sl[k];
-    if (!(in[0] & BW_CAND_BLK)) return;  // ragged tile: the scan recorded exact candidates
-    uint32_t w = 0;
-    for (uint32_t k = 0; k < c; k++) {
-        const uint64_t b = BW_CAND_POS(in[k]);
-        // the block and the 64 bytes before it (from 0 at the buffer start, where b == 0): all
-        // eight loads in flight at once
-        const uint64_t s = b >= 64 ? b - 64 : 0;
-        const uint4* wp = (const uint4*)(data + s);
-        uint4 v[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) v[q] = wp[b >= 64 ? q : (q & 3)];
-        uint64_t h = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            if (b < 64 && q >= 4) break;
-            const uint32_t ww[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                h = (h << 1) + lg[(ww[j >> 2] >> (8 * (j & 3))) & 0xff];
-                const uint64_t p = s + 16 * (uint64_t)q + j;
-                if (p >= b) {
-                    const bool S = (h & mk.mask_s) == 0, L = (h & mk.mask_l) == 0;
-                    if (S || L) {
-                        if (w < (uint32_t)SCAN_CAP) sl[w] = p | (S ? BW_CAND_S : 0) | (L ? BW_CAND_L : 0);
-                        w++;
-                    }
-                }
-            }
-        }
-    }
-    if (w > (uint32_t)SCAN_CAP) ovf_push(t, ovf, ctr);
-    else tile_count[t] = w;
-}
-
 template <int BLOCK>
 static void launch_scan_t(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
-                          uint32_t* tile_count, uint64_t* tile_slots) {
+                          uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf, uint64_t* ctr) {
     uint64_t grid = (n_tiles + BLOCK / 64 - 1) / (BLOCK / 64);
     if (grid > 512) grid = 512;  // persistent: every CU holds one block (LDS), two rounds
     hipLaunchKernelGGL((k_scan<BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes,
-                       n_tiles, mk, tile_count, tile_slots);
+                       n_tiles, mk, tile_count, tile_slots, ovf, ctr);
 }
 
 void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
-                 uint32_t* tile_count, uint64_t* tile_slots) {
+                 uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf, uint64_t* ctr) {
     if (!n_tiles) return;
-    launch_scan_t<SCAN_BLOCK>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots);
+    launch_scan_t<SCAN_BLOCK>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
 }
 
 // ======================================================================== block scan helpers
@@ -472,8 +434,6 @@ void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint6
                     uint64_t cand_cap, uint32_t* ovf_list, uint64_t* ctr, uint64_t* btot) {
     if (!n_tiles) return;
     const uint64_t nb = (n_tiles + 4 * TS_BLOCK - 1) / (4 * TS_BLOCK);
-    hipLaunchKernelGGL(k_refine, dim3((unsigned)((n_tiles + REFINE_THREADS - 1) / REFINE_THREADS)),
-                       dim3(REFINE_THREADS), 0, st, data, n_tiles, mk, tile_count, tile_slots, ovf_list, ctr);
     hipLaunchKernelGGL(k_rescan<false>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
                        cand, cand_cap, tile_count, ctr);
     hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, tile_count, n_tiles, tile_off, btot);

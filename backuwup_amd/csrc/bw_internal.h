@@ -78,7 +78,8 @@ struct BlobArrays {
 
 // ------------------------------------------------------------------ launchers (bw_cdc.hip)
 void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
-                 const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots);
+                 const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf_list,
+                 uint64_t* ctr);
 void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
                     const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots,
                     uint64_t* tile_off, uint64_t* cand, uint64_t cand_cap, uint32_t* ovf_list,

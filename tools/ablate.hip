@@ -143,7 +143,7 @@ int main() {
     printf("copy_strided   %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { hipLaunchKernelGGL(copy_coalesced, dim3(4096), dim3(512), 0, 0, d, n, out); });
     printf("copy_coalesced %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
-    t = timeit([&] { launch_scan(0, d, n, tiles, mk, tc, ts); });
+    t = timeit([&] { launch_scan(0, d, n, tiles, mk, tc, ts, (uint32_t*)ts, (uint64_t*)out); });
     printf("scan_full      %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { launch_scan_t<512>(0, d, n, tiles, mk, tc, ts); });
     printf("scan_b512      %8.3f ms %8.1f GB/s (8-wave blocks: leaves LDS for a co-resident kernel)\n", t, gb / t * 1e3);
