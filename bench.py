@@ -80,6 +80,8 @@ def main():
                     help="batches in flight: consecutive steps alternate between this many contexts/streams")
     ap.add_argument("--host-stream", action="store_true",
                     help="batches start in pinned host memory (H2D copies overlapped with processing)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
     if args.gib is None:
         args.gib = {"c1": 1.0, "c2": 16.0, "c3": 4.0, "c4": 0.0}[args.workload]
@@ -96,8 +98,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    multi = world > 1 or args.exchange  # the sharded-index path (digest all-to-all over RCCL)
+    if multi:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     t0 = time.time()
     data, file_off, file_len, desc = make_workload(args.workload, args.gib, rank, dev, args.files)
@@ -106,7 +112,8 @@ def main():
     processed = int(np.sum(np.asarray(file_len, dtype=np.uint64)))  # file bytes per step (C4 copies alias)
     log("rank %d: %s -- generated in %.1f s" % (rank, desc, time.time() - t0))
 
-    nctx = 2 if args.host_stream else max(1, args.streams)
+    # N > 1: two contexts, so batch k's chunk+hash runs while batch k-1's digests are exchanged
+    nctx = 2 if (args.host_stream or multi) else max(1, args.streams)
     ctxs, streams = [], []
     for k in range(nctx):
         c = Context(local)
@@ -115,7 +122,7 @@ def main():
         ctxs.append(c)
         streams.append(st)
     ctx = ctxs[0]
-    flags = BW_F_NO_DEDUP if world > 1 else 0
+    flags = BW_F_NO_DEDUP if multi else 0
     params = make_params(flags=flags)
     index_hint = 2 * (processed // (256 << 10)) + len(file_len) + 1024
     owner_bits = world.bit_length() - 1
@@ -138,6 +145,20 @@ def main():
 
     step_no = [0]
     host_ms = [0.0]  # host time inside the library's submit calls (metadata build + upload)
+    pending = [None]  # N > 1: the context whose batch still awaits its digest exchange
+
+    def exchange(k):
+        # digest all-to-all by owner = digest[0] >> (8 - log2 N); verdicts come back (RCCL on the
+        # batch's own stream, beside the next batch's kernels on the other stream)
+        c = ctxs[k]
+        with torch.cuda.stream(streams[k]):
+            nb, d_dig, d_dup = c.device_views()
+            exchange_dedup(DeviceShardOps(c, dev), d_dig, nb, d_dup, world, dev)
+
+    def drain():
+        if pending[0] is not None:
+            exchange(pending[0])
+            pending[0] = None
 
     def step():
         k = step_no[0] % len(ctxs)
@@ -157,15 +178,15 @@ def main():
             c.index_reset(index_hint)
             c.submit_device(src.data_ptr(), n, file_off, file_len, params)
             host_ms[0] += (time.perf_counter() - th) * 1e3
-            if world > 1:
-                # digest all-to-all by owner = digest[0] >> (8 - log2 N); verdicts come back
-                nb, d_dig, d_dup = c.device_views()
-                exchange_dedup(DeviceShardOps(c, dev), d_dig, nb, d_dup, world, dev)
             if host is not None:
                 done[k].record(streams[k])
+        if multi:
+            drain()  # the previous batch's exchange, while this batch computes
+            pending[0] = k
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
 
     check = None
@@ -177,18 +198,19 @@ def main():
 
     for c in ctxs:
         c.profile_enable(True)
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     host_ms[0] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if multi:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -239,7 +261,7 @@ def main():
                            "batches_in_flight": len(ctxs)},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": check}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
