@@ -43,7 +43,7 @@ struct bw_ctx {
     DevBuf tile_count, tile_slots, tile_off, tile_btot, cand, ovf, ctr;
     DevBuf segs, cfiles, units, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
-    DevBuf cv, digests, is_dup, packed, fstart, data, scratch, ucnt, ubtot;
+    DevBuf cv, cv2, digests, is_dup, packed, fstart, data, scratch, ucnt, ubtot;
     PinBuf stage;
 
     // persistent dedup index
@@ -217,7 +217,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
     DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->ctr, &c->segs,
                      &c->cfiles, &c->units, &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
-                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->digests,
+                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->digests,
                      &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->table,
                      &c->log, &c->dstate};
     for (DevBuf* b : all)
@@ -463,6 +463,7 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     rc |= ensure(c, c->b_fend, max_blobs * 8);
     rc |= ensure(c, c->b_ghash, max_blobs * 8);
     rc |= ensure(c, c->cv, max_groups * 32);
+    rc |= ensure(c, c->cv2, max_leaves > 64 ? max_groups * 32 : 16);
     rc |= ensure(c, c->digests, max_blobs * 32);
     rc |= ensure(c, c->is_dup, max_blobs);
     rc |= ensure(c, c->packed, max_blobs * sizeof(bw_blob));
@@ -541,8 +542,8 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     // ---- hashing + dedup
     prof_mark(c, BW_STAGE_B3LEAF);
     if (do_hash) {
-        launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint8_t>(c->digests),
-                      max_leaves, c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : nullptr);
+        launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint32_t>(c->cv2),
+                      P<uint8_t>(c->digests), max_leaves, c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : nullptr);
     } else {
         prof_mark(c, BW_STAGE_B3TREE);
         HIPCHK(c, hipMemsetAsync(c->digests.p, 0, max_blobs * 32, st));

@@ -105,7 +105,8 @@ void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const
 // ------------------------------------------------------------------ launchers (bw_blake3.hip)
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b,
                    uint64_t max_blobs, uint64_t max_groups, uint32_t* cv_buf,
-                   uint8_t* digests, int max_leaves, hipEvent_t between /* may be null */);
+                   uint32_t* cv_tmp /* like cv_buf */, uint8_t* digests, int max_leaves,
+                   hipEvent_t between /* may be null */);
 
 // ------------------------------------------------------------------ launchers (bw_dedup.hip)
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),
