@@ -8,11 +8,13 @@ modules mirror the reference's call sites:
   backuwup_amd.blake3.hash       <- blake3::hash              (dir_packer.rs:286)
   backuwup_amd.packer.BlobIndex  <- packfile::blob_index::BlobIndex (blob_index.rs:44-148)
   backuwup_amd.packer.process_files <- dir_packer::process_file + add_file_blob
+  Context.tree_blobs / tree_serialize <- split_serialize_tree + add_tree_to_blobs (dir_packer.rs:314-390)
 """
 from . import _lib
-from .context import BLOB_DTYPE, Context, default_context, make_params
+from .context import BLOB_DTYPE, TREE_BLOB_DTYPE, Context, default_context, make_params, make_tree, tree_serialize
 
-__all__ = ["Context", "default_context", "make_params", "BLOB_DTYPE", "load_library"]
+__all__ = ["Context", "default_context", "make_params", "make_tree", "tree_serialize", "BLOB_DTYPE",
+           "TREE_BLOB_DTYPE", "load_library"]
 
 
 def load_library():

@@ -33,6 +33,21 @@ class BwParams(ctypes.Structure):
                 ("small_file_threshold", ctypes.c_uint64)]
 
 
+class BwTree(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("size", ctypes.c_uint64),
+                ("mtime", ctypes.c_uint64), ("ctime", ctypes.c_uint64), ("name", vp),
+                ("name_len", ctypes.c_uint64), ("children", vp), ("n_children", ctypes.c_uint64)]
+
+
+class BwTreeBlob(ctypes.Structure):
+    _fields_ = [("tree", ctypes.c_uint64), ("piece", ctypes.c_uint64), ("length", ctypes.c_uint64),
+                ("hash", ctypes.c_uint8 * 32), ("is_dup", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 7)]
+
+
+BW_TREE_FILE, BW_TREE_DIR = 0, 1
+BW_TREE_HAS_SIZE, BW_TREE_HAS_MTIME, BW_TREE_HAS_CTIME = 1, 2, 4
+BW_TREE_BLOB_MAX_CHILDREN = 10000
+
 # (name, restype, argtypes) for every symbol of include/backuwup_gpu.h
 SIGNATURES = [
     ("bw_params_default", None, [ctypes.POINTER(BwParams)]),
@@ -60,6 +75,9 @@ SIGNATURES = [
     ("bw_partition_by_owner", ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, u64p]),
     ("bw_index_check_insert_device", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),
     ("bw_scatter_verdicts", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, vp]),
+    ("bw_tree_serialize", ctypes.c_int, [ctypes.POINTER(BwTree), vp, vp, ctypes.c_uint64, u64p]),
+    ("bw_tree_blobs", ctypes.c_int, [vp, ctypes.POINTER(BwTree), ctypes.c_uint64, ctypes.c_uint32, vp,
+                                     ctypes.POINTER(BwTreeBlob), ctypes.c_uint64, u64p]),
     ("bw_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
 ]

@@ -34,6 +34,45 @@ def make_params(min_size=BLOB_MINIMUM_TARGET_SIZE, avg_size=BLOB_DESIRED_TARGET_
     return p
 
 
+TREE_BLOB_DTYPE = np.dtype([("tree", "<u8"), ("piece", "<u8"), ("length", "<u8"), ("hash", "u1", (32,)),
+                            ("is_dup", "u1"), ("pad", "u1", (7,))])
+assert TREE_BLOB_DTYPE.itemsize == ctypes.sizeof(_lib.BwTreeBlob) == 64
+
+
+def make_tree(kind, name, size=None, mtime=None, ctime=None, children=b""):
+    """A Tree (client/src/backup/filesystem/mod.rs:63-77) as the C struct plus the buffers it
+    points at: kind 0 = File, 1 = Dir; name str/bytes; children = concatenated 32-byte hashes."""
+    nm = name.encode("utf-8", "surrogateescape") if isinstance(name, str) else bytes(name)
+    ch = np.ascontiguousarray(np.frombuffer(bytes(children), dtype=np.uint8) if not isinstance(children, np.ndarray)
+                              else children.reshape(-1).view(np.uint8))
+    assert ch.size % 32 == 0
+    nb = np.frombuffer(nm, dtype=np.uint8).copy() if nm else np.zeros(0, dtype=np.uint8)
+    t = _lib.BwTree()
+    t.kind = kind
+    t.flags = (_lib.BW_TREE_HAS_SIZE if size is not None else 0) | \
+        (_lib.BW_TREE_HAS_MTIME if mtime is not None else 0) | (_lib.BW_TREE_HAS_CTIME if ctime is not None else 0)
+    t.size, t.mtime, t.ctime = size or 0, mtime or 0, ctime or 0
+    t.name = nb.ctypes.data if nb.size else None
+    t.name_len = nb.size
+    t.children = ch.ctypes.data if ch.size else None
+    t.n_children = ch.size // 32
+    return t, (nb, ch)
+
+
+def tree_serialize(tree, next_sibling=None):
+    """bincode bytes of one Tree (host-only entry point of the library)."""
+    t, keep = tree
+    L = _lib.load()
+    n = ctypes.c_uint64()
+    sib = None if next_sibling is None else (ctypes.c_uint8 * 32).from_buffer_copy(bytes(next_sibling))
+    rc = L.bw_tree_serialize(ctypes.byref(t), sib, None, 0, ctypes.byref(n))
+    if rc != _lib.BW_ENOSPC:
+        check(rc)
+    out = (ctypes.c_uint8 * max(n.value, 1))()
+    check(L.bw_tree_serialize(ctypes.byref(t), sib, out, n.value, ctypes.byref(n)))
+    return bytes(out[:n.value])
+
+
 class Context:
     """Owns one bw_ctx on `device`.  Not thread-safe (like the reference's packer mutex)."""
 
@@ -157,6 +196,21 @@ class Context:
         d, dup = ctypes.c_void_p(), ctypes.c_void_p()
         check(self._L.bw_batch_device_views(self.h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(dup)), self.h)
         return n.value, d.value, dup.value
+
+    # -------------------------------------------------------------- tree blobs
+    def tree_blobs(self, trees, dedup=True):
+        """split_serialize_tree + add_tree_to_blobs for a list of make_tree() results ->
+        (tree hashes n x 32, every piece as TREE_BLOB_DTYPE records in canonical order)."""
+        arr = (_lib.BwTree * max(len(trees), 1))(*[t for t, _ in trees])
+        cap = sum(max(1, -(-int(t.n_children) // _lib.BW_TREE_BLOB_MAX_CHILDREN)) for t, _ in trees)
+        hashes = np.zeros((max(len(trees), 1), 32), dtype=np.uint8)
+        out = np.zeros(max(cap, 1), dtype=TREE_BLOB_DTYPE)
+        n = ctypes.c_uint64()
+        flags = 0 if dedup else _lib.BW_F_NO_DEDUP
+        check(self._L.bw_tree_blobs(self.h, arr, len(trees), flags, ctypes.c_void_p(hashes.ctypes.data),
+                                    out.ctypes.data_as(ctypes.POINTER(_lib.BwTreeBlob)), cap, ctypes.byref(n)),
+              self.h)
+        return hashes[:len(trees)], out[:n.value]
 
     # -------------------------------------------------------------- stage timing
     def profile_enable(self, on=True):

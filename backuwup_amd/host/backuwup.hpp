@@ -10,10 +10,12 @@
 //   packfile::BlobIndex                packfile/blob_index.rs:44-148
 //   packfile::Manager::add_blob gate   packfile/pack.rs:31-39
 //   dir_packer::process_file           dir_packer.rs:231-282 (batched over many files)
+//   Tree / split_serialize_tree / add_tree_to_blobs   filesystem/mod.rs:63-77, dir_packer.rs:314-390
 #pragma once
 
 #include <array>
 #include <cstdint>
+#include <optional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -160,6 +162,68 @@ inline std::vector<bw_blob> process_files(Context& ctx, const uint8_t* data, siz
           ctx.get());
     out.resize(n);
     return out;
+}
+
+enum class TreeKind : uint32_t { File = BW_TREE_FILE, Dir = BW_TREE_DIR };
+
+struct TreeMetadata {  // filesystem/mod.rs:63-68
+    std::optional<uint64_t> size, mtime, ctime;
+};
+
+struct Tree {  // filesystem/mod.rs:70-77 (next_sibling is set by the split, not by callers)
+    TreeKind kind = TreeKind::File;
+    std::string name;
+    TreeMetadata metadata;
+    std::vector<BlobHash> children;
+};
+
+inline bw_tree to_c(const Tree& t) {
+    bw_tree c{};
+    c.kind = (uint32_t)t.kind;
+    c.flags = (t.metadata.size ? BW_TREE_HAS_SIZE : 0) | (t.metadata.mtime ? BW_TREE_HAS_MTIME : 0) |
+              (t.metadata.ctime ? BW_TREE_HAS_CTIME : 0);
+    c.size = t.metadata.size.value_or(0);
+    c.mtime = t.metadata.mtime.value_or(0);
+    c.ctime = t.metadata.ctime.value_or(0);
+    c.name = (const uint8_t*)t.name.data();
+    c.name_len = t.name.size();
+    c.children = t.children.empty() ? nullptr : t.children[0].data();
+    c.n_children = t.children.size();
+    return c;
+}
+
+// bincode::serialize(&tree) of one piece (dir_packer.rs:318)
+inline std::vector<uint8_t> serialize(const Tree& t, const BlobHash* next_sibling = nullptr) {
+    const bw_tree c = to_c(t);
+    uint64_t n = 0;
+    const int rc = bw_tree_serialize(&c, next_sibling ? next_sibling->data() : nullptr, nullptr, 0, &n);
+    if (rc != BW_ENOSPC) check(rc);
+    std::vector<uint8_t> out(n);
+    check(bw_tree_serialize(&c, next_sibling ? next_sibling->data() : nullptr, out.data(), n, &n));
+    return out;
+}
+
+// add_tree_to_blobs for many trees: every piece through the dedup gate in canonical order;
+// returns the hash each tree contributes to its parent (its first piece's hash).
+inline std::vector<BlobHash> add_trees_to_blobs(Context& ctx, const std::vector<Tree>& trees,
+                                                std::vector<bw_tree_blob>* pieces = nullptr) {
+    std::vector<bw_tree> c;
+    c.reserve(trees.size());
+    uint64_t cap = 0;
+    for (const Tree& t : trees) {
+        c.push_back(to_c(t));
+        cap += t.children.size() <= BW_TREE_BLOB_MAX_CHILDREN
+                   ? 1
+                   : (t.children.size() + BW_TREE_BLOB_MAX_CHILDREN - 1) / BW_TREE_BLOB_MAX_CHILDREN;
+    }
+    std::vector<BlobHash> hashes(trees.size());
+    std::vector<bw_tree_blob> out(pieces ? cap : 0);
+    uint64_t n = 0;
+    check(bw_tree_blobs(ctx.get(), c.data(), c.size(), 0, hashes.empty() ? nullptr : hashes[0].data(),
+                        pieces ? out.data() : nullptr, cap, &n),
+          ctx.get());
+    if (pieces) *pieces = std::move(out);
+    return hashes;
 }
 
 }  // namespace backuwup

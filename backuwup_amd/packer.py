@@ -7,14 +7,16 @@ Mirrors, on the GPU:
   * Manager::add_blob's dedup gate (packfile/pack.rs:31-39): BlobTooLarge for > 3 MiB blobs,
     `Ok(None)` for duplicates;
   * BlobIndex (packfile/blob_index.rs:44-148): seeded from the sorted prior index, then
-    is_blob_duplicate + blobs_queued insert in canonical order.
+    is_blob_duplicate + blobs_queued insert in canonical order;
+  * split_serialize_tree + add_tree_to_blobs (dir_packer.rs:314-390): file and directory trees
+    as bincode blobs, split at 10,000 children, through the same gate.
 """
 import numpy as np
 
 from .context import (BLOB_DESIRED_TARGET_SIZE, BLOB_MAX_UNCOMPRESSED_SIZE, BLOB_MINIMUM_TARGET_SIZE,
-                      BLOB_DTYPE, Context, default_context, make_params)
+                      BLOB_DTYPE, Context, default_context, make_params, make_tree)
 
-__all__ = ["BlobIndex", "Manager", "BlobTooLarge", "process_files", "process_file", "BLOB_DTYPE",
+__all__ = ["BlobIndex", "Manager", "BlobTooLarge", "process_files", "process_file", "add_trees_to_blobs", "BLOB_DTYPE",
            "BLOB_MINIMUM_TARGET_SIZE", "BLOB_DESIRED_TARGET_SIZE", "BLOB_MAX_UNCOMPRESSED_SIZE"]
 
 
@@ -78,3 +80,11 @@ def process_file(data, ctx=None, **kw):
     data = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     blobs = process_files(data, [0], [data.size], ctx=ctx, **kw)
     return [bytes(b) for b in blobs["digest"]]
+
+
+def add_trees_to_blobs(trees, ctx=None, dedup=True):
+    """add_tree_to_blobs for many trees: `trees` = [(kind, name, size, mtime, ctime, children
+    bytes)] with kind 0 = File, 1 = Dir and None for an absent metadata field.  Returns (the hash
+    each tree gives its parent, per-piece records with dedup verdicts in canonical order)."""
+    ctx = ctx or default_context()
+    return ctx.tree_blobs([make_tree(*t) for t in trees], dedup=dedup)

@@ -162,6 +162,49 @@ int bw_index_check_insert_device(bw_ctx* ctx, const uint8_t* d_digests, uint64_t
 int bw_scatter_verdicts(bw_ctx* ctx, const uint8_t* d_verdict, const uint64_t* d_perm,
                         uint64_t n, uint8_t* d_is_dup);
 
+/* ---- tree blobs: split_serialize_tree + add_tree_to_blobs, dir_packer.rs:314-390 ----
+ * Tree { kind: TreeKind, name: String, metadata: TreeMetadata { size, mtime, ctime: Option<u64> },
+ *        children: Vec<BlobHash>, next_sibling: Option<BlobHash> }   (filesystem/mod.rs:63-77)
+ * serialized with bincode 1.3.3 `bincode::serialize` (fixint, little endian). */
+#define BW_TREE_FILE 0u /* TreeKind::File */
+#define BW_TREE_DIR 1u  /* TreeKind::Dir  */
+#define BW_TREE_HAS_SIZE 1u
+#define BW_TREE_HAS_MTIME 2u
+#define BW_TREE_HAS_CTIME 4u
+#define BW_TREE_BLOB_MAX_CHILDREN 10000u /* dir_packer.rs:35 */
+
+typedef struct bw_tree {
+    uint32_t kind;            /* BW_TREE_FILE or BW_TREE_DIR                               */
+    uint32_t flags;           /* BW_TREE_HAS_*: which metadata options are Some            */
+    uint64_t size, mtime, ctime;
+    const uint8_t* name;      /* UTF-8 bytes (the reference's to_string_lossy), no NUL     */
+    uint64_t name_len;
+    const uint8_t* children;  /* n_children x 32-byte BlobHash, in the parent's order      */
+    uint64_t n_children;
+} bw_tree;
+
+/* One tree blob (a piece of a split tree), canonical order: trees as given, pieces in order. */
+typedef struct bw_tree_blob {
+    uint64_t tree;      /* index of the tree                                 */
+    uint64_t piece;     /* 0 = the blob whose hash represents the tree        */
+    uint64_t length;    /* serialized bytes                                  */
+    uint8_t hash[32];   /* blake3 of the serialized piece                     */
+    uint8_t is_dup;     /* Manager::add_blob returns Ok(None)                 */
+    uint8_t pad[7];
+} bw_tree_blob;
+
+/* bincode of one Tree (no splitting); next_sibling NULL = None.  Host only.  BW_ENOSPC with the
+ * required size in *n_out when cap is too small. */
+int bw_tree_serialize(const bw_tree* tree, const uint8_t* next_sibling, uint8_t* out, uint64_t cap,
+                      uint64_t* n_out);
+/* n trees: split (> 10,000 children), serialize, BLAKE3 every piece on the GPU (the last pieces
+ * first, each earlier piece with its successor's hash as next_sibling), then the dedup gate over
+ * all pieces in canonical order (skipped with BW_F_NO_DEDUP in flags).  tree_hashes[32*i] = the
+ * tree's hash (its first piece).  out (may be NULL) receives every piece; *n_out = pieces.
+ * Runs through the context's batch machinery: read a batch's results before calling it. */
+int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint32_t flags, uint8_t* tree_hashes,
+                  bw_tree_blob* out, uint64_t cap, uint64_t* n_out);
+
 /* ---- stage timing (HIP events on the context stream, accumulated over profiled batches) ---- */
 enum {
     BW_STAGE_SCAN = 0,     /* gear candidate scan (k_scan)                                 */

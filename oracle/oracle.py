@@ -145,3 +145,39 @@ BLOB_DTYPE = np.dtype([("file", "<u8"), ("offset", "<u8"), ("length", "<u8"),
                        ("gear_hash", "<u8"), ("digest", "u1", (32,)), ("is_dup", "u1"),
                        ("pad", "u1", (7,))])
 assert BLOB_DTYPE.itemsize == ctypes.sizeof(OrcBlob) == 72
+
+
+# ------------------------------------------------------------------ tree blobs (pure Python)
+# dir_packer.rs:314-363 split_serialize_tree; mod.rs:63-77 Tree / TreeMetadata; bincode 1.3.3
+# `bincode::serialize` (Cargo.lock:117-119): fixint little endian, enum = u32 variant index,
+# String / Vec = u64 length + items, Option = u8 tag + value, [u8; 32] = 32 raw bytes.
+TREE_BLOB_MAX_CHILDREN = 10000  # dir_packer.rs:35
+
+
+def tree_serialize(kind, name, size, mtime, ctime, children, next_sibling=None):
+    import struct
+    nm = name.encode("utf-8") if isinstance(name, str) else bytes(name)
+    out = struct.pack("<I", kind) + struct.pack("<Q", len(nm)) + nm
+    for v in (size, mtime, ctime):
+        out += b"\x00" if v is None else b"\x01" + struct.pack("<Q", v)
+    ch = bytes(children)
+    assert len(ch) % 32 == 0
+    out += struct.pack("<Q", len(ch) // 32) + ch
+    out += b"\x00" if next_sibling is None else b"\x01" + bytes(next_sibling)
+    return out
+
+
+def split_serialize_tree(kind, name, size, mtime, ctime, children):
+    """-> [(serialized piece, blake3 hash)] in the order add_tree_to_blobs adds them."""
+    ch = bytes(children)
+    n = len(ch) // 32
+    if n <= TREE_BLOB_MAX_CHILDREN:
+        d = tree_serialize(kind, name, size, mtime, ctime, ch)
+        return [(d, blake3(d))]
+    pieces = [ch[i * 32:(i + TREE_BLOB_MAX_CHILDREN) * 32] for i in range(0, n, TREE_BLOB_MAX_CHILDREN)]
+    out = []
+    for idx, part in enumerate(reversed(pieces)):
+        sib = None if idx == 0 else out[0][1]
+        d = tree_serialize(kind, name, size, mtime, ctime, part, sib)
+        out.insert(0, (d, blake3(d)))
+    return out

@@ -48,5 +48,20 @@ int main() {
     } catch (const BlobTooLarge&) {
         printf("too-large ok\n");
     }
+    // the file tree of the A.5 file (dir_packer.rs:237-274): chunk hashes as children
+    Tree ft;
+    ft.kind = TreeKind::File;
+    ft.name = "a5.bin";
+    ft.metadata.size = data.size();
+    ft.metadata.mtime = 1700000000;
+    for (const auto& c : chunker) ft.children.push_back(blake3::hash(ctx, data.data() + c.offset, c.length));
+    auto bytes = serialize(ft);
+    printf("tree-bytes ");
+    for (auto x : bytes) printf("%02x", x);
+    printf("\n");
+    auto th = add_trees_to_blobs(ctx, {ft, ft});
+    printf("tree-hash ");
+    for (auto x : th[0]) printf("%02x", x);
+    printf("\n");
     return 0;
 }

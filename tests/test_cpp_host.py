@@ -41,3 +41,8 @@ def test_cpp_mirror_parity(tmp_path, oracle):
     # a seeded -> duplicate; b new then duplicate; index holds 2
     assert "gate 0 1 0 2" in out
     assert "too-large ok" in out
+    tb = bytes.fromhex([l.split()[1] for l in out if l.startswith("tree-bytes ")][0])
+    children = b"".join(oracle.blake3(data[wo:wo + wl]) for _, wo, wl in want)
+    assert tb == oracle.tree_serialize(0, "a5.bin", len(data), 1700000000, None, children)
+    th = [l.split()[1] for l in out if l.startswith("tree-hash ")][0]
+    assert th == oracle.blake3(tb).hex()
