@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from backuwup_amd import make_tree, tree_serialize
-from backuwup_amd._lib import BwError
+from backuwup_amd._lib import BW_EINVAL
 
 
 def test_tree_bincode_layout_literal():
@@ -48,8 +48,9 @@ def test_tree_serialize_matches_oracle(oracle):
 def test_tree_serialize_rejects_bad_kind():
     t, keep = make_tree(0, "f")
     t.kind = 2
-    with pytest.raises(BwError):
+    with pytest.raises(RuntimeError) as e:  # BwError (compared by rc: test_capi reloads _lib)
         tree_serialize((t, keep))
+    assert e.value.rc == BW_EINVAL
 
 
 def test_split_tree_sibling_chain(oracle):
