@@ -34,6 +34,10 @@ def make_params(min_size=BLOB_MINIMUM_TARGET_SIZE, avg_size=BLOB_DESIRED_TARGET_
     return p
 
 
+# the C struct bw_tree as a numpy record, for building many trees without Python objects
+TREE_DTYPE = np.dtype([("kind", "<u4"), ("flags", "<u4"), ("size", "<u8"), ("mtime", "<u8"), ("ctime", "<u8"),
+                       ("name", "<u8"), ("name_len", "<u8"), ("children", "<u8"), ("n_children", "<u8")])
+assert TREE_DTYPE.itemsize == ctypes.sizeof(_lib.BwTree) == 64
 TREE_BLOB_DTYPE = np.dtype([("tree", "<u8"), ("piece", "<u8"), ("length", "<u8"), ("hash", "u1", (32,)),
                             ("is_dup", "u1"), ("pad", "u1", (7,))])
 assert TREE_BLOB_DTYPE.itemsize == ctypes.sizeof(_lib.BwTreeBlob) == 64
@@ -208,6 +212,20 @@ class Context:
         n = ctypes.c_uint64()
         flags = 0 if dedup else _lib.BW_F_NO_DEDUP
         check(self._L.bw_tree_blobs(self.h, arr, len(trees), flags, ctypes.c_void_p(hashes.ctypes.data),
+                                    out.ctypes.data_as(ctypes.POINTER(_lib.BwTreeBlob)), cap, ctypes.byref(n)),
+              self.h)
+        return hashes[:len(trees)], out[:n.value]
+
+    def tree_blobs_array(self, trees, dedup=True):
+        """tree_blobs over a TREE_DTYPE array whose pointers the caller keeps alive."""
+        n_ch = trees["n_children"].astype(np.int64)
+        cap = int(np.maximum(1, -(-n_ch // _lib.BW_TREE_BLOB_MAX_CHILDREN)).sum())
+        hashes = np.zeros((max(len(trees), 1), 32), dtype=np.uint8)
+        out = np.zeros(max(cap, 1), dtype=TREE_BLOB_DTYPE)
+        n = ctypes.c_uint64()
+        flags = 0 if dedup else _lib.BW_F_NO_DEDUP
+        check(self._L.bw_tree_blobs(self.h, trees.ctypes.data_as(ctypes.POINTER(_lib.BwTree)), len(trees), flags,
+                                    ctypes.c_void_p(hashes.ctypes.data),
                                     out.ctypes.data_as(ctypes.POINTER(_lib.BwTreeBlob)), cap, ctypes.byref(n)),
               self.h)
         return hashes[:len(trees)], out[:n.value]

@@ -80,6 +80,8 @@ def main():
                     help="batches in flight: consecutive steps alternate between this many contexts/streams")
     ap.add_argument("--host-stream", action="store_true",
                     help="batches start in pinned host memory (H2D copies overlapped with processing)")
+    ap.add_argument("--trees", action="store_true",
+                    help="also time the file-tree blobs of the last batch (bw_tree_blobs, §8f row 1)")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
@@ -237,6 +239,8 @@ def main():
     if host is not None:
         roofline.update({"host_stream_pcie_frac": round(value / PCIE_PEAK_GBS, 4)})
 
+    trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         from oracle import oracle
@@ -260,9 +264,50 @@ def main():
                            "parallelism": "dp%d (files sharded, index by digest prefix)" % world,
                            "batches_in_flight": len(ctxs)},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": check}
+        if trees:
+            line["file_trees"] = trees
         print(json.dumps(line), flush=True)
     if multi:
         dist.destroy_process_group()
+
+
+def time_file_trees(ctx, res, file_len, reps):
+    """The File tree of every file of the last batch (dir_packer.rs:237-274: name, size, mtime,
+    children = the file's chunk hashes) through bw_tree_blobs -- bincode, BLAKE3 on the GPU and
+    the dedup gate -- timed over `reps` fresh indexes; spot-checked against the oracle."""
+    import numpy as np
+    from backuwup_amd.context import TREE_DTYPE
+    from oracle import oracle
+    nf = len(file_len)
+    fidx = res["file"].astype(np.int64)
+    first = np.searchsorted(fidx, np.arange(nf))
+    count = np.bincount(fidx, minlength=nf)
+    names = np.frombuffer(b"".join(b"f%07d" % i for i in range(nf)), dtype=np.uint8)
+    t = np.zeros(nf, dtype=TREE_DTYPE)
+    t["kind"] = 0
+    t["flags"] = 1 | 2  # size, mtime
+    t["size"] = np.asarray(file_len, dtype=np.uint64)
+    t["mtime"] = 1700000000 + np.arange(nf, dtype=np.uint64)
+    t["name"] = names.ctypes.data + 8 * np.arange(nf, dtype=np.uint64)
+    t["name_len"] = 8
+    digests = np.ascontiguousarray(res["digest"])  # a file's chunk hashes, 32 B apart
+    t["children"] = digests.ctypes.data + 32 * first.astype(np.uint64)
+    t["n_children"] = count
+    best = None
+    for _ in range(max(1, reps)):
+        ctx.index_reset(2 * nf + 1024)
+        t0 = time.perf_counter()
+        hashes, pieces = ctx.tree_blobs_array(t)
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    ok = True
+    for i in np.random.default_rng(0).integers(0, nf, 16):
+        ch = b"".join(bytes(d) for d in res["digest"][first[i]:first[i] + count[i]])
+        want = oracle.split_serialize_tree(0, b"f%07d" % i, int(file_len[i]), 1700000000 + int(i), None, ch)
+        ok = ok and bytes(hashes[i]) == want[0][1]
+    return {"trees": nf, "pieces": int(len(pieces)), "ms": round(best * 1e3, 2),
+            "trees_per_s": round(nf / best, 1), "bytes_serialized": int(pieces["length"].sum()),
+            "bit_exact_sample": bool(ok)}
 
 
 def pmc_traffic(args, kernel):
