@@ -78,6 +78,12 @@ SIGNATURES = [
     ("bw_tree_serialize", ctypes.c_int, [ctypes.POINTER(BwTree), vp, vp, ctypes.c_uint64, u64p]),
     ("bw_tree_blobs", ctypes.c_int, [vp, ctypes.POINTER(BwTree), ctypes.c_uint64, ctypes.c_uint32, vp,
                                      ctypes.POINTER(BwTreeBlob), ctypes.c_uint64, u64p]),
+    ("bw_seal_device", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp,
+                                      u64p]),
+    ("bw_open_device", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp,
+                                      u64p, u8p]),
+    ("bw_seal", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp, u64p]),
+    ("bw_open", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp, u64p, u8p]),
     ("bw_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
 ]

@@ -139,6 +139,52 @@ class Context:
         check(self._L.bw_blake3_hash(self.h, _ptr(buf), buf.size, out), self.h)
         return bytes(out)
 
+    # -------------------------------------------------------------- sealing (§8f row 3)
+    @staticmethod
+    def _seal_tables(src_off, src_len, infos, nonces, dst_off):
+        so = np.ascontiguousarray(src_off, dtype=np.uint64)
+        sl = np.ascontiguousarray(src_len, dtype=np.uint64)
+        n = len(so)
+        info = np.ascontiguousarray(np.asarray(infos, dtype=np.uint8).reshape(n, -1)) if n else \
+            np.zeros((0, 0), np.uint8)
+        non = np.ascontiguousarray(np.asarray(nonces, dtype=np.uint8).reshape(n, 12)) if n else \
+            np.zeros((0, 12), np.uint8)
+        do = np.ascontiguousarray(dst_off, dtype=np.uint64)
+        assert len(sl) == n and len(do) == n
+        return so, sl, info, non, do, n
+
+    def seal(self, prk, src, src_off, src_len, infos, nonces, dst_off, dst_size, open_=False):
+        """Host buffers: derive_backup_key(info_i) + Aes256Gcm encrypt (open_=False) or decrypt
+        (open_=True).  infos: n x info_len bytes (blob hashes), nonces: n x 12.  Returns the output
+        buffer (and the ok flags when opening)."""
+        buf = _as_u8(src)
+        so, sl, info, non, do, n = self._seal_tables(src_off, src_len, infos, nonces, dst_off)
+        out = np.zeros(max(int(dst_size), 1), dtype=np.uint8)
+        k = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(prk))
+        args = [self.h, k, _ptr(buf), so.ctypes.data_as(_lib.u64p), sl.ctypes.data_as(_lib.u64p), n, _ptr(info),
+                info.shape[1] if n else 0, _ptr(non), _ptr(out), do.ctypes.data_as(_lib.u64p)]
+        if open_:
+            ok = np.zeros(n, dtype=np.uint8)
+            check(self._L.bw_open(*args, ok.ctypes.data_as(_lib.u8p)), self.h)
+            return out[:int(dst_size)], ok
+        check(self._L.bw_seal(*args), self.h)
+        return out[:int(dst_size)]
+
+    def seal_device(self, prk, d_src, src_off, src_len, infos, nonces, d_dst, dst_off, open_=False):
+        """Device pointers (ints); tables on the host.  Sealing is asynchronous on the context
+        stream; opening synchronizes and returns the ok flags."""
+        so, sl, info, non, do, n = self._seal_tables(src_off, src_len, infos, nonces, dst_off)
+        k = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(prk))
+        args = [self.h, k, ctypes.c_void_p(d_src), so.ctypes.data_as(_lib.u64p), sl.ctypes.data_as(_lib.u64p), n,
+                _ptr(info), info.shape[1] if n else 0, _ptr(non), ctypes.c_void_p(d_dst),
+                do.ctypes.data_as(_lib.u64p)]
+        if open_:
+            ok = np.zeros(n, dtype=np.uint8)
+            check(self._L.bw_open_device(*args, ok.ctypes.data_as(_lib.u8p)), self.h)
+            return ok
+        check(self._L.bw_seal_device(*args), self.h)
+        return None
+
     # -------------------------------------------------------------- index
     def index_reset(self, capacity_hint=0):
         check(self._L.bw_index_reset(self.h, capacity_hint), self.h)

@@ -46,6 +46,12 @@ struct bw_ctx {
     DevBuf cv, cv2, digests, is_dup, packed, fstart, data, scratch, ucnt, ubtot;
     PinBuf stage;
 
+    // blob sealing (bw_seal.hip): item table staging + per-item key material + piece partials
+    DevBuf seal_items, seal_keys, seal_parts, seal_ok, seal_io;
+    PinBuf seal_stage;
+    hipEvent_t seal_done = nullptr;  // seal_stage reusable once this fired
+    bool seal_pending = false;
+
     // persistent dedup index
     DevBuf table, log, dstate;
     uint64_t table_cap = 0, log_cap = 0, log_hi = 0;  // log_hi: host upper bound of log length
@@ -219,10 +225,13 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->digests,
                      &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->table,
-                     &c->log, &c->dstate};
+                     &c->log, &c->dstate, &c->seal_items, &c->seal_keys, &c->seal_parts, &c->seal_ok,
+                     &c->seal_io};
     for (DevBuf* b : all)
         if (b->p) hipFree(b->p);
     if (c->stage.p) hipHostFree(c->stage.p);
+    if (c->seal_stage.p) hipHostFree(c->seal_stage.p);
+    if (c->seal_done) hipEventDestroy(c->seal_done);
     if (c->meta_done) hipEventDestroy(c->meta_done);
     for (int k = 0; k < 2; k++)
         for (int i = 0; i <= BW_N_STAGES; i++)
@@ -731,4 +740,115 @@ extern "C" int bw_profile_read(bw_ctx* c, double* stage_ms, uint64_t* n_batches)
         for (int i = 0; i < BW_N_STAGES; i++) stage_ms[i] = c->stage_ms[i];
     if (n_batches) *n_batches = c->prof_batches;
     return BW_OK;
+}
+
+// ------------------------------------------------------------------ blob sealing (§8f row 3)
+// compress_encrypt_blob's HKDF key + AES-256-GCM (pack.rs:70-80) and the inverse
+// (unpack.rs:58-63, blob_index.rs:185-191); kernels in bw_seal.hip.
+
+static int seal_submit(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* d_src, const uint64_t* src_off,
+                       const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                       const uint8_t* nonces, uint8_t* d_dst, const uint64_t* dst_off, uint8_t* ok) {
+    if (!c || !prk || info_len > BW_SEAL_MAX_INFO) return BW_EINVAL;
+    if (n && (!d_src || !src_off || !src_len || !nonces || !d_dst || !dst_off || (info_len && !info))) return BW_EINVAL;
+    if (dec && n && !ok) return BW_EINVAL;
+    hipSetDevice(c->device);
+    if (!n) return BW_OK;
+    if (dec)
+        for (uint64_t i = 0; i < n; i++)
+            if (src_len[i] < 16) return BW_EINVAL;  // shorter than the tag: decrypt_in_place fails
+    if (!c->seal_done) HIPCHK(c, hipEventCreateWithFlags(&c->seal_done, hipEventDisableTiming));
+    if (c->seal_pending) {
+        hipEventSynchronize(c->seal_done);
+        c->seal_pending = false;
+    }
+    const size_t bytes = n * sizeof(SealItem);
+    if (c->seal_stage.cap < bytes) {
+        if (c->seal_stage.p) hipHostFree(c->seal_stage.p);
+        c->seal_stage.p = nullptr;
+        c->seal_stage.cap = 0;
+        const size_t want = bytes + bytes / 4 + 4096;
+        if (hipHostMalloc(&c->seal_stage.p, want, hipHostMallocDefault) != hipSuccess) {
+            c->err = "hipHostMalloc failed";
+            return BW_ENOMEM;
+        }
+        c->seal_stage.cap = want;
+    }
+    SealItem* it = (SealItem*)c->seal_stage.p;
+    uint64_t pieces = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t len = dec ? src_len[i] - 16 : src_len[i];
+        seal_fill_item(&it[i], src_off[i], len, dst_off[i], pieces, nonces + 12 * i, info + (uint64_t)info_len * i,
+                       info_len);
+        pieces += seal_pieces(len);
+    }
+    if (int rc = ensure(c, c->seal_items, bytes)) return rc;
+    if (int rc = ensure(c, c->seal_keys, n * sizeof(SealKey))) return rc;
+    if (int rc = ensure(c, c->seal_parts, (pieces + 1) * 16)) return rc;
+    if (dec)
+        if (int rc = ensure(c, c->seal_ok, n)) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->seal_items.p, it, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->seal_done, c->stream));
+    c->seal_pending = true;
+    SealPads pads;
+    seal_pads(prk, &pads);
+    launch_seal(c->stream, dec, d_src, d_dst, P<SealItem>(c->seal_items), n, pads, P<SealKey>(c->seal_keys), pieces,
+                P<uint32_t>(c->seal_parts), dec ? P<uint8_t>(c->seal_ok) : nullptr);
+    HIPCHK(c, hipGetLastError());
+    if (dec) {
+        HIPCHK(c, hipMemcpyAsync(ok, c->seal_ok.p, n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return BW_OK;
+}
+
+extern "C" int bw_seal_device(bw_ctx* c, const uint8_t prk[32], const uint8_t* d_src, const uint64_t* src_off,
+                              const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                              const uint8_t* nonces, uint8_t* d_dst, const uint64_t* dst_off) {
+    return seal_submit(c, false, prk, d_src, src_off, src_len, n, info, info_len, nonces, d_dst, dst_off, nullptr);
+}
+
+extern "C" int bw_open_device(bw_ctx* c, const uint8_t prk[32], const uint8_t* d_src, const uint64_t* src_off,
+                              const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                              const uint8_t* nonces, uint8_t* d_dst, const uint64_t* dst_off, uint8_t* ok) {
+    return seal_submit(c, true, prk, d_src, src_off, src_len, n, info, info_len, nonces, d_dst, dst_off, ok);
+}
+
+// Host-buffer forms: both buffers go through one device staging area ([src | dst]).
+static int seal_host(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* src, const uint64_t* src_off,
+                     const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                     const uint8_t* nonces, uint8_t* dst, const uint64_t* dst_off, uint8_t* ok) {
+    if (!c || (n && (!src || !src_off || !src_len || !dst || !dst_off))) return BW_EINVAL;
+    hipSetDevice(c->device);
+    uint64_t s_end = 0, d_end = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (dec && src_len[i] < 16) return BW_EINVAL;
+        s_end = std::max(s_end, src_off[i] + src_len[i]);
+        d_end = std::max(d_end, dst_off[i] + (dec ? src_len[i] - 16 : src_len[i] + 16));
+    }
+    const uint64_t d_base = (s_end + 255) & ~255ull;
+    if (int rc = ensure(c, c->seal_io, d_base + d_end + 16)) return rc;
+    uint8_t* io = P<uint8_t>(c->seal_io);
+    if (s_end) HIPCHK(c, hipMemcpyAsync(io, src, s_end, hipMemcpyHostToDevice, c->stream));
+    int rc = seal_submit(c, dec, prk, io, src_off, src_len, n, info, info_len, nonces, io + d_base, dst_off, ok);
+    if (rc) return rc;
+    // copy back only the written ranges (the caller's gaps stay untouched)
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t len = dec ? src_len[i] - 16 : src_len[i] + 16;
+        if (len) HIPCHK(c, hipMemcpyAsync(dst + dst_off[i], io + d_base + dst_off[i], len, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BW_OK;
+}
+
+extern "C" int bw_seal(bw_ctx* c, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,
+                       const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                       const uint8_t* nonces, uint8_t* dst, const uint64_t* dst_off) {
+    return seal_host(c, false, prk, src, src_off, src_len, n, info, info_len, nonces, dst, dst_off, nullptr);
+}
+
+extern "C" int bw_open(bw_ctx* c, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,
+                       const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                       const uint8_t* nonces, uint8_t* dst, const uint64_t* dst_off, uint8_t* ok) {
+    return seal_host(c, true, prk, src, src_off, src_len, n, info, info_len, nonces, dst, dst_off, ok);
 }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/backuwup_gpu.h"
+
 namespace bw {
 
 // ------------------------------------------------------------------ tunables
@@ -127,5 +129,34 @@ void launch_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm
                     uint8_t* is_dup);
 void launch_pack(hipStream_t st, const uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
                  const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs);
+
+// ------------------------------------------------------------------ sealing (bw_seal.hip)
+// BW_SEAL_MAX_INFO (include/backuwup_gpu.h): HKDF info bytes that fit one HMAC block with 0x01 + padding
+constexpr uint32_t PIECE_BLOCKS = 8192;  // 16-byte blocks per k_seal_ctr wave task (128 KiB)
+constexpr int SEAL_THREADS = 1024;       // 16 waves: one LDS set per CU
+
+struct SealItem {
+    uint64_t src_off, len, dst_off, piece0;  // len = plaintext bytes; piece0 = first piece
+    uint32_t nonce[3];                       // big-endian words of the 12-byte nonce
+    uint32_t info_len;
+    uint8_t info[56];
+};
+
+struct SealKey {
+    uint32_t rk[60];   // AES-256 round keys, big-endian words
+    uint32_t H[4], E0[4], HP[4], H64[4];  // E(0), E(J0), H^PIECE_BLOCKS, H^64
+    uint32_t P[6][4];  // H^(2^k), k = 0..5
+};
+
+struct SealPads {
+    uint32_t istate[8], ostate[8];  // SHA-256 states after the HMAC key ^ ipad / ^ opad blocks
+};
+void seal_pads(const uint8_t prk[32], SealPads* pads);
+uint64_t seal_pieces(uint64_t len);  // k_seal_ctr wave tasks of an item of len bytes
+void seal_fill_item(SealItem* it, uint64_t src_off, uint64_t len, uint64_t dst_off, uint64_t piece0,
+                    const uint8_t nonce[12], const uint8_t* info, uint32_t info_len);
+// dec = false: dst = ciphertext || tag; dec = true: dst = plaintext, ok[i] = tag verified
+void launch_seal(hipStream_t st, bool dec, const uint8_t* src, uint8_t* dst, const SealItem* items, uint64_t n,
+                 const SealPads& pads, SealKey* keys, uint64_t n_pieces, uint32_t* parts, uint8_t* ok);
 
 }  // namespace bw

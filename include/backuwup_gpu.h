@@ -205,6 +205,36 @@ int bw_tree_serialize(const bw_tree* tree, const uint8_t* next_sibling, uint8_t*
 int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint32_t flags, uint8_t* tree_hashes,
                   bw_tree_blob* out, uint64_t cap, uint64_t* n_out);
 
+/* ---- blob sealing ----
+ * The encryption half of Manager::compress_encrypt_blob (pack.rs:70-80) for already compressed
+ * payloads, and the packfile header / index keys (pack.rs:212-217, blob_index.rs:185-191,205-213):
+ *   key_i = KeyManager::derive_backup_key(info_i)  (key_manager.rs:80-86:
+ *           Hkdf::<Sha256>::from_prk(prk).expand(info_i, 32 bytes); prk = backup_secret_key)
+ *   out_i = Aes256Gcm::new(key_i).encrypt_in_place(nonce_i, b"", src_i)  = ciphertext || 16-byte tag
+ * Item i: src_i = src[src_off[i] .. + src_len[i]), info_i = info[i*info_len .. + info_len)
+ * (info_len <= BW_SEAL_MAX_INFO: 32 for a blob hash, 6 for "header", 5 for "index"),
+ * nonce_i = nonces[12*i .. + 12]; the output goes to dst + dst_off[i] (src_len[i] + 16 bytes).
+ * Output ranges must not overlap each other or the inputs.  Tables are host arrays. */
+#define BW_SEAL_MAX_INFO 54u
+#define BW_SEAL_TAG_BYTES 16u
+/* Device buffers; asynchronous on the context stream. */
+int bw_seal_device(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* d_src, const uint64_t* src_off,
+                   const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                   const uint8_t* nonces, uint8_t* d_dst, const uint64_t* dst_off);
+/* decrypt_in_place: src_len[i] includes the tag (>= 16, else BW_EINVAL); plaintext (src_len[i] - 16
+ * bytes) to dst + dst_off[i]; ok[i] (host) = 1 if the tag verified, 0 where the reference returns
+ * Err(aes_gcm::Error) -- the plaintext of such an item must be discarded.  Synchronous. */
+int bw_open_device(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* d_src, const uint64_t* src_off,
+                   const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+                   const uint8_t* nonces, uint8_t* d_dst, const uint64_t* dst_off, uint8_t* ok);
+/* Same over host buffers (synchronous; only the output ranges are written). */
+int bw_seal(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,
+            const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+            const uint8_t* nonces, uint8_t* dst, const uint64_t* dst_off);
+int bw_open(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,
+            const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
+            const uint8_t* nonces, uint8_t* dst, const uint64_t* dst_off, uint8_t* ok);
+
 /* ---- stage timing (HIP events on the context stream, accumulated over profiled batches) ---- */
 enum {
     BW_STAGE_SCAN = 0,     /* gear candidate scan (k_scan)                                 */

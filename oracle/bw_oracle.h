@@ -64,6 +64,20 @@ int orc_process_files(const uint8_t* data, const uint64_t* file_off, const uint6
                       uint64_t small_file_threshold, orc_index* ix, int threads,
                       orc_blob* out, size_t cap, size_t* n_out);
 
+/* ---- sealing (bw_oracle_seal.c): pack.rs:58-80, key_manager.rs:80-86 ---- */
+void orc_sha256(const uint8_t* data, size_t len, uint8_t out[32]);
+void orc_hmac_sha256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen, uint8_t out[32]);
+void orc_hkdf_expand32(const uint8_t prk[32], const uint8_t* info, size_t info_len, uint8_t out[32]);
+void orc_aes256_encrypt_block(const uint8_t key[32], const uint8_t in[16], uint8_t out[16]);
+void orc_aes256_gcm_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* pt, size_t len,
+                         uint8_t* out /* len + 16 */);
+int orc_aes256_gcm_open(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* ct,
+                        size_t len_with_tag, uint8_t* out);
+void orc_seal_blob(const uint8_t prk[32], const uint8_t* info, size_t info_len, const uint8_t nonce[12],
+                   const uint8_t* payload, size_t len, uint8_t* out);
+int orc_open_blob(const uint8_t prk[32], const uint8_t* info, size_t info_len, const uint8_t nonce[12],
+                  const uint8_t* sealed, size_t len_with_tag, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,15 @@ def lib():
         L.orc_index_free.argtypes = [ctypes.c_void_p]
         L.orc_index_is_duplicate.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.orc_index_insert.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        vp = ctypes.c_void_p
+        L.orc_sha256.argtypes = [vp, ctypes.c_size_t, vp]
+        L.orc_hmac_sha256.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp]
+        L.orc_hkdf_expand32.argtypes = [vp, vp, ctypes.c_size_t, vp]
+        L.orc_aes256_encrypt_block.argtypes = [vp, vp, vp]
+        L.orc_aes256_gcm_seal.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
+        L.orc_aes256_gcm_open.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
+        L.orc_seal_blob.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp]
+        L.orc_open_blob.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp]
         L.orc_process_files.argtypes = [ctypes.c_void_p, u64p, u64p, ctypes.c_size_t,
                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
@@ -181,3 +190,64 @@ def split_serialize_tree(kind, name, size, mtime, ctime, children):
         d = tree_serialize(kind, name, size, mtime, ctime, part, sib)
         out.insert(0, (d, blake3(d)))
     return out
+
+
+# ------------------------------------------------------------------ sealing (bw_oracle_seal.c)
+# pack.rs:58-80 compress_encrypt_blob (after zstd), key_manager.rs:80-86 derive_backup_key.
+
+
+def _out(n):
+    return (ctypes.c_uint8 * max(n, 1))()
+
+
+def sha256(data):
+    ptr, n, keep = _buf(data)
+    o = _out(32)
+    lib().orc_sha256(ptr, n, o)
+    return bytes(o)
+
+
+def hmac_sha256(key, msg):
+    o = _out(32)
+    key, msg = bytes(key), bytes(msg)
+    lib().orc_hmac_sha256(key, len(key), msg, len(msg), o)
+    return bytes(o)
+
+
+def hkdf_expand32(prk, info):
+    """Hkdf::<Sha256>::from_prk(prk).expand(info, [0u8; 32])"""
+    o = _out(32)
+    info = bytes(info)
+    lib().orc_hkdf_expand32(bytes(prk), info, len(info), o)
+    return bytes(o)
+
+
+def aes256_block(key, block):
+    o = _out(16)
+    lib().orc_aes256_encrypt_block(bytes(key), bytes(block), o)
+    return bytes(o)
+
+
+def gcm_seal(key, nonce, pt):
+    """Aes256Gcm::new(key).encrypt_in_place(nonce, b"", pt) -> ciphertext || tag"""
+    ptr, n, keep = _buf(pt)
+    o = _out(n + 16)
+    lib().orc_aes256_gcm_seal(bytes(key), bytes(nonce), ptr, n, o)
+    return bytes(o)[:n + 16]
+
+
+def gcm_open(key, nonce, ct):
+    """decrypt_in_place: plaintext, or None when the tag does not verify"""
+    ptr, n, keep = _buf(ct)
+    o = _out(n)
+    if lib().orc_aes256_gcm_open(bytes(key), bytes(nonce), ptr, n, o):
+        return None
+    return bytes(o)[:max(n - 16, 0)]
+
+
+def seal_blob(prk, info, nonce, payload):
+    return gcm_seal(hkdf_expand32(prk, info), nonce, payload)
+
+
+def open_blob(prk, info, nonce, sealed):
+    return gcm_open(hkdf_expand32(prk, info), nonce, sealed)
