@@ -146,6 +146,7 @@ struct SealKey {
     uint32_t rk[60];   // AES-256 round keys, big-endian words
     uint32_t H[4], E0[4], HP[4], H64[4];  // E(0), E(J0), H^PIECE_BLOCKS, H^64
     uint32_t P[6][4];  // H^(2^k), k = 0..5
+    uint32_t R1[4];    // AES round 1 minus its counter-word terms (the nonce words are constant)
 };
 
 struct SealPads {

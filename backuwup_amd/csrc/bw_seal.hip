@@ -21,8 +21,8 @@
 //                256-byte row at LDS address 0, so one v_perm_b32 forms a conflict-free lookup
 //                address and Te1 is the same address + 128 (ds_read offset); Te2/Te3 are one
 //                rotation of (Te0 ^ Te1) terms.
-//   k_seal_tag   one lane per item: folds the piece partials with H^PIECE_BLOCKS (H^q for a
-//                ragged last piece), appends the length block and masks with E(J0); sealing
+//   k_seal_tag   one lane per item: folds the piece partials with H^PIECE_BLOCKS (pieces are
+//                cut from the item's end, so only the first is ragged), appends the length block and masks with E(J0); sealing
 //                stores the tag after the ciphertext, opening compares it (ok flag).
 //
 // GF(2^128) elements are four big-endian words w0..w3 of the block (GCM bit order: the MSB of
@@ -111,17 +111,6 @@ __device__ G4 gmul_slow(G4 x, G4 y) {
             v = gmulx(v);
         }
     return z;
-}
-
-__device__ G4 gpow_slow(G4 h, uint64_t e) {
-    G4 r = {0x80000000u, 0, 0, 0};  // 1
-    G4 b = h;
-    while (e) {
-        if (e & 1) r = gmul_slow(r, b);
-        e >>= 1;
-        if (e) b = gmul_slow(b, b);
-    }
-    return r;
 }
 
 // ------------------------------------------------------------------ AES-256 helpers
@@ -237,6 +226,15 @@ __global__ __launch_bounds__(256) void k_seal_prep(const SealItem* __restrict__ 
     const uint32_t zero[4] = {0, 0, 0, 0};
     const uint32_t j0[4] = {it.nonce[0], it.nonce[1], it.nonce[2], 1u};
     uint32_t hb[4], e0[4];
+    {
+        const uint32_t a0 = it.nonce[0] ^ rk[0], a1 = it.nonce[1] ^ rk[1], a2 = it.nonce[2] ^ rk[2];
+#define TE(x, r) ror32(s_te[(x) & 0xff], (r))
+        K.R1[0] = TE(a0 >> 24, 0) ^ TE(a1 >> 16, 8) ^ TE(a2 >> 8, 16) ^ rk[4];
+        K.R1[1] = TE(a1 >> 24, 0) ^ TE(a2 >> 16, 8) ^ TE(a0, 24) ^ rk[5];
+        K.R1[2] = TE(a2 >> 24, 0) ^ TE(a0 >> 8, 16) ^ TE(a1, 24) ^ rk[6];
+        K.R1[3] = TE(a0 >> 16, 8) ^ TE(a1 >> 8, 16) ^ TE(a2, 24) ^ rk[7];
+#undef TE
+    }
     aes_encrypt_plain(rk, s_te, zero, hb);
     aes_encrypt_plain(rk, s_te, j0, e0);
     const G4 H = {hb[0], hb[1], hb[2], hb[3]};
@@ -255,63 +253,102 @@ __global__ __launch_bounds__(256) void k_seal_prep(const SealItem* __restrict__ 
 // ------------------------------------------------------------------ k_seal_ctr
 struct SealLds {
     uint32_t te[256][64];       // [byte][Te0 x 32 replicas | Te1 x 32 replicas], at LDS address 0
-    uint32_t gt[256][16][4];    // [byte][wave] Shoup 8-bit table of H^64 (LDS address 64 KiB)
+    uint32_t gt[16][256][4];    // [wave][byte] Shoup 8-bit table of H^64 (contiguous: random bytes spread the banks)
     uint32_t g4[16][6][16][4];  // [wave][level][nibble] Shoup 4-bit tables of H^(2^k)
     uint32_t r8[256], r4[16];   // reduction of 8 / 4 shifted-out bits (xor into w0)
 };
 
 #define SEAL_SEL(k) (0x0c0c0000u | ((4u + (k)) << 8))          // (byte k of w) << 8 | lane_off
-#define SEAL_SELG(k) (0x0c020000u | ((4u + (k)) << 8))         // 0x10000 | (byte k of w) << 8 | off
 
 template <int OFF>
 __device__ __forceinline__ uint32_t te_at(const SealLds& L, uint32_t addr) {
     return *(const uint32_t*)((const uint8_t*)&L.te[0][0] + addr + OFF);
 }
 
-// One AES-256 encryption of the counter block (n0, n1, n2, ctr), all words big-endian.
-__device__ __forceinline__ void aes_ctr_block(const SealLds& L, const uint32_t* rk, uint32_t lane_off, uint32_t n0,
-                                              uint32_t n1, uint32_t n2, uint32_t ctr, uint32_t o[4]) {
-    uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2], s3 = ctr ^ rk[3];
+// Two AES-256 encryptions of counter blocks (n0, n1, n2, ctr), words big-endian, interleaved so
+// one block's LDS lookups overlap the other's xors.  Round 1 starts from r1 (its nonce-word
+// terms, precomputed per item): only the counter word's four lookups remain.
+__device__ __forceinline__ void aes_ctr2(const SealLds& L, const uint32_t* rk, const uint32_t* r1, uint32_t lane_off,
+                                         uint32_t ca, uint32_t cb, uint32_t oa[4], uint32_t ob[4]) {
 #define A0(w, k) te_at<0>(L, __builtin_amdgcn_perm((w), lane_off, SEAL_SEL(k)))
 #define A1(w, k) te_at<128>(L, __builtin_amdgcn_perm((w), lane_off, SEAL_SEL(k)))
-#define COL(a, b, c, d, r) (A0(a, 3) ^ A1(b, 2) ^ __builtin_amdgcn_alignbit(A0(c, 1) ^ A1(d, 0), A0(c, 1) ^ A1(d, 0), 16) ^ (r))
+#define R16(x) __builtin_amdgcn_alignbit((x), (x), 16)
+    uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+    {
+        const uint32_t xa = ca ^ rk[3], xb = cb ^ rk[3];
+        a0 = r1[0] ^ R16(A1(xa, 0)); b0 = r1[0] ^ R16(A1(xb, 0));
+        a1 = r1[1] ^ R16(A0(xa, 1)); b1 = r1[1] ^ R16(A0(xb, 1));
+        a2 = r1[2] ^ A1(xa, 2);      b2 = r1[2] ^ A1(xb, 2);
+        a3 = r1[3] ^ A0(xa, 3);      b3 = r1[3] ^ A0(xb, 3);
+    }
+#define COL(s0, s1, s2, s3, r) (A0(s0, 3) ^ A1(s1, 2) ^ R16(A0(s2, 1) ^ A1(s3, 0)) ^ (r))
 #pragma unroll
-    for (int r = 1; r < 14; r++) {
-        uint32_t t0, t1, t2, t3;
-        {
-            const uint32_t x = A0(s2, 1) ^ A1(s3, 0);
-            t0 = A0(s0, 3) ^ A1(s1, 2) ^ __builtin_amdgcn_alignbit(x, x, 16) ^ rk[4 * r];
-        }
-        {
-            const uint32_t x = A0(s3, 1) ^ A1(s0, 0);
-            t1 = A0(s1, 3) ^ A1(s2, 2) ^ __builtin_amdgcn_alignbit(x, x, 16) ^ rk[4 * r + 1];
-        }
-        {
-            const uint32_t x = A0(s0, 1) ^ A1(s1, 0);
-            t2 = A0(s2, 3) ^ A1(s3, 2) ^ __builtin_amdgcn_alignbit(x, x, 16) ^ rk[4 * r + 2];
-        }
-        {
-            const uint32_t x = A0(s1, 1) ^ A1(s2, 0);
-            t3 = A0(s3, 3) ^ A1(s0, 2) ^ __builtin_amdgcn_alignbit(x, x, 16) ^ rk[4 * r + 3];
-        }
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    for (int r = 2; r < 14; r++) {
+        const uint32_t ta0 = COL(a0, a1, a2, a3, rk[4 * r]), tb0 = COL(b0, b1, b2, b3, rk[4 * r]);
+        const uint32_t ta1 = COL(a1, a2, a3, a0, rk[4 * r + 1]), tb1 = COL(b1, b2, b3, b0, rk[4 * r + 1]);
+        const uint32_t ta2 = COL(a2, a3, a0, a1, rk[4 * r + 2]), tb2 = COL(b2, b3, b0, b1, rk[4 * r + 2]);
+        const uint32_t ta3 = COL(a3, a0, a1, a2, rk[4 * r + 3]), tb3 = COL(b3, b0, b1, b2, rk[4 * r + 3]);
+        a0 = ta0; a1 = ta1; a2 = ta2; a3 = ta3;
+        b0 = tb0; b1 = tb1; b2 = tb2; b3 = tb3;
     }
     // last round: S-box bytes (byte 2 of Te0 and byte 0 of Te1 are S[x]), assembled by v_perm
-#define LAST(a, b, c, d, r) \
-    ((__builtin_amdgcn_perm(A0(a, 3), A0(b, 2), 0x06020c0cu) | __builtin_amdgcn_perm(A1(c, 1), A1(d, 0), 0x0c0c0400u)) ^ (r))
-    o[0] = LAST(s0, s1, s2, s3, rk[56]);
-    o[1] = LAST(s1, s2, s3, s0, rk[57]);
-    o[2] = LAST(s2, s3, s0, s1, rk[58]);
-    o[3] = LAST(s3, s0, s1, s2, rk[59]);
+#define LAST(s0, s1, s2, s3, r) \
+    ((__builtin_amdgcn_perm(A0(s0, 3), A0(s1, 2), 0x06020c0cu) | __builtin_amdgcn_perm(A1(s2, 1), A1(s3, 0), 0x0c0c0400u)) ^ (r))
+    oa[0] = LAST(a0, a1, a2, a3, rk[56]); ob[0] = LAST(b0, b1, b2, b3, rk[56]);
+    oa[1] = LAST(a1, a2, a3, a0, rk[57]); ob[1] = LAST(b1, b2, b3, b0, rk[57]);
+    oa[2] = LAST(a2, a3, a0, a1, rk[58]); ob[2] = LAST(b2, b3, b0, b1, rk[58]);
+    oa[3] = LAST(a3, a0, a1, a2, rk[59]); ob[3] = LAST(b3, b0, b1, b2, rk[59]);
 #undef LAST
 #undef COL
+#undef R16
 #undef A1
 #undef A0
 }
 
+// CTR xor of block g of the item (keystream ks) from s to d; returns the GHASH input (the
+// ciphertext, zero-padded past the end of the item).
+template <bool DEC>
+__device__ __forceinline__ G4 crypt_block(const uint8_t* s, uint8_t* d, uint64_t len, uint64_t g, const uint32_t ks[4]) {
+    const uint64_t at = 16 * g;
+    uint32_t in[4];
+    const bool full = at + 16 <= len;
+    if (full) {
+        const uint4 v = *(const uint4*)(s + at);
+        in[0] = __builtin_bswap32(v.x); in[1] = __builtin_bswap32(v.y);
+        in[2] = __builtin_bswap32(v.z); in[3] = __builtin_bswap32(v.w);
+    } else {
+        const uint32_t nb = (uint32_t)(len - at);
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if ((uint32_t)(4 * w + b) < nb) x |= (uint32_t)s[at + 4 * w + b] << (24 - 8 * b);
+            in[w] = x;
+        }
+    }
+    uint32_t out[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) out[w] = in[w] ^ ks[w];
+    if (full) {
+        *(uint4*)(d + at) = make_uint4(__builtin_bswap32(out[0]), __builtin_bswap32(out[1]), __builtin_bswap32(out[2]),
+                                       __builtin_bswap32(out[3]));
+    } else {
+        const uint32_t nb = (uint32_t)(len - at);
+        for (uint32_t b = 0; b < nb; b++) d[at + b] = (uint8_t)(out[b >> 2] >> (24 - 8 * (b & 3)));
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int v = (int)nb - 4 * w;  // valid bytes of word w (big-endian)
+            out[w] &= v >= 4 ? ~0u : (v <= 0 ? 0u : ~0u << (32 - 8 * v));
+        }
+    }
+    const uint32_t* c = DEC ? in : out;  // GHASH runs over the ciphertext
+    return {c[0], c[1], c[2], c[3]};
+}
+
 // Z = X * H^64 with this wave's 8-bit table: Horner over the bytes of X from the last
-__device__ __forceinline__ G4 gmul_h64(const SealLds& L, G4 x, uint32_t goff) {
-    const uint8_t* gbase = (const uint8_t*)&L.te[0][0];  // gt sits at +64 KiB: SEAL_SELG sets bit 16
+__device__ __forceinline__ G4 gmul_h64(const SealLds& L, G4 x, uint32_t wid) {
+    const uint8_t* gbase = (const uint8_t*)&L.gt[wid][0][0];
     const uint32_t xw[4] = {x.w0, x.w1, x.w2, x.w3};
     G4 z = {0, 0, 0, 0};
 #pragma unroll
@@ -323,8 +360,8 @@ __device__ __forceinline__ G4 gmul_h64(const SealLds& L, G4 x, uint32_t goff) {
             z.w1 = __builtin_amdgcn_alignbyte(z.w0, z.w1, 1);
             z.w0 = (z.w0 >> 8) ^ L.r8[rem];
         }
-        const uint32_t a = __builtin_amdgcn_perm(xw[i >> 2], goff, SEAL_SELG(3 - (i & 3)));
-        const uint4 m = *(const uint4*)(gbase + a);
+        const uint32_t b = (xw[i >> 2] >> (8 * (3 - (i & 3)))) & 0xff;
+        const uint4 m = *(const uint4*)(gbase + (b << 4));
         z.w0 ^= m.x; z.w1 ^= m.y; z.w2 ^= m.z; z.w3 ^= m.w;
     }
     return z;
@@ -382,7 +419,6 @@ __global__ __launch_bounds__(SEAL_THREADS) void k_seal_ctr(const uint8_t* __rest
     }
     __syncthreads();
     const uint32_t lane_off = (lane & 31) * 4;
-    const uint32_t goff = 0x10000u | (wid << 4);  // perm operand: byte 2 = 1 (64 KiB), byte 0 = wave column
 
     for (uint64_t p = (uint64_t)blockIdx.x * (SEAL_THREADS / 64) + wid; p < n_pieces;
          p += (uint64_t)gridDim.x * (SEAL_THREADS / 64)) {
@@ -397,8 +433,12 @@ __global__ __launch_bounds__(SEAL_THREADS) void k_seal_ctr(const uint8_t* __rest
         const SealItem& it = items[ii];
         const SealKey& K = keys[ii];
         const uint64_t len = it.len, m = (len + 15) / 16;
-        const uint64_t b0 = (p - it.piece0) * PIECE_BLOCKS;
-        const uint32_t q = (uint32_t)(m - b0 < PIECE_BLOCKS ? m - b0 : PIECE_BLOCKS);
+        // pieces are cut from the end: the first takes the ragged remainder, so every later piece is
+        // full and k_seal_tag folds them with the one multiplier H^PIECE_BLOCKS
+        const uint64_t pi = p - it.piece0, np = (m + PIECE_BLOCKS - 1) / PIECE_BLOCKS;
+        const uint64_t first = m - (np - 1) * PIECE_BLOCKS;
+        const uint64_t b0 = pi == 0 ? 0 : first + (pi - 1) * PIECE_BLOCKS;
+        const uint32_t q = (uint32_t)(pi == 0 ? first : PIECE_BLOCKS);
         // this wave's tables: 8-bit Shoup table of H^64 (4 entries per lane), 4-bit tables of H^(2^k)
         {
             G4 basis[8];
@@ -412,7 +452,7 @@ __global__ __launch_bounds__(SEAL_THREADS) void k_seal_ctr(const uint8_t* __rest
 #pragma unroll
                 for (int j = 0; j < 8; j++)
                     if (b & (0x80u >> j)) e = gxor(e, basis[j]);
-                st4(L.gt[b][wid], e);
+                st4(L.gt[wid][b], e);
             }
             for (uint32_t pr = lane; pr < 96; pr += 64) {
                 const uint32_t k = pr >> 4, nib = pr & 15;
@@ -432,54 +472,24 @@ __global__ __launch_bounds__(SEAL_THREADS) void k_seal_ctr(const uint8_t* __rest
         uint32_t rk[60];
 #pragma unroll
         for (int w = 0; w < 60; w++) rk[w] = K.rk[w];
-        const uint32_t n0 = it.nonce[0], n1 = it.nonce[1], n2 = it.nonce[2];
         const uint8_t* s = src + it.src_off;
         uint8_t* d = dst + it.dst_off;
         const uint32_t S = (q + 63) / 64, pad = 64 * S - q;
         G4 X = {0, 0, 0, 0};
-        for (uint32_t j = 0; j < S; j++) {
-            if (j) X = gmul_h64(L, X, goff);
-            const int32_t r = (int32_t)(lane + 64 * j) - (int32_t)pad;
-            if (r >= 0) {
-                const uint64_t g = b0 + (uint32_t)r;  // block index inside the item
-                uint32_t ks[4];
-                aes_ctr_block(L, rk, lane_off, n0, n1, n2, (uint32_t)(g + 2), ks);  // inc32 from J0 = nonce||1
-                const uint64_t at = 16 * g;
-                uint32_t in[4];
-                const bool full = at + 16 <= len;
-                if (full) {
-                    const uint4 v = *(const uint4*)(s + at);
-                    in[0] = __builtin_bswap32(v.x); in[1] = __builtin_bswap32(v.y);
-                    in[2] = __builtin_bswap32(v.z); in[3] = __builtin_bswap32(v.w);
-                } else {
-                    const uint32_t nb = (uint32_t)(len - at);
+        uint32_t r1[4];
 #pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        uint32_t x = 0;
-#pragma unroll
-                        for (int b = 0; b < 4; b++)
-                            if ((uint32_t)(4 * w + b) < nb) x |= (uint32_t)s[at + 4 * w + b] << (24 - 8 * b);
-                        in[w] = x;
-                    }
-                }
-                uint32_t out[4];
-#pragma unroll
-                for (int w = 0; w < 4; w++) out[w] = in[w] ^ ks[w];
-                if (full) {
-                    *(uint4*)(d + at) = make_uint4(__builtin_bswap32(out[0]), __builtin_bswap32(out[1]),
-                                                   __builtin_bswap32(out[2]), __builtin_bswap32(out[3]));
-                } else {
-                    const uint32_t nb = (uint32_t)(len - at);
-                    for (uint32_t b = 0; b < nb; b++) d[at + b] = (uint8_t)(out[b >> 2] >> (24 - 8 * (b & 3)));
-                    // GHASH sees the ciphertext zero-padded to the block
-#pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        const int v = (int)nb - 4 * w;  // valid bytes of word w (big-endian)
-                        out[w] &= v >= 4 ? ~0u : (v <= 0 ? 0u : ~0u << (32 - 8 * v));
-                    }
-                }
-                const uint32_t* c = DEC ? in : out;  // GHASH runs over the ciphertext
-                X.w0 ^= c[0]; X.w1 ^= c[1]; X.w2 ^= c[2]; X.w3 ^= c[3];
+        for (int w = 0; w < 4; w++) r1[w] = K.R1[w];
+        // two blocks per lane per step (j, j + 1): their AES runs interleaved, GHASH stays in order
+        for (uint32_t j = 0; j < S; j += 2) {
+            const int32_t ra = (int32_t)(lane + 64 * j) - (int32_t)pad;  // >= -63; rb = ra + 64 >= 1
+            const uint64_t ga = b0 + (uint32_t)(ra < 0 ? 0 : ra), gb = b0 + (uint32_t)(ra + 64);
+            uint32_t ksa[4], ksb[4];
+            aes_ctr2(L, rk, r1, lane_off, (uint32_t)(ga + 2), (uint32_t)(gb + 2), ksa, ksb);  // inc32 of J0 = nonce||1
+            if (j) X = gmul_h64(L, X, wid);
+            if (ra >= 0) X = gxor(X, crypt_block<DEC>(s, d, len, ga, ksa));
+            if (j + 1 < S) {  // wave-uniform
+                X = gmul_h64(L, X, wid);
+                X = gxor(X, crypt_block<DEC>(s, d, len, gb, ksb));
             }
         }
         // fold the 64 lane partials: T = sum_l X_l * H^(63 - l)
@@ -508,14 +518,10 @@ __global__ __launch_bounds__(256) void k_seal_tag(const uint8_t* __restrict__ sr
     const uint64_t np = (m + PIECE_BLOCKS - 1) / PIECE_BLOCKS;
     const G4 H = ld4(K.H);
     G4 acc = {0, 0, 0, 0};
+    const G4 HP = ld4(K.HP);
     for (uint64_t pi = 0; pi < np; pi++) {
         const G4 T = ld4(parts + 4 * (it.piece0 + pi));
-        if (pi == 0) {
-            acc = T;
-        } else {
-            const uint64_t q = pi + 1 == np ? m - pi * PIECE_BLOCKS : PIECE_BLOCKS;
-            acc = gxor(gmul_slow(acc, q == PIECE_BLOCKS ? ld4(K.HP) : gpow_slow(H, q)), T);
-        }
+        acc = pi == 0 ? T : gxor(gmul_slow(acc, HP), T);  // every piece after the first is full
     }
     const uint64_t bits = len * 8;
     const G4 Lb = {0, 0, (uint32_t)(bits >> 32), (uint32_t)bits};

@@ -82,6 +82,8 @@ def main():
                     help="batches start in pinned host memory (H2D copies overlapped with processing)")
     ap.add_argument("--trees", action="store_true",
                     help="also time the file-tree blobs of the last batch (bw_tree_blobs, §8f row 1)")
+    ap.add_argument("--seal", action="store_true",
+                    help="also time sealing the last batch's unique blobs (HKDF + AES-256-GCM, §8f row 3)")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
@@ -240,6 +242,7 @@ def main():
         roofline.update({"host_stream_pcie_frac": round(value / PCIE_PEAK_GBS, 4)})
 
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None
+    seal = time_seal(ctx, data, res, file_off, args.steps) if args.seal else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
@@ -266,6 +269,8 @@ def main():
                 "roofline": roofline, "cpu_baseline": cpu, "parity": check}
         if trees:
             line["file_trees"] = trees
+        if seal:
+            line["seal"] = seal
         print(json.dumps(line), flush=True)
     if multi:
         dist.destroy_process_group()
@@ -308,6 +313,43 @@ def time_file_trees(ctx, res, file_len, reps):
     return {"trees": nf, "pieces": int(len(pieces)), "ms": round(best * 1e3, 2),
             "trees_per_s": round(nf / best, 1), "bytes_serialized": int(pieces["length"].sum()),
             "bit_exact_sample": bool(ok)}
+
+
+def time_seal(ctx, data, res, file_off, reps):
+    """Seal every unique blob of the last batch in HBM (derive_backup_key(hash) + AES-256-GCM,
+    pack.rs:70-80), as the packer would after compression; the blob bytes stand in for the zstd
+    payload (synthetic data is incompressible, so level-3 zstd stores it raw).  Timed over `reps`
+    calls with events on the context stream; spot-checked against the oracle."""
+    import numpy as np
+    import torch
+    from oracle import oracle
+    u = res[res["is_dup"] == 0]
+    fo = np.asarray(file_off, dtype=np.uint64)
+    src_off = fo[u["file"].astype(np.int64)] + u["offset"]
+    lens = u["length"].astype(np.uint64)
+    dst_off = np.concatenate([[0], np.cumsum(lens + 16)[:-1]]).astype(np.uint64)
+    total = int(np.sum(lens + 16))
+    dst = torch.empty(total, dtype=torch.uint8, device=data.device)
+    nonces = np.random.default_rng(1).integers(0, 256, (len(u), 12), dtype=np.uint8)
+    prk = bytes(range(32))
+    ctx.seal_device(prk, data.data_ptr(), src_off, lens, u["digest"], nonces, dst.data_ptr(), dst_off)  # warm-up
+    torch.cuda.synchronize()
+    # the context runs on its own stream (torch's default stream is the null handle), so the
+    # calls are bracketed by device-wide synchronizes and timed on the host clock
+    t0 = time.perf_counter()
+    for _ in range(max(1, reps)):
+        ctx.seal_device(prk, data.data_ptr(), src_off, lens, u["digest"], nonces, dst.data_ptr(), dst_off)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / max(1, reps)
+    ok = True
+    for i in np.random.default_rng(2).integers(0, len(u), 4):
+        pt = data[int(src_off[i]):int(src_off[i] + lens[i])].cpu().numpy()
+        got = dst[int(dst_off[i]):int(dst_off[i] + lens[i]) + 16].cpu().numpy().tobytes()
+        ok = ok and got == oracle.seal_blob(prk, bytes(u["digest"][i]), bytes(nonces[i]), pt)
+    payload = int(np.sum(lens))
+    return {"blobs": int(len(u)), "payload_bytes": payload, "ms": round(ms, 3),
+            "GBps": round(payload / (ms * 1e-3) / 1e9, 1),
+            "hbm_algorithmic_bytes": payload + total, "bit_exact_sample": bool(ok)}
 
 
 def pmc_traffic(args, kernel):
