@@ -10,6 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BW_LIB") or os.path.join(HERE, "libbackuwup_amd.so")
 
 BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -1, -2, -3, -4, -5, -6
+BW_ECRYPTO, BW_EFORMAT = -7, -8
 BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -43,6 +44,21 @@ class BwTreeBlob(ctypes.Structure):
     _fields_ = [("tree", ctypes.c_uint64), ("piece", ctypes.c_uint64), ("length", ctypes.c_uint64),
                 ("hash", ctypes.c_uint8 * 32), ("is_dup", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 7)]
 
+
+class BwPackfile(ctypes.Structure):
+    _fields_ = [("first_blob", ctypes.c_uint64), ("n_blobs", ctypes.c_uint64), ("offset", ctypes.c_uint64),
+                ("size", ctypes.c_uint64), ("header_len", ctypes.c_uint64)]
+
+
+class BwIndexFile(ctypes.Structure):
+    _fields_ = [("file_num", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("offset", ctypes.c_uint64),
+                ("size", ctypes.c_uint64), ("n_entries", ctypes.c_uint64)]
+
+
+BW_PACKFILE_TARGET_SIZE, BW_PACKFILE_MAX_SIZE, BW_PACKFILE_MAX_BLOBS = 3 * 1024 * 1024, 16 * 1024 * 1024, 100_000
+BW_BLOB_NONCE_SIZE, BW_INDEX_MAX_FILE_ENTRIES, BW_INDEX_ENTRY_BYTES = 12, 50_000, 44
+BW_BLOB_FILE_CHUNK, BW_BLOB_TREE = 0, 1
+BW_PACK_ZSTD_STORE = 1
 
 BW_TREE_FILE, BW_TREE_DIR = 0, 1
 BW_TREE_HAS_SIZE, BW_TREE_HAS_MTIME, BW_TREE_HAS_CTIME = 1, 2, 4
@@ -84,6 +100,17 @@ SIGNATURES = [
                                       u64p, u8p]),
     ("bw_seal", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp, u64p]),
     ("bw_open", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp, u64p, u8p]),
+    ("bw_zstd_store_size", ctypes.c_uint64, [ctypes.c_uint64]),
+    ("bw_pack_plan", ctypes.c_int, [u64p, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(BwPackfile),
+                                    ctypes.c_uint64, u64p, u64p]),
+    ("bw_pack_build_device", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint32,
+                                            ctypes.POINTER(BwPackfile), ctypes.c_uint64, vp, vp]),
+    ("bw_pack_build", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint32,
+                                     ctypes.POINTER(BwPackfile), ctypes.c_uint64, vp, vp]),
+    ("bw_index_files_build", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64,
+                                            ctypes.POINTER(BwIndexFile), ctypes.c_uint64, u64p, u64p]),
+    ("bw_index_load_files", ctypes.c_int, [vp, vp, vp, ctypes.POINTER(BwIndexFile), ctypes.c_uint64, vp,
+                                           ctypes.c_uint64, u64p, u64p]),
     ("bw_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
 ]

@@ -41,6 +41,9 @@ assert TREE_DTYPE.itemsize == ctypes.sizeof(_lib.BwTree) == 64
 TREE_BLOB_DTYPE = np.dtype([("tree", "<u8"), ("piece", "<u8"), ("length", "<u8"), ("hash", "u1", (32,)),
                             ("is_dup", "u1"), ("pad", "u1", (7,))])
 assert TREE_BLOB_DTYPE.itemsize == ctypes.sizeof(_lib.BwTreeBlob) == 64
+PACKFILE_DTYPE = np.dtype([("first_blob", "<u8"), ("n_blobs", "<u8"), ("offset", "<u8"), ("size", "<u8"),
+                           ("header_len", "<u8")])
+assert PACKFILE_DTYPE.itemsize == ctypes.sizeof(_lib.BwPackfile) == 40
 
 
 def make_tree(kind, name, size=None, mtime=None, ctime=None, children=b""):
@@ -275,6 +278,87 @@ class Context:
                                     out.ctypes.data_as(ctypes.POINTER(_lib.BwTreeBlob)), cap, ctypes.byref(n)),
               self.h)
         return hashes[:len(trees)], out[:n.value]
+
+    # -------------------------------------------------------------- packfiles / index files (§8f row 4)
+    def pack_plan(self, payload_len, flags=_lib.BW_PACK_ZSTD_STORE):
+        """write_packfiles' grouping (pack.rs:123-148): PACKFILE_DTYPE records and total bytes."""
+        pl = np.ascontiguousarray(payload_len, dtype=np.uint64)
+        n, total = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self._L.bw_pack_plan(pl.ctypes.data_as(_lib.u64p), pl.size, flags, None, 0, ctypes.byref(n),
+                                  ctypes.byref(total))
+        if rc not in (_lib.BW_OK, _lib.BW_ENOSPC):
+            check(rc)
+        out = np.zeros(max(n.value, 1), dtype=PACKFILE_DTYPE)
+        check(self._L.bw_pack_plan(pl.ctypes.data_as(_lib.u64p), pl.size, flags,
+                                   out.ctypes.data_as(ctypes.POINTER(_lib.BwPackfile)), n.value, ctypes.byref(n),
+                                   ctypes.byref(total)))
+        return out[:n.value], total.value
+
+    def _pack_args(self, prk, src_off, src_len, hashes, kinds, nonces, plan, packfile_ids):
+        so = np.ascontiguousarray(src_off, dtype=np.uint64)
+        sl = np.ascontiguousarray(src_len, dtype=np.uint64)
+        h = np.ascontiguousarray(np.asarray(hashes, dtype=np.uint8).reshape(-1, 32))
+        kd = np.ascontiguousarray(kinds, dtype=np.uint8)
+        no = np.ascontiguousarray(np.asarray(nonces, dtype=np.uint8).reshape(-1, 12))
+        pl = np.ascontiguousarray(plan, dtype=PACKFILE_DTYPE)
+        ids = np.ascontiguousarray(np.asarray(packfile_ids, dtype=np.uint8).reshape(-1, 12))
+        assert so.size == sl.size == h.shape[0] == kd.size == no.shape[0] and ids.shape[0] >= pl.size
+        k = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(prk))
+        keep = (so, sl, h, kd, no, pl, ids, k)
+        return keep, [k, None, so.ctypes.data_as(_lib.u64p), sl.ctypes.data_as(_lib.u64p), so.size, _ptr(h), _ptr(kd),
+                      _ptr(no)], [pl.ctypes.data_as(ctypes.POINTER(_lib.BwPackfile)), pl.size, _ptr(ids)]
+
+    def pack_build(self, prk, src, src_off, src_len, hashes, kinds, nonces, plan, total, packfile_ids,
+                   flags=_lib.BW_PACK_ZSTD_STORE):
+        """Host buffers: the planned packfiles back to back (numpy u8, `total` bytes)."""
+        buf = _as_u8(src)
+        keep, a, b = self._pack_args(prk, src_off, src_len, hashes, kinds, nonces, plan, packfile_ids)
+        a[1] = _ptr(buf)
+        out = np.zeros(max(int(total), 1), dtype=np.uint8)
+        check(self._L.bw_pack_build(self.h, *a, flags, *b, _ptr(out)), self.h)
+        return out[:int(total)]
+
+    def pack_build_device(self, prk, d_src, src_off, src_len, hashes, kinds, nonces, plan, packfile_ids, d_out,
+                          flags=_lib.BW_PACK_ZSTD_STORE):
+        """Device pointers (ints) for the payloads and the output; asynchronous on the context stream."""
+        keep, a, b = self._pack_args(prk, src_off, src_len, hashes, kinds, nonces, plan, packfile_ids)
+        a[1] = ctypes.c_void_p(d_src)
+        check(self._L.bw_pack_build_device(self.h, *a, flags, *b, ctypes.c_void_p(d_out)), self.h)
+        self._keep = keep
+
+    def index_files_build(self, prk, entries, last_file_num=0):
+        """BlobIndex::push + flush over n (hash, packfile id) entries (n x 44 bytes):
+        [(file_num, bytes)] as the reference writes them to index/{file_num:0>10}."""
+        e = np.ascontiguousarray(np.asarray(entries, dtype=np.uint8).reshape(-1, 44))
+        k = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(prk))
+        nf, total = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self._L.bw_index_files_build(self.h, k, _ptr(e), e.shape[0], last_file_num, None, 0, None, 0,
+                                          ctypes.byref(nf), ctypes.byref(total))
+        if rc != _lib.BW_ENOSPC:
+            check(rc, self.h)
+        out = np.zeros(max(total.value, 1), dtype=np.uint8)
+        tab = (_lib.BwIndexFile * nf.value)()
+        check(self._L.bw_index_files_build(self.h, k, _ptr(e), e.shape[0], last_file_num, _ptr(out), out.size, tab,
+                                           nf.value, ctypes.byref(nf), ctypes.byref(total)), self.h)
+        return [(t.file_num, out[t.offset:t.offset + t.size].tobytes()) for t in tab]
+
+    def index_load_files(self, prk, files, want_entries=True):
+        """BlobIndex::load fused with the device seed: files = [(file_num, bytes)].  Returns the
+        (n x 44) records in file order (or their count)."""
+        blobs = [bytes(b) for _, b in files]
+        data = np.frombuffer(b"".join(blobs) or b"\0", dtype=np.uint8)
+        tab = (_lib.BwIndexFile * max(len(files), 1))()
+        off = 0
+        for i, (num, b) in enumerate(zip([f for f, _ in files], blobs)):
+            tab[i].file_num, tab[i].offset, tab[i].size = num, off, len(b)
+            off += len(b)
+        k = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(prk))
+        n, bad = ctypes.c_uint64(), ctypes.c_uint64()
+        cap = sum(max(len(b) - 17, 0) // 44 + 1 for b in blobs)
+        out = np.zeros((max(cap, 1), 44), dtype=np.uint8) if want_entries else None
+        check(self._L.bw_index_load_files(self.h, k, _ptr(data), tab, len(files), _ptr(out) if want_entries else None,
+                                          cap if want_entries else 0, ctypes.byref(n), ctypes.byref(bad)), self.h)
+        return out[:n.value] if want_entries else n.value
 
     # -------------------------------------------------------------- stage timing
     def profile_enable(self, on=True):

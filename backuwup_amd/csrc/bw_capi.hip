@@ -52,6 +52,14 @@ struct bw_ctx {
     hipEvent_t seal_done = nullptr;  // seal_stage reusable once this fired
     bool seal_pending = false;
 
+    // packfiles / index files (bw_pack.hip): tables, zstd staging, header plaintexts, host I/O
+    DevBuf pk_blobs, pk_files, pk_store, pk_stage, pk_hdr, pk_src, pk_out, ix_io, ix_tab, ix_dig;
+    std::vector<PackBlob> h_pk_blobs;
+    std::vector<PackFileDesc> h_pk_files;
+    std::vector<StoreItem> h_pk_store;
+    hipEvent_t pk_done = nullptr;  // the host tables above reusable once this fired
+    bool pk_pending = false;
+
     // persistent dedup index
     DevBuf table, log, dstate;
     uint64_t table_cap = 0, log_cap = 0, log_hi = 0;  // log_hi: host upper bound of log length
@@ -191,6 +199,8 @@ extern "C" const char* bw_strerror(int rc) {
         case BW_ENOMEM: return "out of memory";
         case BW_ECOLLISION: return "64-bit digest key collision in the index";
         case BW_ESTATE: return "invalid call order";
+        case BW_ECRYPTO: return "AES-GCM authentication failed";
+        case BW_EFORMAT: return "malformed bincode data";
         default: return "unknown error";
     }
 }
@@ -226,12 +236,14 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->digests,
                      &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->table,
                      &c->log, &c->dstate, &c->seal_items, &c->seal_keys, &c->seal_parts, &c->seal_ok,
-                     &c->seal_io};
+                     &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_store, &c->pk_stage, &c->pk_hdr,
+                     &c->pk_src, &c->pk_out, &c->ix_io, &c->ix_tab, &c->ix_dig};
     for (DevBuf* b : all)
         if (b->p) hipFree(b->p);
     if (c->stage.p) hipHostFree(c->stage.p);
     if (c->seal_stage.p) hipHostFree(c->seal_stage.p);
     if (c->seal_done) hipEventDestroy(c->seal_done);
+    if (c->pk_done) hipEventDestroy(c->pk_done);
     if (c->meta_done) hipEventDestroy(c->meta_done);
     for (int k = 0; k < 2; k++)
         for (int i = 0; i <= BW_N_STAGES; i++)
@@ -851,4 +863,327 @@ extern "C" int bw_open(bw_ctx* c, const uint8_t prk[32], const uint8_t* src, con
                        const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
                        const uint8_t* nonces, uint8_t* dst, const uint64_t* dst_off, uint8_t* ok) {
     return seal_host(c, true, prk, src, src_off, src_len, n, info, info_len, nonces, dst, dst_off, ok);
+}
+
+// ------------------------------------------------------------------ packfiles (§8f row 4)
+// Manager::write_packfiles / serialize_packfile (pack.rs:115-227); kernels in bw_pack.hip.
+
+static uint32_t varint_len(uint64_t v) { return v < 251 ? 1 : (v < (1ull << 16) ? 3 : (v < (1ull << 32) ? 5 : 9)); }
+
+extern "C" uint64_t bw_zstd_store_size(uint64_t len) {
+    const uint64_t nb = len ? (len + ZSTD_BLOCK - 1) / ZSTD_BLOCK : 1;
+    return 2 + 3 * nb + len;
+}
+
+static uint64_t sealed_len_of(uint64_t payload, uint32_t flags) {
+    return (flags & BW_PACK_ZSTD_STORE ? bw_zstd_store_size(payload) : payload) + BW_SEAL_TAG_BYTES;
+}
+
+// header plaintext bytes of a PackfileHeaderBlob entry
+static uint64_t entry_len(uint64_t sealed, uint64_t section_off) {
+    return 32 + 1 + 1 + varint_len(sealed) + varint_len(section_off);
+}
+
+static void plan_packfiles(const uint64_t* payload_len, uint64_t n, uint32_t flags, std::vector<bw_packfile>& out) {
+    uint64_t i = 0, off = 0;
+    while (i < n) {
+        bw_packfile p{};
+        p.first_blob = i;
+        uint64_t written = 0, hdr = 0;
+        while (i < n) {
+            const uint64_t sealed = sealed_len_of(payload_len[i], flags);
+            hdr += entry_len(sealed, written);
+            written += sealed + BW_BLOB_NONCE_SIZE;
+            p.n_blobs++;
+            i++;
+            if (written >= BW_PACKFILE_TARGET_SIZE || p.n_blobs >= BW_PACKFILE_MAX_BLOBS) break;
+        }
+        hdr += varint_len(p.n_blobs);
+        p.header_len = hdr + BW_SEAL_TAG_BYTES;
+        p.offset = off;
+        p.size = 8 + p.header_len + written;
+        off += p.size;
+        out.push_back(p);
+    }
+}
+
+extern "C" int bw_pack_plan(const uint64_t* payload_len, uint64_t n, uint32_t flags, bw_packfile* out, uint64_t cap,
+                            uint64_t* n_out, uint64_t* total_bytes) {
+    if (!n_out || !total_bytes || (n && !payload_len) || (cap && !out)) return BW_EINVAL;
+    std::vector<bw_packfile> pl;
+    plan_packfiles(payload_len, n, flags, pl);
+    *n_out = pl.size();
+    *total_bytes = pl.empty() ? 0 : pl.back().offset + pl.back().size;
+    if (pl.size() > cap) return BW_ENOSPC;
+    std::copy(pl.begin(), pl.end(), out);
+    return BW_OK;
+}
+
+static int pack_submit(bw_ctx* c, const uint8_t* prk, const uint8_t* d_src, const uint64_t* src_off,
+                       const uint64_t* src_len, uint64_t n, const uint8_t* hashes, const uint8_t* kinds,
+                       const uint8_t* nonces, uint32_t flags, const bw_packfile* plan, uint64_t npf,
+                       const uint8_t* ids, uint8_t* d_out) {
+    if (!c || !prk || (flags & ~BW_PACK_ZSTD_STORE)) return BW_EINVAL;
+    if (n && (!d_src || !src_off || !src_len || !hashes || !kinds || !nonces)) return BW_EINVAL;
+    if (npf && (!plan || !ids || !d_out)) return BW_EINVAL;
+    hipSetDevice(c->device);
+    // the plan must be the reference's grouping of exactly these blobs
+    std::vector<bw_packfile> want;
+    plan_packfiles(src_len, n, flags, want);
+    if (want.size() != npf) return BW_EINVAL;
+    for (uint64_t p = 0; p < npf; p++) {
+        const bw_packfile &a = want[p], &b = plan[p];
+        if (a.first_blob != b.first_blob || a.n_blobs != b.n_blobs || a.offset != b.offset || a.size != b.size ||
+            a.header_len != b.header_len) {
+            c->err = "packfile plan does not match the blobs (use bw_pack_plan)";
+            return BW_EINVAL;
+        }
+        if (a.size > BW_PACKFILE_MAX_SIZE) {
+            c->err = "bug: violated packfile size limit";  // pack.rs:152-156 asserts
+            return BW_EINVAL;
+        }
+    }
+    for (uint64_t i = 0; i < n; i++)
+        if (kinds[i] > BW_BLOB_TREE || ((flags & BW_PACK_ZSTD_STORE) && src_len[i] > (1ull << 31))) return BW_EINVAL;
+    if (!n) return BW_OK;
+    if (!c->pk_done) HIPCHK(c, hipEventCreateWithFlags(&c->pk_done, hipEventDisableTiming));
+    if (c->pk_pending) {
+        hipEventSynchronize(c->pk_done);
+        c->pk_pending = false;
+    }
+    const bool store = flags & BW_PACK_ZSTD_STORE;
+    c->h_pk_blobs.resize(n);
+    c->h_pk_files.resize(npf);
+    c->h_pk_store.resize(store ? n : 0);
+    std::vector<uint64_t> s_off(n), s_len(n), d_off(n), h_off(npf), h_len(npf), h_dst(npf);
+    uint64_t hdr_total = 0, stage_total = 0, units = 0;
+    for (uint64_t p = 0; p < npf; p++) {
+        const bw_packfile& f = plan[p];
+        h_off[p] = hdr_total;
+        h_len[p] = f.header_len - BW_SEAL_TAG_BYTES;
+        h_dst[p] = f.offset + 8;
+        c->h_pk_files[p] = PackFileDesc{hdr_total, f.n_blobs, f.offset, f.header_len};
+        uint64_t entry = hdr_total + varint_len(f.n_blobs), section = 0;
+        const uint64_t data0 = f.offset + 8 + f.header_len;
+        for (uint64_t i = f.first_blob; i < f.first_blob + f.n_blobs; i++) {
+            const uint64_t frame = store ? bw_zstd_store_size(src_len[i]) : src_len[i];
+            const uint64_t sealed = frame + BW_SEAL_TAG_BYTES;
+            PackBlob& b = c->h_pk_blobs[i];
+            memcpy(b.hash, hashes + 32 * i, 32);
+            memcpy(b.nonce, nonces + 12 * i, 12);
+            b.kind = kinds[i];
+            b.sealed_len = sealed;
+            b.section_off = section;
+            b.hdr_off = entry;
+            b.nonce_off = data0 + section;
+            entry += entry_len(sealed, section);
+            section += sealed + BW_BLOB_NONCE_SIZE;
+            s_len[i] = frame;
+            d_off[i] = b.nonce_off + BW_BLOB_NONCE_SIZE;
+            if (store) {
+                uint32_t wlog = src_len[i] > 1 ? 64 - __builtin_clzll(src_len[i] - 1) : 0;
+                wlog = std::min(21u, std::max(10u, wlog));
+                c->h_pk_store[i] = StoreItem{src_off[i], src_len[i], stage_total, units, (wlog - 10) << 3, 0};
+                s_off[i] = stage_total;
+                stage_total += (frame + 15) & ~15ull;
+                units += (frame + STORE_UNIT - 1) / STORE_UNIT;
+            } else {
+                s_off[i] = src_off[i];
+            }
+        }
+        hdr_total = entry;
+    }
+    if (int rc = ensure(c, c->pk_blobs, n * sizeof(PackBlob))) return rc;
+    if (int rc = ensure(c, c->pk_files, npf * sizeof(PackFileDesc))) return rc;
+    if (int rc = ensure(c, c->pk_hdr, hdr_total)) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->pk_blobs.p, c->h_pk_blobs.data(), n * sizeof(PackBlob), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->pk_files.p, c->h_pk_files.data(), npf * sizeof(PackFileDesc), hipMemcpyHostToDevice,
+                             c->stream));
+    const uint8_t* seal_src = d_src;
+    if (store) {
+        if (int rc = ensure(c, c->pk_store, n * sizeof(StoreItem))) return rc;
+        if (int rc = ensure(c, c->pk_stage, stage_total)) return rc;
+        HIPCHK(c, hipMemcpyAsync(c->pk_store.p, c->h_pk_store.data(), n * sizeof(StoreItem), hipMemcpyHostToDevice,
+                                 c->stream));
+        launch_zstd_store(c->stream, d_src, P<uint8_t>(c->pk_stage), P<StoreItem>(c->pk_store), n, units);
+        seal_src = P<uint8_t>(c->pk_stage);
+    }
+    HIPCHK(c, hipEventRecord(c->pk_done, c->stream));
+    c->pk_pending = true;
+    launch_pack_meta(c->stream, P<PackBlob>(c->pk_blobs), n, P<PackFileDesc>(c->pk_files), npf, P<uint8_t>(c->pk_hdr),
+                     d_out);
+    HIPCHK(c, hipGetLastError());
+    // every blob: derive_backup_key(hash) + AES-GCM(nonce) into its place behind its nonce
+    if (int rc = seal_submit(c, false, prk, seal_src, s_off.data(), s_len.data(), n, hashes, 32, nonces, d_out,
+                             d_off.data(), nullptr))
+        return rc;
+    // every header: derive_backup_key(b"header") + AES-GCM(packfile id) behind the length prefix
+    std::vector<uint8_t> info(npf * 6);
+    for (uint64_t p = 0; p < npf; p++) memcpy(&info[6 * p], "header", 6);
+    return seal_submit(c, false, prk, P<uint8_t>(c->pk_hdr), h_off.data(), h_len.data(), npf, info.data(), 6, ids,
+                       d_out, h_dst.data(), nullptr);
+}
+
+extern "C" int bw_pack_build_device(bw_ctx* c, const uint8_t prk[32], const uint8_t* d_src, const uint64_t* src_off,
+                                    const uint64_t* src_len, uint64_t n, const uint8_t* hashes, const uint8_t* kinds,
+                                    const uint8_t* nonces, uint32_t flags, const bw_packfile* plan, uint64_t npf,
+                                    const uint8_t* ids, uint8_t* d_out) {
+    return pack_submit(c, prk, d_src, src_off, src_len, n, hashes, kinds, nonces, flags, plan, npf, ids, d_out);
+}
+
+extern "C" int bw_pack_build(bw_ctx* c, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,
+                             const uint64_t* src_len, uint64_t n, const uint8_t* hashes, const uint8_t* kinds,
+                             const uint8_t* nonces, uint32_t flags, const bw_packfile* plan, uint64_t npf,
+                             const uint8_t* ids, uint8_t* out) {
+    if (!c || (n && (!src || !src_off || !src_len)) || (npf && (!plan || !out))) return BW_EINVAL;
+    hipSetDevice(c->device);
+    uint64_t s_end = 0;
+    for (uint64_t i = 0; i < n; i++) s_end = std::max(s_end, src_off[i] + src_len[i]);
+    const uint64_t total = npf ? plan[npf - 1].offset + plan[npf - 1].size : 0;
+    if (int rc = ensure(c, c->pk_src, s_end)) return rc;
+    if (int rc = ensure(c, c->pk_out, total)) return rc;
+    if (s_end) HIPCHK(c, hipMemcpyAsync(c->pk_src.p, src, s_end, hipMemcpyHostToDevice, c->stream));
+    if (int rc = pack_submit(c, prk, P<uint8_t>(c->pk_src), src_off, src_len, n, hashes, kinds, nonces, flags, plan,
+                             npf, ids, P<uint8_t>(c->pk_out)))
+        return rc;
+    if (total) HIPCHK(c, hipMemcpyAsync(out, c->pk_out.p, total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BW_OK;
+}
+
+// ------------------------------------------------------------------ index files (§8f row 4)
+// BlobIndex::push/flush/load (blob_index.rs:151-240).
+
+static void counter_to_nonce(uint32_t num, uint8_t nonce[12]) {
+    memset(nonce, 0, 12);
+    for (int k = 0; k < 4; k++) nonce[k] = (uint8_t)(num >> (8 * k));
+}
+
+extern "C" int bw_index_files_build(bw_ctx* c, const uint8_t prk[32], const uint8_t* entries, uint64_t n,
+                                    uint32_t last_file_num, uint8_t* out, uint64_t cap, bw_index_file* files,
+                                    uint64_t files_cap, uint64_t* n_files, uint64_t* total_bytes) {
+    if (!c || !prk || !n_files || !total_bytes || (n && !entries)) return BW_EINVAL;
+    const uint64_t nf = n / BW_INDEX_MAX_FILE_ENTRIES + 1;  // full files, then the final flush
+    if ((uint64_t)last_file_num + nf > 0xffffffffull) {
+        c->err = "bug: index file counter overflow";  // blob_index.rs:207-210 expects
+        return BW_EINVAL;
+    }
+    std::vector<bw_index_file> tab(nf);
+    std::vector<uint64_t> pt_off(nf), pt_len(nf), dst_off(nf);
+    uint64_t off = 0, pt = 0;
+    for (uint64_t f = 0; f < nf; f++) {
+        const uint64_t cnt = f + 1 < nf ? BW_INDEX_MAX_FILE_ENTRIES : n - f * BW_INDEX_MAX_FILE_ENTRIES;
+        pt_off[f] = pt;
+        pt_len[f] = varint_len(cnt) + BW_INDEX_ENTRY_BYTES * cnt;
+        tab[f] = bw_index_file{(uint32_t)(last_file_num + 1 + f), 0, off, pt_len[f] + BW_SEAL_TAG_BYTES, cnt};
+        dst_off[f] = off;
+        pt += pt_len[f];
+        off += tab[f].size;
+    }
+    *n_files = nf;
+    *total_bytes = off;
+    if (!out || cap < off || !files || files_cap < nf) return BW_ENOSPC;
+    // plaintexts: bincode varint Vec<([u8; 32], [u8; 12])>
+    std::vector<uint8_t> plain(pt);
+    std::vector<uint8_t> nonces(12 * nf), info(5 * nf);
+    for (uint64_t f = 0; f < nf; f++) {
+        uint8_t* p = plain.data() + pt_off[f];
+        const uint64_t cnt = tab[f].n_entries;
+        if (cnt < 251) {
+            *p++ = (uint8_t)cnt;
+        } else {
+            *p++ = 251;  // cnt <= 50 000 < 2^16
+            *p++ = (uint8_t)cnt;
+            *p++ = (uint8_t)(cnt >> 8);
+        }
+        memcpy(p, entries + f * BW_INDEX_MAX_FILE_ENTRIES * BW_INDEX_ENTRY_BYTES, cnt * BW_INDEX_ENTRY_BYTES);
+        counter_to_nonce(tab[f].file_num, &nonces[12 * f]);
+        memcpy(&info[5 * f], "index", 5);
+    }
+    if (int rc = bw_seal(c, prk, plain.data(), pt_off.data(), pt_len.data(), nf, info.data(), 5, nonces.data(), out,
+                         dst_off.data()))
+        return rc;
+    std::copy(tab.begin(), tab.end(), files);
+    return BW_OK;
+}
+
+extern "C" int bw_index_load_files(bw_ctx* c, const uint8_t prk[32], const uint8_t* data, const bw_index_file* files,
+                                   uint64_t nf, uint8_t* entries, uint64_t cap, uint64_t* n_entries,
+                                   uint64_t* bad_file) {
+    if (!c || !prk || !n_entries || (nf && (!data || !files))) return BW_EINVAL;
+    *n_entries = 0;
+    if (bad_file) *bad_file = ~0ull;
+    if (!nf) return BW_OK;
+    hipSetDevice(c->device);
+    uint64_t end = 0, pt_total = 0;
+    std::vector<uint64_t> src_off(nf), src_len(nf), pt_off(nf), pt_len(nf);
+    std::vector<uint8_t> nonces(12 * nf), info(5 * nf);
+    for (uint64_t f = 0; f < nf; f++) {
+        if (files[f].size < BW_SEAL_TAG_BYTES) {  // decrypt_in_place fails on a buffer shorter than the tag
+            if (bad_file) *bad_file = f;
+            c->err = "index file shorter than the GCM tag";
+            return BW_ECRYPTO;
+        }
+        src_off[f] = files[f].offset;
+        src_len[f] = files[f].size;
+        end = std::max(end, files[f].offset + files[f].size);
+        pt_off[f] = pt_total;
+        pt_len[f] = files[f].size - BW_SEAL_TAG_BYTES;
+        pt_total += (pt_len[f] + 15) & ~15ull;
+        counter_to_nonce(files[f].file_num, &nonces[12 * f]);
+        memcpy(&info[5 * f], "index", 5);
+    }
+    const uint64_t pt_base = (end + 255) & ~255ull;
+    if (int rc = ensure(c, c->ix_io, pt_base + pt_total + 16)) return rc;
+    uint8_t* io = P<uint8_t>(c->ix_io);
+    HIPCHK(c, hipMemcpyAsync(io, data, end, hipMemcpyHostToDevice, c->stream));
+    std::vector<uint8_t> ok(nf);
+    if (int rc = seal_submit(c, true, prk, io, src_off.data(), src_len.data(), nf, info.data(), 5, nonces.data(),
+                             io + pt_base, pt_off.data(), ok.data()))
+        return rc;
+    for (uint64_t f = 0; f < nf; f++)
+        if (!ok[f]) {
+            if (bad_file) *bad_file = f;
+            c->err = "index file " + std::to_string(files[f].file_num) + " failed authentication";
+            return BW_ECRYPTO;
+        }
+    // parse the Vec length of every file
+    if (int rc = ensure(c, c->ix_tab, nf * 8 * 4)) return rc;
+    uint64_t* tab = P<uint64_t>(c->ix_tab);
+    std::vector<uint64_t> up(2 * nf);
+    std::copy(pt_off.begin(), pt_off.end(), up.begin());
+    std::copy(pt_len.begin(), pt_len.end(), up.begin() + nf);
+    HIPCHK(c, hipMemcpyAsync(tab, up.data(), 2 * nf * 8, hipMemcpyHostToDevice, c->stream));
+    launch_index_parse(c->stream, io + pt_base, tab, tab + nf, nf, tab + 2 * nf);
+    HIPCHK(c, hipGetLastError());
+    std::vector<uint64_t> parsed(2 * nf);
+    HIPCHK(c, hipMemcpyAsync(parsed.data(), tab + 2 * nf, 2 * nf * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> rec0(nf), fsrc(nf);
+    uint64_t R = 0;
+    for (uint64_t f = 0; f < nf; f++) {
+        if (parsed[2 * f] == ~0ull) {
+            if (bad_file) *bad_file = f;
+            c->err = "index file " + std::to_string(files[f].file_num) + " is not a bincode Vec<(BlobHash, PackfileId)>";
+            return BW_EFORMAT;
+        }
+        rec0[f] = R;
+        fsrc[f] = pt_off[f] + parsed[2 * f + 1];
+        R += parsed[2 * f];
+    }
+    *n_entries = R;
+    if (entries && cap < R) return BW_ENOSPC;
+    if (!R) return BW_OK;
+    std::copy(rec0.begin(), rec0.end(), up.begin());
+    std::copy(fsrc.begin(), fsrc.end(), up.begin() + nf);
+    HIPCHK(c, hipMemcpyAsync(tab, up.data(), 2 * nf * 8, hipMemcpyHostToDevice, c->stream));
+    if (int rc = ensure(c, c->ix_dig, R * 32 + (entries ? R * BW_INDEX_ENTRY_BYTES : 0))) return rc;
+    uint8_t* dig = P<uint8_t>(c->ix_dig);
+    uint8_t* rec = entries ? dig + R * 32 : nullptr;
+    launch_index_gather(c->stream, io + pt_base, tab, tab + nf, nf, R, dig, rec);
+    HIPCHK(c, hipGetLastError());
+    if (entries) HIPCHK(c, hipMemcpyAsync(entries, rec, R * BW_INDEX_ENTRY_BYTES, hipMemcpyDeviceToHost, c->stream));
+    if (int rc = dedup_device(c, dig, nullptr, R, R, nullptr)) return rc;
+    return check_collision(c);
 }

@@ -160,4 +160,37 @@ void seal_fill_item(SealItem* it, uint64_t src_off, uint64_t len, uint64_t dst_o
 void launch_seal(hipStream_t st, bool dec, const uint8_t* src, uint8_t* dst, const SealItem* items, uint64_t n,
                  const SealPads& pads, SealKey* keys, uint64_t n_pieces, uint32_t* parts, uint8_t* ok);
 
+// ------------------------------------------------------------------ packfiles / index files (bw_pack.hip)
+constexpr uint32_t ZSTD_BLOCK = 131072;           // zstd ZSTD_BLOCKSIZE_MAX
+constexpr uint32_t ZSTD_STRIDE = ZSTD_BLOCK + 3;  // a raw block with its 3-byte header
+constexpr uint32_t STORE_UNIT = 65536;            // framed bytes per k_zstd_store wave
+
+struct StoreItem {
+    uint64_t src_off, len, stage_off, unit0;  // unit0: first 64 KiB wave task of this item
+    uint32_t wd, pad;                         // window descriptor byte
+};
+
+struct PackBlob {
+    uint8_t hash[32];
+    uint8_t nonce[12];
+    uint32_t kind;          // BlobKind tag
+    uint64_t sealed_len;    // PackfileHeaderBlob.length (compressed + 16-byte tag)
+    uint64_t section_off;   // PackfileHeaderBlob.offset (from the blob section start, at the nonce)
+    uint64_t hdr_off;       // entry position in the header staging buffer
+    uint64_t nonce_off;     // nonce position in the output
+};
+
+struct PackFileDesc {
+    uint64_t hdr_off, count, out_off, header_len;
+};
+
+void launch_zstd_store(hipStream_t st, const uint8_t* src, uint8_t* stage, const StoreItem* items, uint64_t n_items,
+                       uint64_t n_units);
+void launch_pack_meta(hipStream_t st, const PackBlob* blobs, uint64_t n, const PackFileDesc* files, uint64_t n_files,
+                      uint8_t* hdr, uint8_t* out);
+void launch_index_parse(hipStream_t st, const uint8_t* pt, const uint64_t* pt_off, const uint64_t* pt_len,
+                        uint64_t n_files, uint64_t* parsed);
+void launch_index_gather(hipStream_t st, const uint8_t* pt, const uint64_t* file_rec0, const uint64_t* file_src,
+                         uint64_t n_files, uint64_t n_rec, uint8_t* digests, uint8_t* records);
+
 }  // namespace bw

@@ -45,7 +45,9 @@ enum {
     BW_EHIP = -3,       /* HIP runtime error (message in bw_last_error)                        */
     BW_ENOMEM = -4,     /* device or host allocation failed                                    */
     BW_ECOLLISION = -5, /* two distinct digests share a 64-bit table key: verdicts withheld    */
-    BW_ESTATE = -6      /* call order violated (e.g. bw_results before a batch was submitted)   */
+    BW_ESTATE = -6,     /* call order violated (e.g. bw_results before a batch was submitted)   */
+    BW_ECRYPTO = -7,    /* an AES-GCM tag did not verify (PackfileError::CryptoError)           */
+    BW_EFORMAT = -8     /* bincode deserialization failed (PackfileError::SerializationError)   */
 };
 
 /* fastcdc::v2020 size bounds (asserted by FastCDC::with_level) */
@@ -234,6 +236,85 @@ int bw_seal(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* src, const uint64
 int bw_open(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,
             const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
             const uint8_t* nonces, uint8_t* dst, const uint64_t* dst_off, uint8_t* ok);
+
+/* ---- packfiles and index files ----
+ * Manager::write_packfiles + serialize_packfile (pack.rs:115-227): the queue of unique blobs
+ * (already gated by the index, so write_packfiles' re-check at :131 finds nothing) becomes
+ * packfiles laid out back to back in one buffer:
+ *   u64 LE header_len || AES-GCM(key "header", nonce = packfile id)(bincode varint
+ *   Vec<PackfileHeaderBlob{hash, kind, compression = Zstd, length, offset}>) || (nonce || sealed)*
+ * where sealed = AES-GCM(derive_backup_key(hash), nonce)(zstd payload) (pack.rs:58-80).  A
+ * packfile closes when its blob section reaches BW_PACKFILE_TARGET_SIZE or it holds
+ * BW_PACKFILE_MAX_BLOBS blobs (pack.rs:147).  Packfile ids and blob nonces come from the
+ * caller (the reference draws them from getrandom, pack.rs:74-76, :207-208). */
+#define BW_PACKFILE_TARGET_SIZE 3145728u /* packfile/mod.rs:25 */
+#define BW_PACKFILE_MAX_SIZE 16777216u   /* packfile/mod.rs:27 */
+#define BW_PACKFILE_MAX_BLOBS 100000u    /* packfile/mod.rs:29 */
+#define BW_BLOB_NONCE_SIZE 12u
+#define BW_INDEX_MAX_FILE_ENTRIES 50000u /* blob_index.rs:16 */
+#define BW_INDEX_ENTRY_BYTES 44u         /* (BlobHash, PackfileId) */
+enum { BW_BLOB_FILE_CHUNK = 0, BW_BLOB_TREE = 1 }; /* BlobKind, filesystem/mod.rs:13-17 */
+
+/* payload_len[i] is the raw blob length: each blob is framed on the GPU as the magicless zstd
+ * frame of raw blocks that zstd level 3 emits for incompressible input (2-byte frame header,
+ * 3-byte header per 128 KiB block).  Without this flag payloads are caller-made zstd frames. */
+#define BW_PACK_ZSTD_STORE 1u
+
+typedef struct bw_packfile {
+    uint64_t first_blob; /* queue position of its first blob                         */
+    uint64_t n_blobs;
+    uint64_t offset;     /* start of the packfile in the output buffer               */
+    uint64_t size;       /* 8 + header_len + blob section                            */
+    uint64_t header_len; /* encrypted header bytes (the u64 LE prefix)                */
+} bw_packfile;
+
+/* Size of the zstd store frame of a len-byte blob. */
+uint64_t bw_zstd_store_size(uint64_t len);
+/* Grouping and sizes (host only).  out may be NULL with cap 0 to query *n_out; BW_ENOSPC when
+ * cap is too small; *total_bytes = the output buffer size. */
+int bw_pack_plan(const uint64_t* payload_len, uint64_t n, uint32_t flags, bw_packfile* out, uint64_t cap,
+                 uint64_t* n_out, uint64_t* total_bytes);
+/* Build the planned packfiles.  Blob i: payload d_src + src_off[i] (src_len[i] bytes), hashes
+ * 32 B, kinds 1 B (BW_BLOB_*), nonces 12 B; packfile_ids 12 B per packfile (host arrays).
+ * d_out (device, plan's total_bytes) receives the packfiles.  Asynchronous on the context
+ * stream; BW_EINVAL when the plan does not match the blobs or a packfile exceeds
+ * BW_PACKFILE_MAX_SIZE (the reference's assert, pack.rs:152-156). */
+int bw_pack_build_device(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* d_src, const uint64_t* src_off,
+                         const uint64_t* src_len, uint64_t n, const uint8_t* hashes, const uint8_t* kinds,
+                         const uint8_t* nonces, uint32_t flags, const bw_packfile* plan, uint64_t n_packfiles,
+                         const uint8_t* packfile_ids, uint8_t* d_out);
+/* Same over host buffers (synchronous). */
+int bw_pack_build(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,
+                  const uint64_t* src_len, uint64_t n, const uint8_t* hashes, const uint8_t* kinds,
+                  const uint8_t* nonces, uint32_t flags, const bw_packfile* plan, uint64_t n_packfiles,
+                  const uint8_t* packfile_ids, uint8_t* out);
+
+/* Index files: BlobIndex::push/flush (blob_index.rs:151-164, 202-226).  file =
+ * AES-GCM(key "index", nonce = u32 LE file number || 0^8)(bincode varint Vec<(BlobHash,
+ * PackfileId)>). */
+typedef struct bw_index_file {
+    uint32_t file_num; /* the file name, "{file_num:0>10}"               */
+    uint32_t pad;
+    uint64_t offset;   /* start of the file in the buffer                  */
+    uint64_t size;     /* bytes (plaintext + 16)                           */
+    uint64_t n_entries;
+} bw_index_file;
+/* entries (host, n x 44 B) pushed in order from last_file_num: one file per
+ * BW_INDEX_MAX_FILE_ENTRIES entries plus the final unconditional flush (Manager::flush,
+ * pack.rs:84-90), so n = 0 still writes one empty file.  out (host) receives the files back to
+ * back; files[] their table.  out = NULL or a small cap: BW_ENOSPC with *n_files and
+ * *total_bytes set.  Sealed on the GPU; synchronous. */
+int bw_index_files_build(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* entries, uint64_t n,
+                         uint32_t last_file_num, uint8_t* out, uint64_t cap, bw_index_file* files, uint64_t files_cap,
+                         uint64_t* n_files, uint64_t* total_bytes);
+/* BlobIndex::load (blob_index.rs:167-200) fused with the device seed: n_files index files (host
+ * buffer `data`, table files[] with file_num/offset/size) are decrypted and parsed on the GPU
+ * and every digest is seeded into the context's index (as bw_index_seed).  entries (optional,
+ * host, cap x 44 B) receives the records in file order (the reference sorts its `items` by hash
+ * afterwards).  A file whose tag fails -> BW_ECRYPTO, one that is not exactly one varint Vec ->
+ * BW_EFORMAT; *bad_file = its position and nothing is seeded.  Synchronous. */
+int bw_index_load_files(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* data, const bw_index_file* files,
+                        uint64_t n_files, uint8_t* entries, uint64_t cap, uint64_t* n_entries, uint64_t* bad_file);
 
 /* ---- stage timing (HIP events on the context stream, accumulated over profiled batches) ---- */
 enum {

@@ -1,0 +1,336 @@
+"""Packfiles and index files: Manager::write_packfiles / serialize_packfile
+(pack.rs:115-227), the reader Manager::get_blob (unpack.rs:22-78), BlobIndex::push / flush / load
+(blob_index.rs:151-240), and the zstd store frames that stand in for level-3 zstd on
+incompressible blobs (pack.rs:58-64).
+
+CPU tests pin the format oracle (oracle/pack_oracle.py) to hand-derived bincode literals, the
+reference's own size test (pack.rs:239-265 `validate_size_constraints`) and the system libzstd
+(tests/zstd_ref.py), and check the C ABI's host-only planner against the oracle's grouping.  GPU
+tests compare the packfiles and index files built through the C ABI with the oracle byte for
+byte, read every blob back through the oracle's get_blob + libzstd, and seed the device index
+from index files.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from backuwup_amd.synth import splitmix_bytes as _smb
+
+
+def splitmix_bytes(seed, n):
+    return _smb(seed, n).tobytes()
+
+PRK = bytes.fromhex("5c" * 32)
+
+
+@pytest.fixture(scope="module")
+def po(oracle):
+    from oracle import pack_oracle
+    return pack_oracle
+
+
+def _zstd():
+    import zstd_ref
+    if not zstd_ref.available():
+        pytest.skip("libzstd not available")
+    return zstd_ref
+
+
+# ------------------------------------------------------------------ CPU: bincode + formats
+
+def test_varint_literals(po):
+    assert po.varint(0) == b"\x00" and po.varint(250) == b"\xfa"
+    assert po.varint(251) == b"\xfb\xfb\x00" and po.varint(65535) == b"\xfb\xff\xff"
+    assert po.varint(65536) == b"\xfc\x00\x00\x01\x00"
+    assert po.varint(1 << 32) == b"\xfd" + struct.pack("<Q", 1 << 32)
+    for v in (0, 250, 251, 65535, 65536, (1 << 32) - 1, 1 << 32, (1 << 64) - 1):
+        assert po.read_varint(po.varint(v), 0) == (v, len(po.varint(v)))
+    with pytest.raises(po.FormatError):
+        po.read_varint(b"\xfe", 0)
+
+
+def test_header_entry_matches_reference_size_test(po):
+    """pack.rs:239-265: the entry {hash [0;32], FileChunk, Zstd, offset 0, length 0} and the
+    packfile size bound it asserts."""
+    e = po.header_entry(bytes(32), po.KIND_FILE_CHUNK, po.COMPRESSION_ZSTD, 0, 0)
+    assert e == bytes(32) + b"\x00\x01\x00\x00" and len(e) == 36
+    assert (po.PACKFILE_TARGET_SIZE + po.BLOB_MAX_UNCOMPRESSED_SIZE + len(e) * po.PACKFILE_MAX_BLOBS
+            + po.BLOB_NONCE_SIZE <= po.PACKFILE_MAX_SIZE)
+    # field order hash, kind, compression, length, offset (filesystem/mod.rs:36-43)
+    e = po.header_entry(b"\x11" * 32, po.KIND_TREE, po.COMPRESSION_ZSTD, 300, 7)
+    assert e == b"\x11" * 32 + b"\x01\x01\xfb\x2c\x01\x07"
+    hdr = po.serialize_header([(b"\x11" * 32, 1, 1, 300, 7)])
+    assert hdr[0] == 1 and po.deserialize_header(hdr) == [(b"\x11" * 32, 1, 1, 300, 7)]
+    with pytest.raises(po.FormatError):
+        po.deserialize_header(hdr + b"\x00")  # DefaultOptions reject trailing bytes
+    with pytest.raises(po.FormatError):
+        po.deserialize_header(hdr[:-1])
+
+
+def test_index_plaintext_literals(po):
+    h, p = b"\xaa" * 32, b"\xbb" * 12
+    assert po.index_plaintext([]) == b"\x00"
+    assert po.index_plaintext([(h, p)]) == b"\x01" + h + p
+    assert po.index_plaintext([(h, p)] * 251)[:3] == b"\xfb\xfb\x00"
+    assert po.counter_to_nonce(0x01020304) == b"\x04\x03\x02\x01" + bytes(8)
+    with pytest.raises(po.FormatError):
+        po.parse_index_plaintext(po.index_plaintext([(h, p)]) + b"\x00")
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 100, 1023, 1025, 65536, 131071, 131072, 131073, 262145,
+                               1048576, 1048577, 3145728])
+def test_zstd_store_frame_is_level3_output_for_incompressible_data(po, n):
+    z = _zstd()
+    data = splitmix_bytes(0x5eed + n, n)
+    frame = po.zstd_store(data)
+    assert len(frame) == po.zstd_store_size(n)
+    assert frame == z.compress(data)       # what the reference's Compressor emits (pack.rs:58-64)
+    assert z.decompress(frame) == data     # what its Decompressor reads back (unpack.rs:66-68)
+
+
+def test_zstd_store_frame_is_valid_for_compressible_data(po):
+    z = _zstd()
+    data = bytes(200000) + b"abc" * 1000
+    frame = po.zstd_store(data)
+    assert z.decompress(frame) == data and len(z.compress(data)) < len(frame)
+
+
+def test_plan_matches_oracle_grouping(po):
+    from backuwup_amd import _lib
+    from backuwup_amd.context import Context
+    ctx = object.__new__(Context)
+    ctx._L = _lib.load()
+    rng = np.random.default_rng(11)
+    cases = [
+        [],
+        [0],
+        [3 * 1024 * 1024],
+        [po.PACKFILE_TARGET_SIZE - 12 - 16 - 5],  # frame + tag + nonce lands exactly on the target
+        list(rng.integers(0, 3 << 20, 40)),
+        list(rng.integers(0, 70000, 300)),
+    ]
+    for lens in cases:
+        plan, total = ctx.pack_plan(np.asarray(lens, dtype=np.uint64))
+        sealed = [po.zstd_store_size(int(x)) + 16 for x in lens]
+        groups = po.plan_packfiles(sealed)
+        assert [(int(p["first_blob"]), int(p["n_blobs"])) for p in plan] == groups
+        off = 0
+        for p, (f, c) in zip(plan, groups):
+            hdr = len(po.varint(c)) + sum(36 - 2 + len(po.varint(sealed[i])) +
+                                          len(po.varint(sum(sealed[j] + 12 for j in range(f, i))))
+                                          for i in range(f, f + c)) if c < 1000 else None
+            if hdr is not None:
+                assert int(p["header_len"]) == hdr + 16
+            assert int(p["offset"]) == off
+            off += int(p["size"])
+        assert total == off
+    # store frames are >= 5 bytes, so 3 MiB is always reached before PACKFILE_MAX_BLOBS (33 B per blob);
+    # the count limit needs caller payloads under 4 bytes
+    assert ctx.pack_plan([0] * (po.PACKFILE_MAX_BLOBS + 3))[0]["n_blobs"].tolist() == [95326, 4677]
+    lens = [0, 1, 2, 3] * 25001
+    plan, total = ctx.pack_plan(lens, flags=0)
+    assert plan["n_blobs"].tolist() == [po.PACKFILE_MAX_BLOBS, 4]
+    assert [(int(p["first_blob"]), int(p["n_blobs"])) for p in plan] == po.plan_packfiles([x + 16 for x in lens])
+
+
+def test_oracle_packfile_round_trip(po):
+    z = _zstd()
+    rng = np.random.default_rng(3)
+    blobs, raw = [], {}
+    for i, n in enumerate([0, 1, 4096, 131072, 131073, 1 << 20, 3 << 20]):
+        data = splitmix_bytes(100 + i, n)
+        h = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        nonce = bytes(rng.integers(0, 256, 12, dtype=np.uint8))
+        raw[h] = data
+        blobs.append((h, i & 1, nonce, po.seal_blob_payload(PRK, h, nonce, po.zstd_store(data))))
+    ids = [bytes(rng.integers(0, 256, 12, dtype=np.uint8)) for _ in blobs]
+    packs = po.write_packfiles(PRK, blobs, ids)
+    assert len(packs) == len(po.plan_packfiles([len(b[3]) for b in blobs]))
+    found = 0
+    for pid, buf in packs:
+        hl = struct.unpack_from("<Q", buf)[0]
+        hdr = po.deserialize_header(po.oracle.open_blob(PRK, b"header", pid, buf[8:8 + hl]))
+        for h, kind, comp, length, offset in hdr:
+            k, payload = po.get_blob(PRK, pid, buf, h)
+            assert z.decompress(payload) == raw[h] and comp == po.COMPRESSION_ZSTD
+            found += 1
+    assert found == len(blobs)
+    # a flipped ciphertext byte of the packfile's last blob fails its tag
+    pid, buf = packs[0]
+    hl = struct.unpack_from("<Q", buf)[0]
+    last = po.deserialize_header(po.oracle.open_blob(PRK, b"header", pid, buf[8:8 + hl]))[-1][0]
+    bad = bytearray(buf)
+    bad[-1] ^= 1
+    with pytest.raises(po.CryptoError):
+        po.get_blob(PRK, pid, bytes(bad), last)
+    with pytest.raises(po.FormatError):
+        po.get_blob(PRK, pid, buf, b"\x00" * 32)  # IndexHeaderMismatch
+
+
+def test_oracle_index_round_trip(po):
+    rng = np.random.default_rng(4)
+    ents = [(bytes(rng.integers(0, 256, 32, dtype=np.uint8)), bytes(rng.integers(0, 256, 12, dtype=np.uint8)))
+            for _ in range(120)]
+    files = po.push_and_flush(PRK, 7, ents)
+    assert [n for n, _ in files] == [8] and len(files[0][1]) == 1 + 44 * 120 + 16
+    assert po.load_index(PRK, files) == sorted(ents)
+    empty = po.push_and_flush(PRK, 0, [])
+    assert empty[0][0] == 1 and len(empty[0][1]) == 17 and po.load_index(PRK, empty) == []
+    with pytest.raises(po.CryptoError):
+        po.load_index(PRK, [(9, files[0][1])])  # wrong file number = wrong nonce
+
+
+# ------------------------------------------------------------------ GPU
+
+def _blob_set(n_sizes, seed):
+    rng = np.random.default_rng(seed)
+    datas = [splitmix_bytes(seed * 1000 + i, int(n)) for i, n in enumerate(n_sizes)]
+    hashes = rng.integers(0, 256, (len(datas), 32), dtype=np.uint8)
+    kinds = rng.integers(0, 2, len(datas)).astype(np.uint8)
+    nonces = rng.integers(0, 256, (len(datas), 12), dtype=np.uint8)
+    return datas, hashes, kinds, nonces
+
+
+def _concat(datas, align=1):
+    offs, cur = [], 0
+    for d in datas:
+        offs.append(cur)
+        cur += len(d) + (-(len(d)) % align)
+    buf = np.zeros(max(cur, 1), dtype=np.uint8)
+    for o, d in zip(offs, datas):
+        buf[o:o + len(d)] = np.frombuffer(d, dtype=np.uint8)
+    return buf, np.asarray(offs, dtype=np.uint64), np.asarray([len(d) for d in datas], dtype=np.uint64)
+
+
+def _oracle_packs(po, datas, hashes, kinds, nonces, ids, store=True):
+    blobs = [(bytes(hashes[i]), int(kinds[i]), bytes(nonces[i]),
+              po.seal_blob_payload(PRK, hashes[i], nonces[i], po.zstd_store(d) if store else d))
+             for i, d in enumerate(datas)]
+    return po.write_packfiles(PRK, blobs, [bytes(x) for x in ids])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,sizes", [
+    (1, [0, 1, 15, 16, 17, 131071, 131072, 131073, 262147, 1 << 20, 3 << 20, 5, 3 << 20, 77]),
+    (2, list(np.random.default_rng(9).integers(0, 3 << 20, 24))),
+])
+def test_pack_build_matches_oracle(ctx, po, seed, sizes):
+    z = _zstd()
+    datas, hashes, kinds, nonces = _blob_set(sizes, seed)
+    src, offs, lens = _concat(datas, align=1 + seed)  # ragged source offsets
+    plan, total = ctx.pack_plan(lens)
+    ids = np.random.default_rng(seed + 50).integers(0, 256, (len(plan), 12), dtype=np.uint8)
+    got = ctx.pack_build(PRK, src, offs, lens, hashes, kinds, nonces, plan, total, ids)
+    want = _oracle_packs(po, datas, hashes, kinds, nonces, ids)
+    assert len(want) == len(plan)
+    for p, (pid, buf) in zip(plan, want):
+        assert got[int(p["offset"]):int(p["offset"] + p["size"])].tobytes() == buf
+    # and every blob reads back through the reference's reader path + zstd
+    for i, d in enumerate(datas):
+        p = plan[np.searchsorted(plan["first_blob"], i, side="right") - 1]
+        buf = got[int(p["offset"]):int(p["offset"] + p["size"])].tobytes()
+        pid = bytes(ids[list(plan["first_blob"]).index(p["first_blob"])])
+        kind, payload = po.get_blob(PRK, pid, buf, bytes(hashes[i]))
+        assert kind == kinds[i] and z.decompress(payload) == d
+
+
+@pytest.mark.gpu
+def test_pack_build_device_precompressed(ctx, po):
+    """Caller-made zstd frames (libzstd level 3 on compressible data), device buffers."""
+    import torch
+    z = _zstd()
+    raw = [bytes(5000) + splitmix_bytes(i, 3000) * 3 for i in range(9)] + [b"x" * 100000]
+    datas = [z.compress(d) for d in raw]
+    _, hashes, kinds, nonces = _blob_set([len(d) for d in datas], 7)
+    src, offs, lens = _concat(datas)
+    plan, total = ctx.pack_plan(lens, flags=0)
+    ids = np.random.default_rng(8).integers(0, 256, (len(plan), 12), dtype=np.uint8)
+    d_src = torch.from_numpy(src).cuda()
+    d_out = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    ctx.pack_build_device(PRK, d_src.data_ptr(), offs, lens, hashes, kinds, nonces, plan, ids, d_out.data_ptr(),
+                          flags=0)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().tobytes()
+    want = b"".join(b for _, b in _oracle_packs(po, datas, hashes, kinds, nonces, ids, store=False))
+    assert got == want
+    for i, d in enumerate(raw):
+        pid, buf = [(bytes(ids[k]), got[int(p["offset"]):int(p["offset"] + p["size"])]) for k, p in enumerate(plan)
+                    if p["first_blob"] <= i < p["first_blob"] + p["n_blobs"]][0]
+        assert z.decompress(po.get_blob(PRK, pid, buf, bytes(hashes[i]))[1]) == d
+
+
+@pytest.mark.gpu
+def test_pack_build_blob_count_limit(ctx, po):
+    """100 003 tiny caller payloads: the first packfile closes at PACKFILE_MAX_BLOBS (a 5-byte Vec
+    length).  Store frames never get there (>= 33 bytes per blob reach 3 MiB first)."""
+    n = po.PACKFILE_MAX_BLOBS + 3
+    rng = np.random.default_rng(12)
+    lens = rng.integers(0, 4, n).astype(np.uint64)
+    src = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    hashes = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    kinds = np.zeros(n, dtype=np.uint8)
+    nonces = rng.integers(0, 256, (n, 12), dtype=np.uint8)
+    plan, total = ctx.pack_plan(lens, flags=0)
+    assert plan["n_blobs"].tolist() == [po.PACKFILE_MAX_BLOBS, 3]
+    ids = rng.integers(0, 256, (2, 12), dtype=np.uint8)
+    got = ctx.pack_build(PRK, src, offs, lens, hashes, kinds, nonces, plan, total, ids, flags=0)
+    # the second packfile in full, and the first one's header, against the oracle
+    datas = [src[int(o):int(o + l)].tobytes() for o, l in zip(offs, lens)]
+    tail = _oracle_packs(po, datas[-3:], hashes[-3:], kinds[-3:], nonces[-3:], ids[1:], store=False)
+    assert got[int(plan[1]["offset"]):].tobytes() == tail[0][1]
+    hl = int(plan[0]["header_len"])
+    hdr = po.oracle.open_blob(PRK, b"header", bytes(ids[0]), got[8:8 + hl].tobytes())
+    assert hdr[:5] == b"\xfc\xa0\x86\x01\x00"
+    ents = po.deserialize_header(hdr)
+    assert len(ents) == po.PACKFILE_MAX_BLOBS
+    off = 0
+    for i in (0, 1, 99999):
+        h, kind, comp, length, offset = ents[i]
+        assert h == bytes(hashes[i]) and length == int(lens[i]) + 16
+    for i in range(len(ents)):
+        assert ents[i][4] == off
+        off += ents[i][3] + 12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 50000, 50001])
+def test_index_files_build_and_load(ctx, po, n):
+    rng = np.random.default_rng(n + 1)
+    ents = rng.integers(0, 256, (n, 44), dtype=np.uint8)
+    files = ctx.index_files_build(PRK, ents, last_file_num=41)
+    want = po.push_and_flush(PRK, 41, [(bytes(e[:32]), bytes(e[32:])) for e in ents])
+    assert [f for f, _ in files] == [f for f, _ in want] == list(range(42, 42 + n // 50000 + 1))
+    assert [b for _, b in files] == [b for _, b in want]
+    ctx.index_reset()
+    got = ctx.index_load_files(PRK, files)
+    assert got.tobytes() == ents.tobytes()
+    # the loaded digests now gate the next backup: all of them are duplicates, new ones are not
+    if n:
+        probe = np.concatenate([ents[:1000, :32], rng.integers(0, 256, (10, 32), dtype=np.uint8)])
+        assert ctx.index_check_insert(probe).tolist() == [1] * min(n, 1000) + [0] * 10
+
+
+@pytest.mark.gpu
+def test_index_load_errors(ctx, po):
+    from backuwup_amd._lib import BW_ECRYPTO, BW_EFORMAT, BwError
+    ents = [(bytes([i]) * 32, bytes([i]) * 12) for i in range(5)]
+    good = po.push_and_flush(PRK, 0, ents)
+    bad = bytearray(good[0][1])
+    bad[3] ^= 0x40
+    for files, rc in [([good[0], (2, bytes(bad))], BW_ECRYPTO),
+                      ([(5, good[0][1])], BW_ECRYPTO),  # the nonce is the file number
+                      ([(1, b"\x00" * 10)], BW_ECRYPTO),  # shorter than the tag
+                      ([(3, po.oracle.seal_blob(PRK, b"index", po.counter_to_nonce(3),
+                                                po.index_plaintext(ents) + b"\x00"))], BW_EFORMAT),
+                      ([(3, po.oracle.seal_blob(PRK, b"index", po.counter_to_nonce(3), b"\x02" + bytes(44)))],
+                       BW_EFORMAT),
+                      ([(3, po.oracle.seal_blob(PRK, b"index", po.counter_to_nonce(3), b"\xff"))], BW_EFORMAT)]:
+        ctx.index_reset()
+        with pytest.raises(BwError) as e:
+            ctx.index_load_files(PRK, files)
+        assert e.value.rc == rc
+        assert ctx.index_size() == 0  # nothing seeded
+    assert ctx.index_load_files(PRK, good).shape == (5, 44)
