@@ -130,6 +130,13 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libbackuwup_amd.so not built (run __graft_entry__.build() or "
                            "python backuwup_amd/build.py); there is no CPU fallback")
+    # torch ships its own libamdhip64; load it first so the process holds one HIP runtime (our
+    # library binds to the already-loaded soname).  Loaded the other way round, both runtimes end
+    # up mapped and bw_create fails with a HIP error on the GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)

@@ -84,6 +84,9 @@ def main():
                     help="also time the file-tree blobs of the last batch (bw_tree_blobs, §8f row 1)")
     ap.add_argument("--seal", action="store_true",
                     help="also time sealing the last batch's unique blobs (HKDF + AES-256-GCM, §8f row 3)")
+    ap.add_argument("--pack", action="store_true",
+                    help="also time packing the last batch's unique blobs into packfiles: zstd store frames, "
+                         "per-blob + header AES-256-GCM, packfile layout (§8f rows 2-4)")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
@@ -243,6 +246,7 @@ def main():
 
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None
     seal = time_seal(ctx, data, res, file_off, args.steps) if args.seal else None
+    pack = time_pack(ctx, data, res, file_off, args.steps) if args.pack else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
@@ -271,6 +275,8 @@ def main():
             line["file_trees"] = trees
         if seal:
             line["seal"] = seal
+        if pack:
+            line["pack"] = pack
         print(json.dumps(line), flush=True)
     if multi:
         dist.destroy_process_group()
@@ -350,6 +356,49 @@ def time_seal(ctx, data, res, file_off, reps):
     return {"blobs": int(len(u)), "payload_bytes": payload, "ms": round(ms, 3),
             "GBps": round(payload / (ms * 1e-3) / 1e9, 1),
             "hbm_algorithmic_bytes": payload + total, "bit_exact_sample": bool(ok)}
+
+
+def time_pack(ctx, data, res, file_off, reps):
+    """write_packfiles over every unique blob of the last batch, from HBM to HBM (pack.rs:58-80,
+    115-227): zstd store frames (synthetic data is incompressible, so these are the bytes level-3
+    zstd emits), derive_backup_key + AES-256-GCM per blob and per header, the packfile layout.
+    Timed over `reps` calls; one packfile is checked byte for byte against the format oracle and
+    one blob read back through the oracle's get_blob + zstd store parse."""
+    import numpy as np
+    import torch
+    from oracle import pack_oracle as po
+    u = res[res["is_dup"] == 0]
+    fo = np.asarray(file_off, dtype=np.uint64)
+    src_off = fo[u["file"].astype(np.int64)] + u["offset"]
+    lens = u["length"].astype(np.uint64)
+    rng = np.random.default_rng(4)
+    nonces = rng.integers(0, 256, (len(u), 12), dtype=np.uint8)
+    kinds = np.zeros(len(u), dtype=np.uint8)
+    plan, total = ctx.pack_plan(lens)
+    ids = rng.integers(0, 256, (len(plan), 12), dtype=np.uint8)
+    out = torch.empty(total, dtype=torch.uint8, device=data.device)
+    prk = bytes(range(32))
+    args = (prk, data.data_ptr(), src_off, lens, u["digest"], kinds, nonces, plan, ids, out.data_ptr())
+    ctx.pack_build_device(*args)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(max(1, reps)):
+        ctx.pack_build_device(*args)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / max(1, reps)
+    k = int(rng.integers(0, len(plan)))
+    p = plan[k]
+    blobs = []
+    for i in range(int(p["first_blob"]), int(p["first_blob"] + p["n_blobs"])):
+        pt = data[int(src_off[i]):int(src_off[i] + lens[i])].cpu().numpy().tobytes()
+        blobs.append((bytes(u["digest"][i]), 0, bytes(nonces[i]),
+                      po.seal_blob_payload(prk, u["digest"][i], nonces[i], po.zstd_store(pt))))
+    got = out[int(p["offset"]):int(p["offset"] + p["size"])].cpu().numpy().tobytes()
+    ok = got == po.serialize_packfile(prk, bytes(ids[k]), blobs)
+    payload = int(np.sum(lens))
+    return {"blobs": int(len(u)), "packfiles": int(len(plan)), "payload_bytes": payload,
+            "packfile_bytes": int(total), "ms": round(ms, 3), "GBps": round(payload / (ms * 1e-3) / 1e9, 1),
+            "bit_exact_packfile_sample": bool(ok)}
 
 
 def pmc_traffic(args, kernel):
