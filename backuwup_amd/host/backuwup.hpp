@@ -11,8 +11,11 @@
 //   packfile::Manager::add_blob gate   packfile/pack.rs:31-39
 //   dir_packer::process_file           dir_packer.rs:231-282 (batched over many files)
 //   Tree / split_serialize_tree / add_tree_to_blobs   filesystem/mod.rs:63-77, dir_packer.rs:314-390
+//   Manager::write_packfiles / serialize_packfile      packfile/pack.rs:115-227
+//   BlobIndex::flush / load (index files)              packfile/blob_index.rs:151-240
 #pragma once
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <optional>
@@ -224,6 +227,111 @@ inline std::vector<BlobHash> add_trees_to_blobs(Context& ctx, const std::vector<
           ctx.get());
     if (pieces) *pieces = std::move(out);
     return hashes;
+}
+
+// ------------------------------------------------------------------ packfiles (pack.rs:115-227)
+using PackfileId = std::array<uint8_t, 12>;  // shared/src/types.rs
+using BlobNonce = std::array<uint8_t, 12>;
+enum class BlobKind : uint8_t { FileChunk = BW_BLOB_FILE_CHUNK, Tree = BW_BLOB_TREE };  // filesystem/mod.rs:13-17
+
+struct Blob {  // filesystem/mod.rs:46-51 (data = the raw bytes; framed as zstd store on the GPU)
+    BlobHash hash;
+    BlobKind kind;
+    std::vector<uint8_t> data;
+};
+
+// Manager::write_packfiles over a queue of unique blobs: nonces[i] and the packfile ids are the
+// caller's random draws (the reference's getrandom, pack.rs:74-76, :207-208); ids must hold at
+// least as many entries as packfiles result (packfile_count()).  Returns (id, bytes) per packfile.
+inline size_t packfile_count(const std::vector<Blob>& blobs) {
+    std::vector<uint64_t> lens;
+    for (const Blob& b : blobs) lens.push_back(b.data.size());
+    uint64_t n = 0, total = 0;
+    const int rc = bw_pack_plan(lens.data(), lens.size(), BW_PACK_ZSTD_STORE, nullptr, 0, &n, &total);
+    if (rc != BW_ENOSPC && rc != BW_OK) check(rc);
+    return n;
+}
+
+inline std::vector<std::pair<PackfileId, std::vector<uint8_t>>> write_packfiles(
+    Context& ctx, const std::array<uint8_t, 32>& prk, const std::vector<Blob>& blobs,
+    const std::vector<BlobNonce>& nonces, const std::vector<PackfileId>& ids) {
+    std::vector<uint64_t> lens, offs;
+    std::vector<uint8_t> data, hashes, kinds, nb;
+    for (size_t i = 0; i < blobs.size(); i++) {
+        offs.push_back(data.size());
+        lens.push_back(blobs[i].data.size());
+        data.insert(data.end(), blobs[i].data.begin(), blobs[i].data.end());
+        hashes.insert(hashes.end(), blobs[i].hash.begin(), blobs[i].hash.end());
+        kinds.push_back((uint8_t)blobs[i].kind);
+        nb.insert(nb.end(), nonces.at(i).begin(), nonces.at(i).end());
+    }
+    uint64_t np = 0, total = 0;
+    std::vector<bw_packfile> plan(packfile_count(blobs));
+    check(bw_pack_plan(lens.data(), lens.size(), BW_PACK_ZSTD_STORE, plan.data(), plan.size(), &np, &total));
+    if (ids.size() < np) throw Error(BW_EINVAL, "not enough packfile ids");
+    std::vector<uint8_t> idb, out(total);
+    for (size_t k = 0; k < np; k++) idb.insert(idb.end(), ids[k].begin(), ids[k].end());
+    check(bw_pack_build(ctx.get(), prk.data(), data.data(), offs.data(), lens.data(), lens.size(), hashes.data(),
+                        kinds.data(), nb.data(), BW_PACK_ZSTD_STORE, plan.data(), np, idb.data(), out.data()),
+          ctx.get());
+    std::vector<std::pair<PackfileId, std::vector<uint8_t>>> res;
+    for (size_t k = 0; k < np; k++)
+        res.emplace_back(ids[k], std::vector<uint8_t>(out.begin() + plan[k].offset,
+                                                      out.begin() + plan[k].offset + plan[k].size));
+    return res;
+}
+
+// ------------------------------------------------------------------ index files (blob_index.rs)
+using IndexEntry = std::pair<BlobHash, PackfileId>;
+
+// BlobIndex::push for every entry, then the final unconditional flush: (file_num, bytes) per file
+inline std::vector<std::pair<uint32_t, std::vector<uint8_t>>> index_flush(Context& ctx,
+                                                                         const std::array<uint8_t, 32>& prk,
+                                                                         const std::vector<IndexEntry>& entries,
+                                                                         uint32_t last_file_num) {
+    std::vector<uint8_t> e;
+    for (const auto& x : entries) {
+        e.insert(e.end(), x.first.begin(), x.first.end());
+        e.insert(e.end(), x.second.begin(), x.second.end());
+    }
+    uint64_t nf = 0, total = 0;
+    int rc = bw_index_files_build(ctx.get(), prk.data(), e.data(), entries.size(), last_file_num, nullptr, 0, nullptr,
+                                  0, &nf, &total);
+    if (rc != BW_ENOSPC) check(rc, ctx.get());
+    std::vector<uint8_t> out(total);
+    std::vector<bw_index_file> files(nf);
+    check(bw_index_files_build(ctx.get(), prk.data(), e.data(), entries.size(), last_file_num, out.data(), total,
+                               files.data(), nf, &nf, &total),
+          ctx.get());
+    std::vector<std::pair<uint32_t, std::vector<uint8_t>>> res;
+    for (const auto& f : files)
+        res.emplace_back(f.file_num, std::vector<uint8_t>(out.begin() + f.offset, out.begin() + f.offset + f.size));
+    return res;
+}
+
+// BlobIndex::load: decrypt + parse the files on the GPU and seed the context's index; returns
+// `items` sorted by hash as the reference keeps them (blob_index.rs:197).
+inline std::vector<IndexEntry> index_load(Context& ctx, const std::array<uint8_t, 32>& prk,
+                                          const std::vector<std::pair<uint32_t, std::vector<uint8_t>>>& files) {
+    std::vector<uint8_t> data;
+    std::vector<bw_index_file> tab;
+    uint64_t cap = 0;
+    for (const auto& f : files) {
+        tab.push_back(bw_index_file{f.first, 0, data.size(), f.second.size(), 0});
+        data.insert(data.end(), f.second.begin(), f.second.end());
+        cap += f.second.size() / BW_INDEX_ENTRY_BYTES + 1;
+    }
+    std::vector<uint8_t> rec(cap * BW_INDEX_ENTRY_BYTES);
+    uint64_t n = 0, bad = 0;
+    check(bw_index_load_files(ctx.get(), prk.data(), data.data(), tab.data(), tab.size(), rec.data(), cap, &n, &bad),
+          ctx.get());
+    std::vector<IndexEntry> items(n);
+    for (uint64_t i = 0; i < n; i++) {
+        std::copy(rec.begin() + i * 44, rec.begin() + i * 44 + 32, items[i].first.begin());
+        std::copy(rec.begin() + i * 44 + 32, rec.begin() + i * 44 + 44, items[i].second.begin());
+    }
+    std::sort(items.begin(), items.end(), [](const IndexEntry& a, const IndexEntry& b) { return a.first < b.first; });
+    return items;
 }
 
 }  // namespace backuwup

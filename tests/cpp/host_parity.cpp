@@ -1,5 +1,6 @@
 // Host-side C++ mirror exercised the way the reference calls it (dir_packer.rs:254-286,
 // pack.rs:31-39).  Prints one line per result; tests/test_cpp_host.py compares with the oracle.
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
@@ -63,5 +64,40 @@ int main() {
     printf("tree-hash ");
     for (auto x : th[0]) printf("%02x", x);
     printf("\n");
+    // two packfiles' worth of blobs (pack.rs:115-227), then their index entries as files
+    std::array<uint8_t, 32> prk;
+    for (int k = 0; k < 32; k++) prk[k] = (uint8_t)(0x40 + k);
+    std::vector<Blob> blobs;
+    std::vector<BlobNonce> nonces;
+    const size_t sizes[4] = {0, 1000, 3 << 20, 70000};
+    for (size_t i = 0; i < 4; i++) {
+        Blob bl;
+        bl.data.assign(data.begin() + 5 * i, data.begin() + 5 * i + sizes[i]);
+        bl.hash = blake3::hash(ctx, bl.data.data(), bl.data.size());
+        bl.kind = i == 3 ? BlobKind::Tree : BlobKind::FileChunk;
+        blobs.push_back(bl);
+        BlobNonce nn;
+        for (int k = 0; k < 12; k++) nn[k] = (uint8_t)(7 * i + k);
+        nonces.push_back(nn);
+    }
+    std::vector<PackfileId> ids(packfile_count(blobs));
+    for (size_t p = 0; p < ids.size(); p++)
+        for (int k = 0; k < 12; k++) ids[p][k] = (uint8_t)(0xa0 + 16 * p + k);
+    auto packs = write_packfiles(ctx, prk, blobs, nonces, ids);
+    std::vector<IndexEntry> entries;
+    for (const auto& pk : packs) {
+        printf("packfile %zu ", pk.second.size());
+        for (auto x : pk.second) printf("%02x", x);
+        printf("\n");
+    }
+    for (size_t i = 0; i < blobs.size(); i++) entries.push_back({blobs[i].hash, ids[i < 3 ? 0 : 1]});
+    auto files = index_flush(ctx, prk, entries, 9);
+    for (const auto& f : files) {
+        printf("index %u ", f.first);
+        for (auto x : f.second) printf("%02x", x);
+        printf("\n");
+    }
+    auto items = index_load(ctx, prk, files);
+    printf("index-load %zu %d\n", items.size(), (int)std::is_sorted(items.begin(), items.end()));
     return 0;
 }

@@ -46,3 +46,22 @@ def test_cpp_mirror_parity(tmp_path, oracle):
     assert tb == oracle.tree_serialize(0, "a5.bin", len(data), 1700000000, None, children)
     th = [l.split()[1] for l in out if l.startswith("tree-hash ")][0]
     assert th == oracle.blake3(tb).hex()
+    # packfiles and index files (pack.rs:115-227, blob_index.rs:151-240) against the format oracle
+    from oracle import pack_oracle as po
+    prk = bytes(range(0x40, 0x60))
+    sizes = [0, 1000, 3 << 20, 70000]
+    blobs = []
+    for i, n in enumerate(sizes):
+        d = data[5 * i:5 * i + n].tobytes()
+        h = oracle.blake3(d)
+        nonce = bytes(7 * i + k for k in range(12))
+        blobs.append((h, 1 if i == 3 else 0, nonce, po.seal_blob_payload(prk, h, nonce, po.zstd_store(d))))
+    groups = po.plan_packfiles([len(b[3]) for b in blobs])
+    ids = [bytes(0xa0 + 16 * p + k for k in range(12)) for p in range(len(groups))]
+    want = po.write_packfiles(prk, blobs, ids)
+    got = [bytes.fromhex(l.split()[2]) for l in out if l.startswith("packfile ")]
+    assert got == [b for _, b in want] and len(got) == 2
+    ents = [(b[0], ids[0 if i < 3 else 1]) for i, b in enumerate(blobs)]
+    files = [(int(l.split()[1]), bytes.fromhex(l.split()[2])) for l in out if l.startswith("index ")]
+    assert files == po.push_and_flush(prk, 9, ents)
+    assert "index-load 4 1" in out
