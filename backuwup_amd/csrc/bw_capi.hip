@@ -53,10 +53,9 @@ struct bw_ctx {
     bool seal_pending = false;
 
     // packfiles / index files (bw_pack.hip): tables, zstd staging, header plaintexts, host I/O
-    DevBuf pk_blobs, pk_files, pk_store, pk_stage, pk_hdr, pk_src, pk_out, ix_io, ix_tab, ix_dig;
+    DevBuf pk_blobs, pk_files, pk_hdr, pk_src, pk_out, ix_io, ix_tab, ix_dig;
     std::vector<PackBlob> h_pk_blobs;
     std::vector<PackFileDesc> h_pk_files;
-    std::vector<StoreItem> h_pk_store;
     hipEvent_t pk_done = nullptr;  // the host tables above reusable once this fired
     bool pk_pending = false;
 
@@ -236,7 +235,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->digests,
                      &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->table,
                      &c->log, &c->dstate, &c->seal_items, &c->seal_keys, &c->seal_parts, &c->seal_ok,
-                     &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_store, &c->pk_stage, &c->pk_hdr,
+                     &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr,
                      &c->pk_src, &c->pk_out, &c->ix_io, &c->ix_tab, &c->ix_dig};
     for (DevBuf* b : all)
         if (b->p) hipFree(b->p);
@@ -758,9 +757,12 @@ extern "C" int bw_profile_read(bw_ctx* c, double* stage_ms, uint64_t* n_batches)
 // compress_encrypt_blob's HKDF key + AES-256-GCM (pack.rs:70-80) and the inverse
 // (unpack.rs:58-63, blob_index.rs:185-191); kernels in bw_seal.hip.
 
+// raw_len (sealing only, may be null): item i's plaintext is the zstd store frame of raw_len[i]
+// source bytes at d_src + src_off[i], built inside k_seal_ctr; src_len[i] is the frame length.
 static int seal_submit(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* d_src, const uint64_t* src_off,
                        const uint64_t* src_len, uint64_t n, const uint8_t* info, uint32_t info_len,
-                       const uint8_t* nonces, uint8_t* d_dst, const uint64_t* dst_off, uint8_t* ok) {
+                       const uint8_t* nonces, uint8_t* d_dst, const uint64_t* dst_off, uint8_t* ok,
+                       const uint64_t* raw_len = nullptr) {
     if (!c || !prk || info_len > BW_SEAL_MAX_INFO) return BW_EINVAL;
     if (n && (!d_src || !src_off || !src_len || !nonces || !d_dst || !dst_off || (info_len && !info))) return BW_EINVAL;
     if (dec && n && !ok) return BW_EINVAL;
@@ -792,6 +794,10 @@ static int seal_submit(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* d
         const uint64_t len = dec ? src_len[i] - 16 : src_len[i];
         seal_fill_item(&it[i], src_off[i], len, dst_off[i], pieces, nonces + 12 * i, info + (uint64_t)info_len * i,
                        info_len);
+        if (raw_len) {
+            it[i].raw_len = (uint32_t)raw_len[i];
+            it[i].wd = zstd_window_descriptor(raw_len[i]);
+        }
         pieces += seal_pieces(len);
     }
     if (int rc = ensure(c, c->seal_items, bytes)) return rc;
@@ -804,7 +810,8 @@ static int seal_submit(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* d
     c->seal_pending = true;
     SealPads pads;
     seal_pads(prk, &pads);
-    launch_seal(c->stream, dec, d_src, d_dst, P<SealItem>(c->seal_items), n, pads, P<SealKey>(c->seal_keys), pieces,
+    launch_seal(c->stream, dec, raw_len != nullptr, d_src, d_dst, P<SealItem>(c->seal_items), n, pads,
+                P<SealKey>(c->seal_keys), pieces,
                 P<uint32_t>(c->seal_parts), dec ? P<uint8_t>(c->seal_ok) : nullptr);
     HIPCHK(c, hipGetLastError());
     if (dec) {
@@ -954,9 +961,8 @@ static int pack_submit(bw_ctx* c, const uint8_t* prk, const uint8_t* d_src, cons
     const bool store = flags & BW_PACK_ZSTD_STORE;
     c->h_pk_blobs.resize(n);
     c->h_pk_files.resize(npf);
-    c->h_pk_store.resize(store ? n : 0);
     std::vector<uint64_t> s_off(n), s_len(n), d_off(n), h_off(npf), h_len(npf), h_dst(npf);
-    uint64_t hdr_total = 0, stage_total = 0, units = 0;
+    uint64_t hdr_total = 0;
     for (uint64_t p = 0; p < npf; p++) {
         const bw_packfile& f = plan[p];
         h_off[p] = hdr_total;
@@ -979,17 +985,8 @@ static int pack_submit(bw_ctx* c, const uint8_t* prk, const uint8_t* d_src, cons
             entry += entry_len(sealed, section);
             section += sealed + BW_BLOB_NONCE_SIZE;
             s_len[i] = frame;
+            s_off[i] = src_off[i];
             d_off[i] = b.nonce_off + BW_BLOB_NONCE_SIZE;
-            if (store) {
-                uint32_t wlog = src_len[i] > 1 ? 64 - __builtin_clzll(src_len[i] - 1) : 0;
-                wlog = std::min(21u, std::max(10u, wlog));
-                c->h_pk_store[i] = StoreItem{src_off[i], src_len[i], stage_total, units, (wlog - 10) << 3, 0};
-                s_off[i] = stage_total;
-                stage_total += (frame + 15) & ~15ull;
-                units += (frame + STORE_UNIT - 1) / STORE_UNIT;
-            } else {
-                s_off[i] = src_off[i];
-            }
         }
         hdr_total = entry;
     }
@@ -1000,23 +997,15 @@ static int pack_submit(bw_ctx* c, const uint8_t* prk, const uint8_t* d_src, cons
                              c->stream));
     HIPCHK(c, hipMemcpyAsync(c->pk_files.p, c->h_pk_files.data(), npf * sizeof(PackFileDesc), hipMemcpyHostToDevice,
                              c->stream));
-    const uint8_t* seal_src = d_src;
-    if (store) {
-        if (int rc = ensure(c, c->pk_store, n * sizeof(StoreItem))) return rc;
-        if (int rc = ensure(c, c->pk_stage, stage_total)) return rc;
-        HIPCHK(c, hipMemcpyAsync(c->pk_store.p, c->h_pk_store.data(), n * sizeof(StoreItem), hipMemcpyHostToDevice,
-                                 c->stream));
-        launch_zstd_store(c->stream, d_src, P<uint8_t>(c->pk_stage), P<StoreItem>(c->pk_store), n, units);
-        seal_src = P<uint8_t>(c->pk_stage);
-    }
     HIPCHK(c, hipEventRecord(c->pk_done, c->stream));
     c->pk_pending = true;
     launch_pack_meta(c->stream, P<PackBlob>(c->pk_blobs), n, P<PackFileDesc>(c->pk_files), npf, P<uint8_t>(c->pk_hdr),
                      d_out);
     HIPCHK(c, hipGetLastError());
-    // every blob: derive_backup_key(hash) + AES-GCM(nonce) into its place behind its nonce
-    if (int rc = seal_submit(c, false, prk, seal_src, s_off.data(), s_len.data(), n, hashes, 32, nonces, d_out,
-                             d_off.data(), nullptr))
+    // every blob: derive_backup_key(hash) + AES-GCM(nonce) of its payload (its store frame, built
+    // while it is encrypted) into its place behind its nonce
+    if (int rc = seal_submit(c, false, prk, d_src, s_off.data(), s_len.data(), n, hashes, 32, nonces, d_out,
+                             d_off.data(), nullptr, store ? src_len : nullptr))
         return rc;
     // every header: derive_backup_key(b"header") + AES-GCM(packfile id) behind the length prefix
     std::vector<uint8_t> info(npf * 6);

@@ -140,6 +140,8 @@ struct SealItem {
     uint32_t nonce[3];                       // big-endian words of the 12-byte nonce
     uint32_t info_len;
     uint8_t info[56];
+    uint32_t raw_len, wd;  // store-framed items: the plaintext is the zstd store frame of raw_len
+                           // source bytes with window descriptor wd (launch_seal(framed = true))
 };
 
 struct SealKey {
@@ -157,18 +159,14 @@ uint64_t seal_pieces(uint64_t len);  // k_seal_ctr wave tasks of an item of len 
 void seal_fill_item(SealItem* it, uint64_t src_off, uint64_t len, uint64_t dst_off, uint64_t piece0,
                     const uint8_t nonce[12], const uint8_t* info, uint32_t info_len);
 // dec = false: dst = ciphertext || tag; dec = true: dst = plaintext, ok[i] = tag verified
-void launch_seal(hipStream_t st, bool dec, const uint8_t* src, uint8_t* dst, const SealItem* items, uint64_t n,
-                 const SealPads& pads, SealKey* keys, uint64_t n_pieces, uint32_t* parts, uint8_t* ok);
+// framed (sealing only): item plaintexts are zstd store frames built on the fly from the source
+void launch_seal(hipStream_t st, bool dec, bool framed, const uint8_t* src, uint8_t* dst, const SealItem* items,
+                 uint64_t n, const SealPads& pads, SealKey* keys, uint64_t n_pieces, uint32_t* parts, uint8_t* ok);
+uint32_t zstd_window_descriptor(uint64_t raw_len);
 
 // ------------------------------------------------------------------ packfiles / index files (bw_pack.hip)
 constexpr uint32_t ZSTD_BLOCK = 131072;           // zstd ZSTD_BLOCKSIZE_MAX
 constexpr uint32_t ZSTD_STRIDE = ZSTD_BLOCK + 3;  // a raw block with its 3-byte header
-constexpr uint32_t STORE_UNIT = 65536;            // framed bytes per k_zstd_store wave
-
-struct StoreItem {
-    uint64_t src_off, len, stage_off, unit0;  // unit0: first 64 KiB wave task of this item
-    uint32_t wd, pad;                         // window descriptor byte
-};
 
 struct PackBlob {
     uint8_t hash[32];
@@ -184,8 +182,6 @@ struct PackFileDesc {
     uint64_t hdr_off, count, out_off, header_len;
 };
 
-void launch_zstd_store(hipStream_t st, const uint8_t* src, uint8_t* stage, const StoreItem* items, uint64_t n_items,
-                       uint64_t n_units);
 void launch_pack_meta(hipStream_t st, const PackBlob* blobs, uint64_t n, const PackFileDesc* files, uint64_t n_files,
                       uint8_t* hdr, uint8_t* out);
 void launch_index_parse(hipStream_t st, const uint8_t* pt, const uint64_t* pt_off, const uint64_t* pt_len,

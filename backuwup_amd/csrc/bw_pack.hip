@@ -4,11 +4,9 @@
 // filesystem/packfile/pack.rs:115-227) and of BlobIndex::flush / load (blob_index.rs:167-226);
 // the AES-256-GCM of every blob, header and index file runs in bw_seal.hip.
 //
-//   k_zstd_store  frames each blob as the magicless zstd frame that level 3 emits for
-//                 incompressible input (pack.rs:58-64 settings): FHD 0x00, window descriptor,
-//                 raw blocks of <= 128 KiB with 3-byte headers.  One wave per 64 KiB of frame;
-//                 each lane writes 16 aligned bytes per step, read from the blob with one
-//                 16-byte load unless the step straddles a block header (1 step in 8192).
+//   (zstd store frames -- the magicless frame level 3 emits for incompressible input,
+//    pack.rs:58-64 settings -- are built on the fly by k_seal_ctr<false, true> in bw_seal.hip,
+//    so a blob is read once and its sealed frame written once.)
 //   k_pack_meta   one lane per queued blob: its PackfileHeaderBlob entry in bincode varint
 //                 form (hash, kind, compression = Zstd, length, offset; filesystem/mod.rs:36-43)
 //                 into the header staging area, and its 12-byte nonce in front of its sealed
@@ -24,63 +22,6 @@
 #include "bw_internal.h"
 
 namespace bw {
-
-// ------------------------------------------------------------------ zstd store frames
-__device__ __forceinline__ uint8_t frame_byte(const uint8_t* __restrict__ src, uint32_t len, uint32_t nb, uint32_t wd,
-                                              uint32_t f) {
-    if (f == 0) return 0;  // Frame_Header_Descriptor: no FCS, no single segment, no checksum, no dict
-    if (f == 1) return (uint8_t)wd;
-    const uint32_t k = (f - 2) / ZSTD_STRIDE, r = (f - 2) - k * ZSTD_STRIDE;
-    if (r < 3) {
-        const uint32_t bl = k == nb - 1 ? len - k * ZSTD_BLOCK : ZSTD_BLOCK;
-        const uint32_t h = (bl << 3) | (k == nb - 1 ? 1u : 0u);  // Raw_Block, Last_Block bit
-        return (uint8_t)(h >> (8 * r));
-    }
-    return src[(uint64_t)k * ZSTD_BLOCK + r - 3];
-}
-
-__global__ __launch_bounds__(256) void k_zstd_store(const uint8_t* __restrict__ src, uint8_t* __restrict__ stage,
-                                                    const StoreItem* __restrict__ items, uint64_t n_items,
-                                                    uint64_t n_units) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t unit = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (unit >= n_units) return;
-    uint64_t lo = 0, hi = n_items;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (items[mid].unit0 <= unit) lo = mid + 1;
-        else hi = mid;
-    }
-    const StoreItem it = items[lo - 1];
-    const uint32_t len = (uint32_t)it.len, nb = len ? (len + ZSTD_BLOCK - 1) / ZSTD_BLOCK : 1;
-    const uint32_t framed = 2 + 3 * nb + len, wd = it.wd;
-    const uint8_t* s = src + it.src_off;
-    uint8_t* d = stage + it.stage_off;
-    const uint32_t u0 = (uint32_t)(unit - it.unit0) * STORE_UNIT;
-    const uint32_t u1 = u0 + STORE_UNIT < framed ? u0 + STORE_UNIT : framed;
-    for (uint32_t f = u0 + 16 * lane; f < u1; f += 16 * 64) {
-        const uint32_t k0 = f >= 2 ? (f - 2) / ZSTD_STRIDE : 0, r0 = f >= 2 ? (f - 2) - k0 * ZSTD_STRIDE : 0;
-        if (f >= 2 && r0 >= 3 && r0 + 16 <= ZSTD_STRIDE && f + 16 <= framed) {
-            // 16 data bytes of one block: one (unaligned) 16-byte load, one aligned store
-            *(uint4*)(d + f) = *(const uint4*)(s + (uint64_t)k0 * ZSTD_BLOCK + r0 - 3);
-        } else {
-            uint32_t w[4] = {0, 0, 0, 0};
-            for (uint32_t b = 0; b < 16 && f + b < framed; b++) w[b >> 2] |= (uint32_t)frame_byte(s, len, nb, wd, f + b) << (8 * (b & 3));
-            if (f + 16 <= framed) {
-                *(uint4*)(d + f) = make_uint4(w[0], w[1], w[2], w[3]);
-            } else {
-                for (uint32_t b = 0; f + b < framed; b++) d[f + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-            }
-        }
-    }
-}
-
-void launch_zstd_store(hipStream_t st, const uint8_t* src, uint8_t* stage, const StoreItem* items, uint64_t n_items,
-                       uint64_t n_units) {
-    if (!n_units) return;
-    hipLaunchKernelGGL(k_zstd_store, dim3((unsigned)((n_units + 3) / 4)), dim3(256), 0, st, src, stage, items, n_items,
-                       n_units);
-}
 
 // ------------------------------------------------------------------ packfile header entries
 __device__ __forceinline__ uint32_t put_varint(uint8_t* p, uint64_t v) {

@@ -305,14 +305,48 @@ __device__ __forceinline__ void aes_ctr2(const SealLds& L, const uint32_t* rk, c
 #undef A0
 }
 
+// Byte f of the zstd store frame of the raw_len bytes at s (FHD 0x00, window descriptor, raw
+// blocks of <= 128 KiB behind 3-byte headers with the last-block bit).
+__device__ __forceinline__ uint32_t frame_byte(const uint8_t* s, uint32_t raw_len, uint32_t wd, uint32_t f) {
+    if (f == 0) return 0;  // Frame_Header_Descriptor: no content size, no checksum, no dictionary
+    if (f == 1) return wd;
+    const uint32_t nb = raw_len ? (raw_len + ZSTD_BLOCK - 1) / ZSTD_BLOCK : 1;
+    const uint32_t k = (f - 2) / ZSTD_STRIDE, r = (f - 2) - k * ZSTD_STRIDE;
+    if (r < 3) {
+        const uint32_t bl = k == nb - 1 ? raw_len - k * ZSTD_BLOCK : ZSTD_BLOCK;
+        return (((bl << 3) | (k == nb - 1 ? 1u : 0u)) >> (8 * r)) & 0xff;  // Raw_Block
+    }
+    return s[(uint64_t)k * ZSTD_BLOCK + r - 3];
+}
+
 // CTR xor of block g of the item (keystream ks) from s to d; returns the GHASH input (the
-// ciphertext, zero-padded past the end of the item).
-template <bool DEC>
-__device__ __forceinline__ G4 crypt_block(const uint8_t* s, uint8_t* d, uint64_t len, uint64_t g, const uint32_t ks[4]) {
+// ciphertext, zero-padded past the end of the item).  FRAMED: the plaintext is the store frame
+// of the raw bytes at s; a block inside one raw block's data is one (unaligned) 16-byte load.
+template <bool DEC, bool FRAMED>
+__device__ __forceinline__ G4 crypt_block(const uint8_t* s, uint8_t* d, uint64_t len, uint64_t g, const uint32_t ks[4],
+                                          uint32_t raw_len, uint32_t wd) {
     const uint64_t at = 16 * g;
     uint32_t in[4];
     const bool full = at + 16 <= len;
-    if (full) {
+    if (FRAMED) {
+        const uint32_t f = (uint32_t)at;
+        const uint32_t k0 = f >= 2 ? (f - 2) / ZSTD_STRIDE : 0, r0 = f >= 2 ? (f - 2) - k0 * ZSTD_STRIDE : 0;
+        if (full && f >= 2 && r0 >= 3 && r0 + 16 <= ZSTD_STRIDE) {
+            const uint4 v = *(const uint4*)(s + (uint64_t)k0 * ZSTD_BLOCK + r0 - 3);
+            in[0] = __builtin_bswap32(v.x); in[1] = __builtin_bswap32(v.y);
+            in[2] = __builtin_bswap32(v.z); in[3] = __builtin_bswap32(v.w);
+        } else {
+            const uint32_t nb = full ? 16 : (uint32_t)(len - at);
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    if ((uint32_t)(4 * w + b) < nb) x |= frame_byte(s, raw_len, wd, f + 4 * w + b) << (24 - 8 * b);
+                in[w] = x;
+            }
+        }
+    } else if (full) {
         const uint4 v = *(const uint4*)(s + at);
         in[0] = __builtin_bswap32(v.x); in[1] = __builtin_bswap32(v.y);
         in[2] = __builtin_bswap32(v.z); in[3] = __builtin_bswap32(v.w);
@@ -392,7 +426,7 @@ __device__ __forceinline__ G4 shfl_down4(G4 v, int d) {
             (uint32_t)__shfl_down((int)v.w2, d, 64), (uint32_t)__shfl_down((int)v.w3, d, 64)};
 }
 
-template <bool DEC>
+template <bool DEC, bool FRAMED>
 __global__ __launch_bounds__(SEAL_THREADS) void k_seal_ctr(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                            const SealItem* __restrict__ items, uint64_t n_items,
                                                            const SealKey* __restrict__ keys, uint64_t n_pieces,
@@ -486,10 +520,10 @@ __global__ __launch_bounds__(SEAL_THREADS) void k_seal_ctr(const uint8_t* __rest
             uint32_t ksa[4], ksb[4];
             aes_ctr2(L, rk, r1, lane_off, (uint32_t)(ga + 2), (uint32_t)(gb + 2), ksa, ksb);  // inc32 of J0 = nonce||1
             if (j) X = gmul_h64(L, X, wid);
-            if (ra >= 0) X = gxor(X, crypt_block<DEC>(s, d, len, ga, ksa));
+            if (ra >= 0) X = gxor(X, crypt_block<DEC, FRAMED>(s, d, len, ga, ksa, it.raw_len, it.wd));
             if (j + 1 < S) {  // wave-uniform
                 X = gmul_h64(L, X, wid);
-                X = gxor(X, crypt_block<DEC>(s, d, len, gb, ksb));
+                X = gxor(X, crypt_block<DEC, FRAMED>(s, d, len, gb, ksb, it.raw_len, it.wd));
             }
         }
         // fold the 64 lane partials: T = sum_l X_l * H^(63 - l)
@@ -579,19 +613,28 @@ void seal_fill_item(SealItem* it, uint64_t src_off, uint64_t len, uint64_t dst_o
     memcpy(it->info, info, info_len);
 }
 
-void launch_seal(hipStream_t st, bool dec, const uint8_t* src, uint8_t* dst, const SealItem* it, uint64_t n,
-                 const SealPads& pads, SealKey* k, uint64_t n_pieces, uint32_t* parts, uint8_t* ok) {
+uint32_t zstd_window_descriptor(uint64_t raw_len) {
+    uint32_t wlog = raw_len > 1 ? 64 - __builtin_clzll(raw_len - 1) : 0;  // ceil(log2(raw_len))
+    wlog = wlog < 10 ? 10 : (wlog > 21 ? 21 : wlog);  // level 3's windowLog, cut to the source size
+    return (wlog - 10) << 3;
+}
+
+void launch_seal(hipStream_t st, bool dec, bool framed, const uint8_t* src, uint8_t* dst, const SealItem* it,
+                 uint64_t n, const SealPads& pads, SealKey* k, uint64_t n_pieces, uint32_t* parts, uint8_t* ok) {
     if (!n) return;
     hipLaunchKernelGGL(k_seal_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, it, n, pads, k);
     if (n_pieces) {
         uint64_t grid = (n_pieces + SEAL_THREADS / 64 - 1) / (SEAL_THREADS / 64);
         if (grid > 1024) grid = 1024;
         if (dec)
-            hipLaunchKernelGGL(k_seal_ctr<true>, dim3((unsigned)grid), dim3(SEAL_THREADS), 0, st, src, dst, it, n, k,
-                               n_pieces, parts);
+            hipLaunchKernelGGL((k_seal_ctr<true, false>), dim3((unsigned)grid), dim3(SEAL_THREADS), 0, st, src, dst, it,
+                               n, k, n_pieces, parts);
+        else if (framed)
+            hipLaunchKernelGGL((k_seal_ctr<false, true>), dim3((unsigned)grid), dim3(SEAL_THREADS), 0, st, src, dst, it,
+                               n, k, n_pieces, parts);
         else
-            hipLaunchKernelGGL(k_seal_ctr<false>, dim3((unsigned)grid), dim3(SEAL_THREADS), 0, st, src, dst, it, n, k,
-                               n_pieces, parts);
+            hipLaunchKernelGGL((k_seal_ctr<false, false>), dim3((unsigned)grid), dim3(SEAL_THREADS), 0, st, src, dst,
+                               it, n, k, n_pieces, parts);
     }
     if (dec)
         hipLaunchKernelGGL(k_seal_tag<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, dst, it, n, k,
