@@ -67,7 +67,7 @@ def make_workload(name, gib, rank, dev, n_files):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--gib", type=float, default=None,
@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=2,
                     help="batches in flight: consecutive steps alternate between this many contexts/streams")
     ap.add_argument("--host-stream", action="store_true",
                     help="batches start in pinned host memory (H2D copies overlapped with processing)")
@@ -223,6 +223,18 @@ def main():
         el = float(t.item())
     stage_ms, nbatch = ctx.profile_read()
     per = {s: stage_ms[s] / max(nbatch, 1) for s in STAGES}
+    iso = None
+    if len(ctxs) > 1 and not multi and host is None:
+        # the same batch with nothing beside it (one context, synchronized): each kernel's own
+        # duration, reported next to the live one, which shares the GPU with the other batch
+        ctx.profile_enable(True)
+        for _ in range(3):
+            with torch.cuda.stream(streams[0]):
+                ctx.index_reset(index_hint)
+                ctx.submit_device(data.data_ptr(), n, file_off, file_len, params)
+            torch.cuda.synchronize()
+        iso_ms, iso_n = ctx.profile_read()
+        iso = {s: iso_ms[s] / max(iso_n, 1) for s in STAGES}
     res = ctx.results()
     log("rank %d: %d blobs/step, stage ms/step: %s, host submit ms/step %.3f" %
         (rank, len(res), {k: round(v, 3) for k, v in per.items()}, host_ms[0] / args.steps))
@@ -243,6 +255,12 @@ def main():
                 "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
     if host is not None:
         roofline.update({"host_stream_pcie_frac": round(value / PCIE_PEAK_GBS, 4)})
+    if iso is not None:
+        # live durations above include the overlap with the other batch in flight
+        a_iso = algo / (iso["b3_leaf" if kernel == "k_b3_groups" else "scan"] * 1e-3) / 1e9
+        roofline["live_shares_gpu_with"] = "the other batch in flight (%d contexts)" % len(ctxs)
+        roofline["isolated"] = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
+                                "stage_ms_per_step": {k: round(v, 3) for k, v in iso.items()}}
 
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None
     seal = time_seal(ctx, data, res, file_off, args.steps) if args.seal else None

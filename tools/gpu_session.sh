@@ -19,5 +19,7 @@ if [[ "$MODE" == *bench* || "$MODE" == all ]]; then
 fi
 if [[ "$MODE" == *prof* || "$MODE" == all ]]; then
   cd /tmp && export TMPDIR=/tmp
-  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-check || exit 1
+  # the bench command itself (default steps / batches in flight), so the per-launch durations of
+  # the timed region can be compared with the bench line (tools/trace_split.py)
+  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline || exit 1
 fi
