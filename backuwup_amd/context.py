@@ -324,7 +324,7 @@ class Context:
         keep, a, b = self._pack_args(prk, src_off, src_len, hashes, kinds, nonces, plan, packfile_ids)
         a[1] = ctypes.c_void_p(d_src)
         check(self._L.bw_pack_build_device(self.h, *a, flags, *b, ctypes.c_void_p(d_out)), self.h)
-        self._keep = keep
+        self._pack_keep = keep
 
     def index_files_build(self, prk, entries, last_file_num=0):
         """BlobIndex::push + flush over n (hash, packfile id) entries (n x 44 bytes):

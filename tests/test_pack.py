@@ -16,7 +16,7 @@ import struct
 import numpy as np
 import pytest
 
-from backuwup_amd.synth import splitmix_bytes as _smb
+from backuwup_amd.synth import splitmix_bytes as _smb  # noqa: E402
 
 
 def splitmix_bytes(seed, n):
@@ -334,3 +334,63 @@ def test_index_load_errors(ctx, po):
         assert e.value.rc == rc
         assert ctx.index_size() == 0  # nothing seeded
     assert ctx.index_load_files(PRK, good).shape == (5, 44)
+
+
+@pytest.mark.gpu
+def test_two_backups_through_index_files(ctx, po):
+    """The reference's flow across two backups (BlobIndex::new -> load, add_blob gate, write_packfiles,
+    flush): backup 1 chunks, hashes and gates a corpus, packs its unique blobs and writes index files;
+    backup 2 starts from a fresh context seeded only by those files and sees every unchanged chunk
+    as a duplicate -- only the chunks around an edit are new -- and its new blobs pack and read back."""
+    import torch
+    from backuwup_amd import Context
+    z = _zstd()
+    files = [_smb(700 + i, n) for i, n in enumerate([5 << 20, 3 << 20, 700000, 9 << 20, 4096, 0])]
+    lens = np.array([len(f) for f in files], dtype=np.uint64)
+    offs = np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(offs[-1] + lens[-1]) + 16, dtype=np.uint8)
+    for o, f in zip(offs, files):
+        buf[int(o):int(o) + len(f)] = f
+    rng = np.random.default_rng(77)
+
+    def backup(c, data, seed_files):
+        c.index_reset()
+        if seed_files:
+            c.index_load_files(PRK, seed_files, want_entries=False)
+        res = c.process_files(data, offs, lens)
+        u = res[res["is_dup"] == 0]
+        plan, total = c.pack_plan(u["length"].astype(np.uint64))
+        ids = rng.integers(0, 256, (len(plan), 12), dtype=np.uint8)
+        nonces = rng.integers(0, 256, (len(u), 12), dtype=np.uint8)
+        src_off = offs[u["file"].astype(np.int64)] + u["offset"]
+        packs = c.pack_build(PRK, data, src_off, u["length"], u["digest"], np.zeros(len(u), np.uint8), nonces, plan,
+                             total, ids) if len(u) else np.zeros(0, np.uint8)
+        ents = []
+        for k, p in enumerate(plan):
+            for i in range(int(p["first_blob"]), int(p["first_blob"] + p["n_blobs"])):
+                ents.append(np.concatenate([u["digest"][i], ids[k]]))
+        return res, u, plan, ids, packs, np.array(ents, dtype=np.uint8).reshape(-1, 44), src_off
+
+    c2 = Context(0)
+    try:
+        res1, u1, plan1, ids1, packs1, ents1, _ = backup(ctx, buf, None)
+        assert len(u1) == len(res1)  # distinct random files: nothing repeats within backup 1
+        index_files = ctx.index_files_build(PRK, ents1, last_file_num=0)
+        # backup 2: same corpus with 100 bytes inserted into file 3 (a shift that CDC resyncs after)
+        edited = buf.copy()
+        o3 = int(offs[3])
+        edited[o3 + 4000000:o3 + int(lens[3])] = buf[o3 + 3999900:o3 + int(lens[3]) - 100]
+        res2, u2, plan2, ids2, packs2, ents2, src2 = backup(c2, edited, index_files)
+        new = set(map(bytes, u2["digest"]))
+        old = set(map(bytes, u1["digest"]))
+        assert new.isdisjoint(old) and 0 < len(u2) <= 4  # the edited chunk(s) and the file's new tail
+        assert set(u2["file"].tolist()) == {3}
+        # the new blobs read back from backup 2's packfiles
+        for k, p in enumerate(plan2):
+            pf = packs2[int(p["offset"]):int(p["offset"] + p["size"])].tobytes()
+            for i in range(int(p["first_blob"]), int(p["first_blob"] + p["n_blobs"])):
+                kind, payload = po.get_blob(PRK, bytes(ids2[k]), pf, bytes(u2["digest"][i]))
+                want = edited[int(src2[i]):int(src2[i] + u2["length"][i])].tobytes()
+                assert z.decompress(payload) == want
+    finally:
+        c2.close()
