@@ -267,6 +267,24 @@ def main():
     pack = time_pack(ctx, data, res, file_off, args.steps) if args.pack else None
 
     cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "c2":
+        # many files: the reference runs one task per file (dir_packer.rs:166), so the port runs
+        # them on all the cores this GPU's share of the box offers
+        from oracle import oracle
+        threads = min(16, os.cpu_count() or 1)
+        fo = np.asarray(file_off, dtype=np.uint64)
+        fl = np.asarray(file_len, dtype=np.uint64)
+        k = max(1, int(np.searchsorted(np.cumsum(fl), int(args.cpu_sample_gib * (1 << 30)))))
+        end = int(np.max(fo[:k] + fl[:k]))
+        hb = data[:end].cpu().numpy()
+        t1 = time.perf_counter()
+        r = oracle.process_files(hb, fo[:k], fl[:k], threads=threads)
+        ct = time.perf_counter() - t1
+        m = int(np.sum(fl[:k]))
+        cpu = {"value": round(m / ct / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+               "sample": "first %d files (%.2f GB, %d blobs) of the workload, oracle/bw_oracle.c "
+                         "FastCDC+BLAKE3+index, one file per task like the reference" % (k, m / 1e9, len(r)),
+               "seconds": round(ct, 2)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         from oracle import oracle
         m = int(args.cpu_sample_gib * (1 << 30))
