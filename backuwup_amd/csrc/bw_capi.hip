@@ -59,6 +59,9 @@ struct bw_ctx {
     hipEvent_t pk_done = nullptr;  // the host tables above reusable once this fired
     bool pk_pending = false;
 
+    // many small messages (tree blobs): pinned staging of the serialized bytes
+    PinBuf msg_stage;
+
     // persistent dedup index
     DevBuf table, log, dstate;
     uint64_t table_cap = 0, log_cap = 0, log_hi = 0;  // log_hi: host upper bound of log length
@@ -241,6 +244,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
         if (b->p) hipFree(b->p);
     if (c->stage.p) hipHostFree(c->stage.p);
     if (c->seal_stage.p) hipHostFree(c->seal_stage.p);
+    if (c->msg_stage.p) hipHostFree(c->msg_stage.p);
     if (c->seal_done) hipEventDestroy(c->seal_done);
     if (c->pk_done) hipEventDestroy(c->pk_done);
     if (c->meta_done) hipEventDestroy(c->meta_done);
@@ -697,6 +701,40 @@ extern "C" int bw_blake3_hash_many(bw_ctx* c, const uint8_t* data, uint64_t data
     return BW_OK;
 }
 
+uint8_t* bw::message_stage(bw_ctx* c, size_t bytes) {
+    hipSetDevice(c->device);
+    if (c->msg_stage.cap < bytes) {
+        hipStreamSynchronize(c->stream);
+        if (c->msg_stage.p) hipHostFree(c->msg_stage.p);
+        c->msg_stage.p = nullptr;
+        c->msg_stage.cap = 0;
+        const size_t want = bytes + bytes / 4 + 4096;
+        if (hipHostMalloc(&c->msg_stage.p, want, hipHostMallocDefault) != hipSuccess) {
+            c->err = "hipHostMalloc failed";
+            return nullptr;
+        }
+        c->msg_stage.cap = want;
+    }
+    return (uint8_t*)c->msg_stage.p;
+}
+
+int bw::hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const uint64_t* offs, const uint64_t* lens,
+                      uint64_t n, bool dedup, uint8_t* hashes, uint8_t* dup) {
+    if (!n) return BW_OK;
+    hipSetDevice(c->device);
+    if (int rc = upload_data(c, staged, total)) return rc;
+    bw_params p;
+    bw_params_default(&p);
+    p.flags = dedup ? 0 : BW_F_NO_DEDUP;
+    p.small_file_threshold = ~0ull;  // every message is one whole blob, in the order given
+    if (int rc = submit(c, P<uint8_t>(c->data), total, offs, lens, n, &p)) return rc;
+    HIPCHK(c, hipMemcpyAsync(hashes, c->digests.p, n * 32, hipMemcpyDeviceToHost, c->stream));
+    if (dedup) HIPCHK(c, hipMemcpyAsync(dup, c->is_dup.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->pending = false;
+    return dedup ? check_collision(c) : BW_OK;
+}
+
 extern "C" int bw_blake3_hash(bw_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[32]) {
     const uint64_t off = 0;
     static const uint8_t empty[16] = {0};
@@ -779,6 +817,7 @@ static int seal_submit(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* d
     const size_t bytes = n * sizeof(SealItem);
     if (c->seal_stage.cap < bytes) {
         if (c->seal_stage.p) hipHostFree(c->seal_stage.p);
+    if (c->msg_stage.p) hipHostFree(c->msg_stage.p);
         c->seal_stage.p = nullptr;
         c->seal_stage.cap = 0;
         const size_t want = bytes + bytes / 4 + 4096;

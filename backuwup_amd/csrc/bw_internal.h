@@ -164,6 +164,15 @@ void launch_seal(hipStream_t st, bool dec, bool framed, const uint8_t* src, uint
                  uint64_t n, const SealPads& pads, SealKey* keys, uint64_t n_pieces, uint32_t* parts, uint8_t* ok);
 uint32_t zstd_window_descriptor(uint64_t raw_len);
 
+// ------------------------------------------------------------------ many small messages (bw_capi.hip)
+// Pinned host staging owned by the context (valid until the next call that uses it).
+uint8_t* message_stage(bw_ctx* c, size_t bytes);
+// BLAKE3 of n whole messages lying in `staged` (from message_stage) at offs/lens, in one batch;
+// with dedup the digests go through the index in order (add_blob's gate) and dup[i] is the
+// verdict.  Synchronous; hashes (n x 32) and dup are host arrays.
+int hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const uint64_t* offs, const uint64_t* lens,
+                  uint64_t n, bool dedup, uint8_t* hashes, uint8_t* dup);
+
 // ------------------------------------------------------------------ packfiles / index files (bw_pack.hip)
 constexpr uint32_t ZSTD_BLOCK = 131072;           // zstd ZSTD_BLOCKSIZE_MAX
 constexpr uint32_t ZSTD_STRIDE = ZSTD_BLOCK + 3;  // a raw block with its 3-byte header

@@ -18,12 +18,17 @@
 //
 // Serialization is host work (names and metadata come from the file system walk); the BLAKE3 of
 // every piece and the index run on the GPU through the same kernels as the file blobs.
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <vector>
 
 #include "../../include/backuwup_gpu.h"
+#include "bw_internal.h"
 
 namespace {
 
@@ -68,6 +73,20 @@ uint8_t* serialize_piece(uint8_t* p, const bw_tree& t, uint64_t first, uint64_t 
     return p;
 }
 
+// fn(lo, hi) over [0, n) on up to 16 threads (host byte work of million-tree batches)
+template <typename F>
+void parallel_ranges(uint64_t n, F fn) {
+    const uint64_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t t = n < 65536 ? 1 : std::min<uint64_t>(hw, n / 32768);
+    if (t <= 1) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint64_t k = 0; k < t; k++) th.emplace_back(fn, n * k / t, n * (k + 1) / t);
+    for (auto& x : th) x.join();
+}
+
 bool valid(const bw_tree& t) {
     return t.kind <= 1 && (t.name_len == 0 || t.name) && (t.n_children == 0 || t.children);
 }
@@ -87,6 +106,9 @@ extern "C" int bw_tree_serialize(const bw_tree* t, const uint8_t* next_sibling, 
 extern "C" int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint32_t flags, uint8_t* tree_hashes,
                              bw_tree_blob* out, uint64_t cap, uint64_t* n_out) {
     if (!ctx || !n_out || (n && (!trees || !tree_hashes))) return BW_EINVAL;
+    const bool timing = getenv("BW_TREE_TIMING") != nullptr;
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t_ser = 0, t_hash = 0, t0 = now();
     for (uint64_t i = 0; i < n; i++)
         if (!valid(trees[i])) return BW_EINVAL;
     // canonical blob list: tree i's pieces 0 .. p_i - 1
@@ -101,6 +123,46 @@ extern "C" int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint
     const uint64_t nblobs = first_blob[n];
     *n_out = nblobs;
     if (out && cap < nblobs) return BW_ENOSPC;
+    const bool dedup = !(flags & BW_F_NO_DEDUP);
+    if (max_pieces == 1) {
+        std::vector<uint64_t> lens(n);
+        // no tree is split: serialize every tree (in parallel) straight into pinned staging, then
+        // one batch hashes them and gates them in order on the device
+        std::vector<uint64_t> offs(n);
+        uint64_t total = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            offs[i] = total;
+            lens[i] = piece_len(trees[i], trees[i].n_children, false);
+            total += lens[i];
+        }
+        const double ts = now();
+        uint8_t* buf = bw::message_stage(ctx, total + 16);
+        if (!buf) return BW_ENOMEM;
+        parallel_ranges(n, [&](uint64_t lo, uint64_t hi) {
+            for (uint64_t i = lo; i < hi; i++) serialize_piece(buf + offs[i], trees[i], 0, trees[i].n_children, nullptr);
+        });
+        const double th = now();
+        std::vector<uint8_t> dup(n, 0);
+        // one piece per tree: the piece hashes are the tree hashes
+        if (int rc = bw::hash_messages(ctx, buf, total, offs.data(), lens.data(), n, dedup, tree_hashes, dup.data()))
+            return rc;
+        const double tw = now();
+        if (out)
+            parallel_ranges(n, [&](uint64_t lo, uint64_t hi) {
+                for (uint64_t i = lo; i < hi; i++) {
+                    bw_tree_blob& o = out[i];
+                    memset(&o, 0, sizeof o);
+                    o.tree = i;
+                    o.length = lens[i];
+                    memcpy(o.hash, tree_hashes + i * 32, 32);
+                    o.is_dup = dup[i];
+                }
+            });
+        if (timing)
+            fprintf(stderr, "bw_tree_blobs: %llu trees (one piece each), serialize %.2f ms, hash+gate %.2f ms, "
+                    "total %.2f ms\n", (unsigned long long)n, th - ts, tw - th, now() - t0);
+        return BW_OK;
+    }
     std::vector<uint8_t> hashes(nblobs * 32);
     std::vector<uint64_t> lens(nblobs);
     // round r hashes piece p_i - 1 - r of every tree that has one: the last pieces first (no
@@ -123,6 +185,7 @@ extern "C" int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint
             blob_of.push_back(first_blob[i] + k);
             total += l;
         }
+        const double ts = now();
         buf.resize(total + 16);
         for (uint64_t j = 0, i = 0; i < n; i++) {
             const uint64_t p = first_blob[i + 1] - first_blob[i];
@@ -137,13 +200,20 @@ extern "C" int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint
             j++;
         }
         std::vector<uint8_t> h(offs.size() * 32);
+        const double th = now();
+        t_ser += th - ts;
         if (int rc = bw_blake3_hash_many(ctx, buf.data(), total, offs.data(), ln.data(), offs.size(), h.data()))
             return rc;
+        t_hash += now() - th;
         for (uint64_t j = 0; j < offs.size(); j++) memcpy(&hashes[blob_of[j] * 32], &h[j * 32], 32);
     }
     std::vector<uint8_t> dup(nblobs, 0);
+    const double td = now();
     if (!(flags & BW_F_NO_DEDUP) && nblobs)
         if (int rc = bw_index_check_insert(ctx, hashes.data(), nblobs, dup.data())) return rc;
+    if (timing)
+        fprintf(stderr, "bw_tree_blobs: %llu trees, serialize %.2f ms, hash %.2f ms, gate %.2f ms, total %.2f ms\n",
+                (unsigned long long)n, t_ser, t_hash, now() - td, now() - t0);
     for (uint64_t i = 0; i < n; i++) memcpy(tree_hashes + 32 * i, &hashes[first_blob[i] * 32], 32);
     if (out)
         for (uint64_t i = 0; i < n; i++)
