@@ -828,17 +828,23 @@ static int seal_submit(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* d
         c->seal_stage.cap = want;
     }
     SealItem* it = (SealItem*)c->seal_stage.p;
+    std::vector<uint64_t> piece0(n);
     uint64_t pieces = 0;
     for (uint64_t i = 0; i < n; i++) {
-        const uint64_t len = dec ? src_len[i] - 16 : src_len[i];
-        seal_fill_item(&it[i], src_off[i], len, dst_off[i], pieces, nonces + 12 * i, info + (uint64_t)info_len * i,
-                       info_len);
-        if (raw_len) {
-            it[i].raw_len = (uint32_t)raw_len[i];
-            it[i].wd = zstd_window_descriptor(raw_len[i]);
-        }
-        pieces += seal_pieces(len);
+        piece0[i] = pieces;
+        pieces += seal_pieces(dec ? src_len[i] - 16 : src_len[i]);
     }
+    parallel_ranges(n, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; i++) {
+            const uint64_t len = dec ? src_len[i] - 16 : src_len[i];
+            seal_fill_item(&it[i], src_off[i], len, dst_off[i], piece0[i], nonces + 12 * i,
+                           info + (uint64_t)info_len * i, info_len);
+            if (raw_len) {
+                it[i].raw_len = (uint32_t)raw_len[i];
+                it[i].wd = zstd_window_descriptor(raw_len[i]);
+            }
+        }
+    });
     if (int rc = ensure(c, c->seal_items, bytes)) return rc;
     if (int rc = ensure(c, c->seal_keys, n * sizeof(SealKey))) return rc;
     if (int rc = ensure(c, c->seal_parts, (pieces + 1) * 16)) return rc;
@@ -1008,27 +1014,36 @@ static int pack_submit(bw_ctx* c, const uint8_t* prk, const uint8_t* d_src, cons
         h_len[p] = f.header_len - BW_SEAL_TAG_BYTES;
         h_dst[p] = f.offset + 8;
         c->h_pk_files[p] = PackFileDesc{hdr_total, f.n_blobs, f.offset, f.header_len};
-        uint64_t entry = hdr_total + varint_len(f.n_blobs), section = 0;
-        const uint64_t data0 = f.offset + 8 + f.header_len;
-        for (uint64_t i = f.first_blob; i < f.first_blob + f.n_blobs; i++) {
-            const uint64_t frame = store ? bw_zstd_store_size(src_len[i]) : src_len[i];
-            const uint64_t sealed = frame + BW_SEAL_TAG_BYTES;
-            PackBlob& b = c->h_pk_blobs[i];
-            memcpy(b.hash, hashes + 32 * i, 32);
-            memcpy(b.nonce, nonces + 12 * i, 12);
-            b.kind = kinds[i];
-            b.sealed_len = sealed;
-            b.section_off = section;
-            b.hdr_off = entry;
-            b.nonce_off = data0 + section;
-            entry += entry_len(sealed, section);
-            section += sealed + BW_BLOB_NONCE_SIZE;
-            s_len[i] = frame;
-            s_off[i] = src_off[i];
-            d_off[i] = b.nonce_off + BW_BLOB_NONCE_SIZE;
-        }
-        hdr_total = entry;
+        hdr_total += h_len[p];
     }
+    // packfiles are independent once their header offsets are known: fill their blobs in parallel
+    parallel_ranges(
+        npf,
+        [&](uint64_t p_lo, uint64_t p_hi) {
+            for (uint64_t p = p_lo; p < p_hi; p++) {
+                const bw_packfile& f = plan[p];
+                uint64_t entry = h_off[p] + varint_len(f.n_blobs), section = 0;
+                const uint64_t data0 = f.offset + 8 + f.header_len;
+                for (uint64_t i = f.first_blob; i < f.first_blob + f.n_blobs; i++) {
+                    const uint64_t frame = store ? bw_zstd_store_size(src_len[i]) : src_len[i];
+                    const uint64_t sealed = frame + BW_SEAL_TAG_BYTES;
+                    PackBlob& b = c->h_pk_blobs[i];
+                    memcpy(b.hash, hashes + 32 * i, 32);
+                    memcpy(b.nonce, nonces + 12 * i, 12);
+                    b.kind = kinds[i];
+                    b.sealed_len = sealed;
+                    b.section_off = section;
+                    b.hdr_off = entry;
+                    b.nonce_off = data0 + section;
+                    entry += entry_len(sealed, section);
+                    section += sealed + BW_BLOB_NONCE_SIZE;
+                    s_len[i] = frame;
+                    s_off[i] = src_off[i];
+                    d_off[i] = b.nonce_off + BW_BLOB_NONCE_SIZE;
+                }
+            }
+        },
+        n);
     if (int rc = ensure(c, c->pk_blobs, n * sizeof(PackBlob))) return rc;
     if (int rc = ensure(c, c->pk_files, npf * sizeof(PackFileDesc))) return rc;
     if (int rc = ensure(c, c->pk_hdr, hdr_total)) return rc;

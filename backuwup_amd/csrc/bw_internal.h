@@ -1,5 +1,8 @@
 // bw_internal.h -- host-side declarations shared by the backuwup_amd translation units.
 #pragma once
+#include <algorithm>
+#include <thread>
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -163,6 +166,24 @@ void seal_fill_item(SealItem* it, uint64_t src_off, uint64_t len, uint64_t dst_o
 void launch_seal(hipStream_t st, bool dec, bool framed, const uint8_t* src, uint8_t* dst, const SealItem* items,
                  uint64_t n, const SealPads& pads, SealKey* keys, uint64_t n_pieces, uint32_t* parts, uint8_t* ok);
 uint32_t zstd_window_descriptor(uint64_t raw_len);
+
+// ------------------------------------------------------------------ host helpers
+// fn(lo, hi) over [0, n) on up to 16 threads: the host-side table work of million-item batches
+// (16 = this GPU's share of the box's cores).  `work` (default n) sizes the thread count; small
+// work runs inline.
+template <typename F>
+void parallel_ranges(uint64_t n, F fn, uint64_t work = 0) {
+    if (!work) work = n;
+    const uint64_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t t = work < 65536 ? 1 : std::min<uint64_t>(std::min<uint64_t>(hw, work / 32768), n);
+    if (t <= 1) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint64_t k = 0; k < t; k++) th.emplace_back(fn, n * k / t, n * (k + 1) / t);
+    for (auto& x : th) x.join();
+}
 
 // ------------------------------------------------------------------ many small messages (bw_capi.hip)
 // Pinned host staging owned by the context (valid until the next call that uses it).

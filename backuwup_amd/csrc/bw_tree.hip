@@ -24,7 +24,6 @@
 
 #include <algorithm>
 #include <chrono>
-#include <thread>
 #include <vector>
 
 #include "../../include/backuwup_gpu.h"
@@ -71,20 +70,6 @@ uint8_t* serialize_piece(uint8_t* p, const bw_tree& t, uint64_t first, uint64_t 
         p += 32;
     }
     return p;
-}
-
-// fn(lo, hi) over [0, n) on up to 16 threads (host byte work of million-tree batches)
-template <typename F>
-void parallel_ranges(uint64_t n, F fn) {
-    const uint64_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const uint64_t t = n < 65536 ? 1 : std::min<uint64_t>(hw, n / 32768);
-    if (t <= 1) {
-        fn(0, n);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (uint64_t k = 0; k < t; k++) th.emplace_back(fn, n * k / t, n * (k + 1) / t);
-    for (auto& x : th) x.join();
 }
 
 bool valid(const bw_tree& t) {
@@ -138,7 +123,7 @@ extern "C" int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint
         const double ts = now();
         uint8_t* buf = bw::message_stage(ctx, total + 16);
         if (!buf) return BW_ENOMEM;
-        parallel_ranges(n, [&](uint64_t lo, uint64_t hi) {
+        bw::parallel_ranges(n, [&](uint64_t lo, uint64_t hi) {
             for (uint64_t i = lo; i < hi; i++) serialize_piece(buf + offs[i], trees[i], 0, trees[i].n_children, nullptr);
         });
         const double th = now();
@@ -148,7 +133,7 @@ extern "C" int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint
             return rc;
         const double tw = now();
         if (out)
-            parallel_ranges(n, [&](uint64_t lo, uint64_t hi) {
+            bw::parallel_ranges(n, [&](uint64_t lo, uint64_t hi) {
                 for (uint64_t i = lo; i < hi; i++) {
                     bw_tree_blob& o = out[i];
                     memset(&o, 0, sizeof o);
