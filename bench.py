@@ -56,6 +56,23 @@ def make_workload(name, gib, rank, dev, n_files):
         data, o, l = synth.vm_image_variants_torch(base, 16, dev, seed=1 + rank)
         return data, o, l, ("C3: VM images per GPU, %.1f GiB base + 15 variants (32 byte indels + 16 x 4 KiB "
                             "overwrites each) = %.1f GiB" % (gib, data.numel() / 2**30))
+    if name == "c5":
+        # 4 families of C3-style images (base seed 1 + family), 16 files of
+        # `gib` GiB each; every family is split over 2 ranks (8 files each), so at 8 GPUs the job
+        # holds 256 GiB and ranks r, r^1 share a base image (cross-rank duplicates go through the
+        # digest exchange).  The rank's files are staged to pinned host memory by the caller.
+        fam, half = (rank // 2, rank % 2)
+        base = int(gib * (1 << 30))
+        full, o, l = synth.vm_image_variants_torch(base, 16, dev, seed=1 + fam)
+        lo, hi = int(o[8 * half]), int(o[8 * half + 7] + l[8 * half + 7])
+        data = full[lo:hi].clone()
+        del full
+        torch.cuda.empty_cache()
+        o = (o[8 * half:8 * half + 8] - np.uint64(lo)).astype(np.uint64)
+        l = l[8 * half:8 * half + 8]
+        return data, o, l, ("C5: VM-image family %d (base seed %d, %.1f GiB base), files %d-%d of its 16 on this "
+                            "rank = %.1f GiB, staged in pinned host memory" %
+                            (fam, 1 + fam, gib, 8 * half, 8 * half + 7, data.numel() / 2**30))
     if name == "c4":
         u, o, l = synth.small_files_table(n_files, seed=3 + rank)
         data = synth.splitmix_torch(3 + rank, u, dev)
@@ -69,9 +86,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--gib", type=float, default=None,
-                    help="C2: stream size per GPU; C1: corpus size; C3: base image size (GiB)")
+                    help="C2: stream size per GPU; C1: corpus size; C3/C5: base image size (GiB)")
     ap.add_argument("--files", type=int, default=1000000, help="C4: files per GPU")
     ap.add_argument("--cpu-sample-gib", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -91,7 +108,9 @@ def main():
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
     if args.gib is None:
-        args.gib = {"c1": 1.0, "c2": 16.0, "c3": 4.0, "c4": 0.0}[args.workload]
+        args.gib = {"c1": 1.0, "c2": 16.0, "c3": 4.0, "c4": 0.0, "c5": 4.0}[args.workload]
+    if args.workload == "c5":
+        args.host_stream = True  # C5 is quoted end to end from pinned host memory
 
     import numpy as np
     import torch
@@ -281,7 +300,7 @@ def main():
         r = oracle.process_files(hb, fo[:k], fl[:k], threads=threads)
         ct = time.perf_counter() - t1
         m = int(np.sum(fl[:k]))
-        cpu = {"value": round(m / ct / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+        cpu = {"value": round(m / ct / 1e9, 4), "unit": "GB/s", "cores": min(threads, k), "kind": "port",
                "sample": "first %d files (%.2f GB, %d blobs) of the workload, oracle/bw_oracle.c "
                          "FastCDC+BLAKE3+index, one file per task like the reference" % (k, m / 1e9, len(r)),
                "seconds": round(ct, 2)}
