@@ -90,7 +90,9 @@ def main():
     ap.add_argument("--gib", type=float, default=None,
                     help="C2: stream size per GPU; C1: corpus size; C3/C5: base image size (GiB)")
     ap.add_argument("--files", type=int, default=1000000, help="C4: files per GPU")
-    ap.add_argument("--cpu-sample-gib", type=float, default=4.0)
+    ap.add_argument("--cpu-sample-gib", type=float, default=None,
+                    help="CPU baseline sample (default: 8 GiB of C2 on one core, ~10 s; up to 16 GiB of files "
+                         "on 16 cores for the other workloads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
@@ -109,6 +111,8 @@ def main():
     args = ap.parse_args()
     if args.gib is None:
         args.gib = {"c1": 1.0, "c2": 16.0, "c3": 4.0, "c4": 0.0, "c5": 4.0}[args.workload]
+    if args.cpu_sample_gib is None:
+        args.cpu_sample_gib = 8.0 if args.workload == "c2" else 16.0
     if args.workload == "c5":
         args.host_stream = True  # C5 is quoted end to end from pinned host memory
 
