@@ -168,6 +168,24 @@ def test_process_files_mixed(ctx, oracle):
     assert got["is_dup"].sum() > 0
 
 
+def test_process_files_threshold_edges(ctx, oracle):
+    # dir_packer.rs:246: CDC only when file_len > 1 MiB; lengths around that threshold and around
+    # the chunker's min / max (a file is chunked from its own start), plus empty files
+    mib = 1 << 20
+    lens = np.array([0, 1, mib - 1, mib, mib + 1, mib + 2, 262144 + 1, 3145728 - 1, 3145728, 3145728 + 1,
+                     2 * 3145728 + 262144, 2 * 3145728 + 262145, 0, mib], dtype=np.uint64)
+    data = splitmix_bytes(33, int(lens.sum()) + 64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data[int(offs[-1]):int(offs[-1] + lens[-1])] = data[int(offs[3]):int(offs[3] + lens[3])]  # copy of file 3
+    ctx.index_reset()
+    got = ctx.process_files(data, offs, lens)
+    want = oracle.process_files(data, offs, lens)
+    blobs_equal(got, want)
+    per_file = np.bincount(got["file"].astype(np.int64), minlength=len(lens))
+    assert list(per_file[:4]) == [1, 1, 1, 1]  # <= 1 MiB: one blob each
+    assert bool(got["is_dup"][-1]) and int(got["file"][-1]) == len(lens) - 1
+
+
 def test_process_files_small_params_many_files(ctx, oracle):
     rng = np.random.default_rng(9)
     lens = rng.integers(0, 300_000, 120).astype(np.uint64)
