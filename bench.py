@@ -31,6 +31,10 @@ sys.path.insert(0, ROOT)
 METRIC = "GB/s chunked+hashed+deduped (whole node, 1/2/4/8 GPU), bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: PCIe Gen5 x16, 63 GB/s (spec)
+# k_b3_groups' own ceiling: 0.1845 wave-instructions per input byte (SQ_INSTS_VALU)
+# at the measured issue costs of its mix (tools/op_rate.hip: ~3.55 cycles per instruction per
+# SIMD) on 1024 SIMDs at the 1.94 GHz top of the clock the chip holds under this load
+B3_VALU_CEILING_GBS = 3000.0
 
 
 def log(*a):
@@ -276,6 +280,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, kernel), "kernel": kernel,
                 "algorithmic_bytes_per_launch": algo,
                 "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
+    if kernel == "k_b3_groups":
+        # the limit this kernel actually meets: integer VALU issue (B3_VALU_CEILING_GBS)
+        roofline["valu_issue"] = {"ceiling": B3_VALU_CEILING_GBS, "unit": "GB/s",
+                                  "frac": round(achieved / B3_VALU_CEILING_GBS, 4)}
     if host is not None:
         roofline.update({"host_stream_pcie_frac": round(value / PCIE_PEAK_GBS, 4)})
     if iso is not None:
@@ -283,6 +291,8 @@ def main():
         a_iso = algo / (iso["b3_leaf" if kernel == "k_b3_groups" else "scan"] * 1e-3) / 1e9
         roofline["live_shares_gpu_with"] = "the other batch in flight (%d contexts)" % len(ctxs)
         roofline["isolated"] = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
+                                "valu_issue_frac": (round(a_iso / B3_VALU_CEILING_GBS, 4)
+                                                    if kernel == "k_b3_groups" else None),
                                 "stage_ms_per_step": {k: round(v, 3) for k, v in iso.items()}}
 
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None
