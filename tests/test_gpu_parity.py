@@ -290,13 +290,22 @@ def test_exchange_dedup_rccl_world1(ctx, oracle):
     import torch.distributed as dist
     from backuwup_amd.sharded import DeviceShardOps, exchange_dedup
     from backuwup_amd.synth import small_files
-    if not dist.is_initialized():
+    owned = not dist.is_initialized()
+    if owned:
         s = socket.socket()
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
         s.close()
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        _exchange_world1(ctx, torch, DeviceShardOps, exchange_dedup, small_files)
+    finally:
+        if owned:
+            dist.destroy_process_group()
+
+
+def _exchange_world1(ctx, torch, DeviceShardOps, exchange_dedup, small_files):
     data, offs, lens = small_files(4000, seed=8)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     ctx.index_reset()
