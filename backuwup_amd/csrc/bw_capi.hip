@@ -4,6 +4,7 @@
 // every byte of file data is read on the GPU.  A batch is enqueued on one HIP stream with no
 // host synchronisation until results are requested, so a caller can keep batches in flight.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -152,6 +153,7 @@ static int make_masks(uint32_t mn, uint32_t av, uint32_t mx, Masks* mk) {
     mk->mask_pre = mk->mask_s & mk->mask_l;
     mk->pre_shift = (uint32_t)__builtin_clzll(mk->mask_s | mk->mask_l);  // 63 - top bit
     mk->pre_hi = (uint32_t)((mk->mask_pre << mk->pre_shift) >> 32);
+    mk->tile_shift = SCAN_TILE_SHIFT;
     return BW_OK;
 }
 
@@ -458,7 +460,14 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     const uint64_t nseg = segs.size(), ncf = cfs.size(), nunits = units.size();
     const uint64_t max_groups = total_len / 4096 + max_blobs + 1;
     const int max_leaves = (int)std::min<uint64_t>((max_blob_len + 1023) / 1024, 1u << 30);
-    const uint64_t n_tiles = ncf ? (data_len + SCAN_TILE - 1) / SCAN_TILE : 0;
+    // small batches scan half-size tiles: with one 128 KiB tile per wave the per-tile start
+    // costs dominate (C1: 0.50 -> 0.33 ms per GiB); large ones keep the longer strips
+    // (BW_SCAN_SMALL_BYTES overrides the threshold, so the tests can run either tile size on any input)
+    const char* sb = getenv("BW_SCAN_SMALL_BYTES");
+    const uint64_t small_bytes = sb ? strtoull(sb, nullptr, 10) : SCAN_SMALL_BYTES;
+    mk.tile_shift = data_len < small_bytes ? SCAN_TILE_SHIFT - 1 : SCAN_TILE_SHIFT;
+    const uint64_t tile_bytes = 1ull << mk.tile_shift;
+    const uint64_t n_tiles = ncf ? (data_len + tile_bytes - 1) / tile_bytes : 0;
 
     // ---- device buffers
     int rc = 0;

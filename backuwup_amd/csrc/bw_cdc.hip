@@ -149,7 +149,7 @@ __device__ __forceinline__ void refine_block(const uint8_t* __restrict__ data, u
     record_hit(b + lane, h >> mk.pre_shift, mk, cnt, slots);
 }
 
-template <int BLOCK>
+template <int BLOCK, int STRIP>
 __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
                                                        uint64_t n_tiles, Masks mk,
                                                        uint32_t* __restrict__ tile_count,
@@ -184,10 +184,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
 
     for (uint64_t tile = (uint64_t)blockIdx.x * WAVES + wid; tile < n_tiles; tile += nw) {
         if (lane == 0) { *cnt = 0; *fcnt = 0; }
-        const uint64_t base = tile * SCAN_TILE;
-        const uint64_t ss = base + (uint64_t)lane * SCAN_STRIP;
+        const uint64_t base = tile * (64ull * STRIP);
+        const uint64_t ss = base + (uint64_t)lane * STRIP;
         uint64_t h = 0;
-        if (base + SCAN_TILE <= n_bytes) {
+        if (base + (64ull * STRIP) <= n_bytes) {
             if (ss >= 64) {  // warm-up on the 64 bytes before the strip
                 const uint4* wp = (const uint4*)(data + ss - 64);
                 uint4 w[4];
@@ -207,11 +207,11 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
                 // loads run one double step (two 64-byte steps) ahead, so the second half of a
                 // line meets the first half's miss in L2 instead of arriving one step later,
                 // after ~4 MiB of other waves' half-open lines per XCD have evicted it.
-                const uint8_t* src = data + base + (uint64_t)(lane >> 2) * SCAN_STRIP + (lane & 3) * 16;
+                const uint8_t* src = data + base + (uint64_t)(lane >> 2) * STRIP + (lane & 3) * 16;
                 uint8_t* wr = stage + (lane >> 2) * STAGE_ROW + (lane & 3) * 16;
                 const uint8_t* rd = stage + lane * STAGE_ROW;
-                constexpr int STEPS = SCAN_STRIP / SCAN_STEP;
-                constexpr uint64_t JS = 16ull * SCAN_STRIP;
+                constexpr int STEPS = STRIP / SCAN_STEP;
+                constexpr uint64_t JS = 16ull * STRIP;
 #define BW_LOAD8(r, ds)                                                                          \
     do {                                                                                         \
         const uint8_t* s_ = src + (uint64_t)(ds) * (2 * SCAN_STEP);                              \
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
             }
         } else if (ss < n_bytes) {  // ragged last sub-tile: exact byte path (h' >> pre_shift is h
                                     // modulo 2^(64 - pre_shift), which holds every mask bit)
-            const uint64_t se = ss + SCAN_STRIP < n_bytes ? ss + SCAN_STRIP : n_bytes;
+            const uint64_t se = ss + STRIP < n_bytes ? ss + STRIP : n_bytes;
             for (uint64_t p = ss >= 64 ? ss - 64 : 0; p < se; p++) {
                 h = (h << 1) + s_gear[(uint32_t)data[p] * GEAR_REP];
                 if (p >= ss) record_hit(p, h >> mk.pre_shift, mk, cnt, slots);
@@ -269,19 +269,22 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
     }
 }
 
-template <int BLOCK>
+template <int BLOCK, int STRIP>
 static void launch_scan_t(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                           uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf, uint64_t* ctr) {
     uint64_t grid = (n_tiles + BLOCK / 64 - 1) / (BLOCK / 64);
     if (grid > 512) grid = 512;  // persistent: every CU holds one block (LDS), two rounds
-    hipLaunchKernelGGL((k_scan<BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes,
+    hipLaunchKernelGGL((k_scan<BLOCK, STRIP>), dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes,
                        n_tiles, mk, tile_count, tile_slots, ovf, ctr);
 }
 
 void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                  uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf, uint64_t* ctr) {
     if (!n_tiles) return;
-    launch_scan_t<SCAN_BLOCK>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
+    if (64ull * SCAN_STRIP == 1ull << mk.tile_shift)
+        launch_scan_t<SCAN_BLOCK, SCAN_STRIP>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
+    else if (64ull * SCAN_STRIP_SMALL == 1ull << mk.tile_shift)
+        launch_scan_t<SCAN_BLOCK, SCAN_STRIP_SMALL>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
 }
 
 // ======================================================================== block scan helpers
@@ -387,7 +390,6 @@ __global__ void k_compact(const uint32_t* __restrict__ cnt, const uint64_t* __re
 // parameters): WRITE = false counts a tile's candidates before the offset scan (tile_count =
 // count | TILE_OVF), WRITE = true stores them at the tile's offset after it.
 constexpr int RESCAN_THREADS = 256;
-constexpr uint64_t RESCAN_STRIP = SCAN_TILE / RESCAN_THREADS;
 
 template <bool WRITE>
 __global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __restrict__ data, uint64_t n_bytes,
@@ -402,8 +404,9 @@ __global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __rest
     const uint64_t novf = ctr[C_NOVF];
     for (uint64_t k = blockIdx.x; k < novf; k += gridDim.x) {
         const uint64_t tile = ovf[k];
-        const uint64_t ss = tile * SCAN_TILE + (uint64_t)threadIdx.x * RESCAN_STRIP;
-        const uint64_t se = ss + RESCAN_STRIP < n_bytes ? ss + RESCAN_STRIP : n_bytes;
+        const uint64_t rs = (1ull << mk.tile_shift) / RESCAN_THREADS;  // bytes per thread
+        const uint64_t ss = (tile << mk.tile_shift) + (uint64_t)threadIdx.x * rs;
+        const uint64_t se = ss + rs < n_bytes ? ss + rs : n_bytes;
         uint64_t mine = 0;
         for (int pass = 0; pass < (WRITE ? 2 : 1); pass++) {
             uint64_t h = 0, w = 0;
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_chains(Walker W, const
     const uint64_t j = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
     if (j >= nseg) return;
     const SegDesc sd = segs[j];
-    uint64_t s = sd.start, cptr = tile_off[s / SCAN_TILE];
+    uint64_t s = sd.start, cptr = tile_off[s >> W.mk.tile_shift];
     uint32_t n = 0;
     for (;;) {
         const uint64_t c = walk_next(W, s, sd.file_end, cptr);
@@ -659,7 +662,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_fallback(Walker W, con
     const uint64_t f = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
     if (f >= ncf || !cf_invalid[f]) return;
     const CFileDesc cf = cfiles[f];
-    uint64_t s = cf.start, cptr = tile_off[s / SCAN_TILE], n = 0;
+    uint64_t s = cf.start, cptr = tile_off[s >> W.mk.tile_shift], n = 0;
     while (s < cf.end) {
         if (bw_lane() == 0) fb_starts[cf.fb_off + n] = s;
         n++;

@@ -20,6 +20,9 @@ constexpr int SCAN_BLOCK = 1024;                                   // 16 waves, 
 #endif
 constexpr int SCAN_STRIP = BW_SCAN_STRIP;                          // bytes per lane
 constexpr uint64_t SCAN_TILE = 64ull * SCAN_STRIP;                 // one wave's sub-tile (128 KiB)
+constexpr int SCAN_STRIP_SMALL = SCAN_STRIP / 2;                   // batches below SCAN_SMALL_BYTES
+constexpr uint64_t SCAN_SMALL_BYTES = 4ull << 30;                  // (one tile per wave otherwise: slow)
+constexpr uint32_t SCAN_TILE_SHIFT = __builtin_ctzll(SCAN_TILE);
 constexpr int SCAN_CAP = BW_SCAN_CAP;                              // candidate slots per tile
 constexpr int SCAN_STEP = 64;                                      // bytes per lane per staged step
 constexpr int STAGE_ROW = SCAN_STEP + 16;                          // padded LDS staging row
@@ -46,6 +49,7 @@ struct Masks {
     uint64_t mask_s, mask_l, mask_pre;  // mask_pre = mask_s & mask_l (scan prefilter)
     uint32_t pre_shift;  // the scan carries h << pre_shift; 63 - top bit of (mask_s | mask_l)
     uint32_t pre_hi;     // bits of mask_pre inside the high dword of h << pre_shift
+    uint32_t tile_shift; // log2 of the scan tile in bytes (SCAN_TILE, or half of it for small batches)
 };
 
 // One boundary-resolution segment: a window [start, end) of one CDC file.

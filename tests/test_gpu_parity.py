@@ -264,6 +264,11 @@ def test_unmerged_chains_fall_back_exactly(ctx, oracle):
 def test_candidate_dense_input(ctx, oracle):
     """A period whose every window passes the prefilter: tiles overflow their slots and the exact
     rescan + candidate-capacity retry paths run."""
+    data = _dense_input()
+    assert ctx.fastcdc_chunks(data, *SMALL) == chunks_oracle(oracle, data, SMALL)
+
+
+def _dense_input():
     from oracle import oracle as o
     g = [int(x) for x in o.gear_table()]
     # find a byte b whose constant window hash -GEAR[b]*(2^64-1)... passes mask_l for SMALL params
@@ -278,7 +283,30 @@ def test_candidate_dense_input(ctx, oracle):
         pytest.skip("no constant byte passes the mask")
     data = np.full(3 << 20, b, dtype=np.uint8)
     data[:1000] = splitmix_bytes(1, 1000)
+    return data
+
+
+@pytest.mark.parametrize("small_bytes", ["0", "18446744073709551615"])
+def test_scan_tile_sizes(ctx, oracle, monkeypatch, small_bytes):
+    """Batches below 4 GiB scan half-size tiles (bw_capi.hip submit): force each tile size on the
+    same inputs -- ragged ends, the candidate-dense overflow/rescan path, many small-parameter
+    files and a multi-file corpus -- and compare with the oracle."""
+    from backuwup_amd.synth import tree_corpus
+    monkeypatch.setenv("BW_SCAN_SMALL_BYTES", small_bytes)
+    for n, p in [(1, SMALL), (64 * 1024 + 1, SMALL), ((3 << 20) + 12345, MID), ((40 << 20) + 7, BK)]:
+        data = splitmix_bytes(n, n)
+        assert ctx.fastcdc_chunks(data, *p) == chunks_oracle(oracle, data, p), n
+    data = _dense_input()
     assert ctx.fastcdc_chunks(data, *SMALL) == chunks_oracle(oracle, data, SMALL)
+    rng = np.random.default_rng(21)
+    lens = rng.integers(0, 400_000, 80).astype(np.uint64)
+    data = splitmix_bytes(91, int(lens.sum()) + 100)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    ctx.index_reset()
+    blobs_equal(ctx.process_files(data, offs, lens, make_params(*SMALL)), oracle.process_files(data, offs, lens, *SMALL))
+    data, offs, lens = tree_corpus(40 << 20, seed=12, max_file=9 << 20)
+    ctx.index_reset()
+    blobs_equal(ctx.process_files(data, offs, lens), oracle.process_files(data, offs, lens))
 
 
 def test_exchange_dedup_rccl_world1(ctx, oracle):
