@@ -8,6 +8,8 @@ modules mirror the reference's call sites:
   backuwup_amd.blake3.hash       <- blake3::hash              (dir_packer.rs:286)
   backuwup_amd.packer.BlobIndex  <- packfile::blob_index::BlobIndex (blob_index.rs:44-148)
   backuwup_amd.packer.process_files <- dir_packer::process_file + add_file_blob
+  Context.submit_host / submit_device / wait <- the same, pipelined (batches in flight, host-streamed)
+  Index + Context.attach_index    <- one BlobIndex shared by every task of a backup session
   Context.tree_blobs / tree_serialize <- split_serialize_tree + add_tree_to_blobs (dir_packer.rs:314-390)
   Context.seal / seal_device      <- derive_backup_key + Aes256Gcm (pack.rs:66-80, key_manager.rs:80-86)
   Context.pack_plan / pack_build  <- Manager::write_packfiles + serialize_packfile (pack.rs:115-227)
@@ -16,10 +18,11 @@ modules mirror the reference's call sites:
   backuwup_amd.stream_split       <- one long file split across ranks (halo windows, settlement)
 """
 from . import _lib
-from .context import BLOB_DTYPE, TREE_BLOB_DTYPE, Context, default_context, make_params, make_tree, tree_serialize
+from .context import (BLOB_DTYPE, TREE_BLOB_DTYPE, Context, Index, default_context, host_register, host_unregister,
+                      make_params, make_tree, tree_serialize)
 
-__all__ = ["Context", "default_context", "make_params", "make_tree", "tree_serialize", "BLOB_DTYPE",
-           "TREE_BLOB_DTYPE", "load_library"]
+__all__ = ["Context", "Index", "default_context", "make_params", "make_tree", "tree_serialize", "BLOB_DTYPE",
+           "TREE_BLOB_DTYPE", "host_register", "host_unregister", "load_library"]
 
 
 def load_library():

@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("BW_LIB") or os.path.join(HERE, "libbackuwup_amd.so")
 BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -1, -2, -3, -4, -5, -6
 BW_ECRYPTO, BW_EFORMAT = -7, -8
 BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
+BW_OPT_DEPTH, BW_OPT_SCAN_SMALL_BYTES, BW_OPT_CAND_CAP, BW_OPT_STAGE_CHUNK = 1, 2, 3, 4
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -81,6 +82,18 @@ SIGNATURES = [
     ("bw_index_seed", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("bw_index_check_insert", ctypes.c_int, [vp, vp, ctypes.c_uint64, u8p]),
     ("bw_index_size", ctypes.c_int, [vp, u64p]),
+    ("bw_index_check", ctypes.c_int, [vp]),
+    ("bw_index_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+    ("bw_index_destroy", None, [vp]),
+    ("bw_attach_index", ctypes.c_int, [vp, vp]),
+    ("bw_set_option", ctypes.c_int, [vp, ctypes.c_int, ctypes.c_uint64]),
+    ("bw_submit_device", ctypes.c_int, [vp, vp, ctypes.c_uint64, u64p, u64p, ctypes.c_uint64,
+                                        ctypes.POINTER(BwParams), u64p]),
+    ("bw_submit_host", ctypes.c_int, [vp, vp, ctypes.c_uint64, u64p, u64p, ctypes.c_uint64,
+                                      ctypes.POINTER(BwParams), u64p]),
+    ("bw_wait", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.POINTER(BwBlob), ctypes.c_uint64, u64p]),
+    ("bw_host_register", ctypes.c_int, [vp, ctypes.c_uint64]),
+    ("bw_host_unregister", ctypes.c_int, [vp]),
     ("bw_process_files", ctypes.c_int, [vp, vp, ctypes.c_uint64, u64p, u64p, ctypes.c_uint64,
                                         ctypes.POINTER(BwParams), ctypes.POINTER(BwBlob), ctypes.c_uint64,
                                         u64p]),

@@ -80,6 +80,39 @@ def tree_serialize(tree, next_sibling=None):
     return bytes(out[:n.value])
 
 
+class Index:
+    """One seen-chunk index (bw_index) that several contexts gate against: one backup session
+    with several batches in flight on several streams (BlobIndex behind the packer mutex,
+    blob_index.rs:44-57, packfile/mod.rs:77)."""
+
+    def __init__(self, device=0):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        check(self._L.bw_index_create(device, ctypes.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.bw_index_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_register(ptr, length):
+    """Page-lock [ptr, ptr + length) so submit_host DMAs it directly."""
+    check(_lib.load().bw_host_register(ctypes.c_void_p(ptr), length))
+
+
+def host_unregister(ptr):
+    check(_lib.load().bw_host_unregister(ctypes.c_void_p(ptr)))
+
+
 class Context:
     """Owns one bw_ctx on `device`.  Not thread-safe (like the reference's packer mutex)."""
 
@@ -203,6 +236,10 @@ class Context:
             check(self._L.bw_index_check_insert(self.h, _ptr(d), d.shape[0], out.ctypes.data_as(_lib.u8p)), self.h)
         return out
 
+    def index_check(self):
+        """Raises BwError(BW_ECOLLISION) if the index ever saw a 64-bit key collision."""
+        check(self._L.bw_index_check(self.h), self.h)
+
     def index_size(self):
         n = ctypes.c_uint64()
         check(self._L.bw_index_size(self.h, ctypes.byref(n)), self.h)
@@ -224,25 +261,64 @@ class Context:
         return out[:n.value]
 
     def submit_device(self, d_ptr, data_len, file_off, file_len, params=None):
-        """Enqueue a batch whose bytes are already in HBM (d_ptr = device address)."""
+        """Enqueue a batch whose bytes are already in HBM (d_ptr = device address) -> its ticket."""
         fo = np.ascontiguousarray(file_off, dtype=np.uint64)
         fl = np.ascontiguousarray(file_len, dtype=np.uint64)
-        self._keep = (fo, fl)
         p = params or make_params()
-        check(self._L.bw_process_files_device(self.h, ctypes.c_void_p(d_ptr), data_len,
-                                              fo.ctypes.data_as(_lib.u64p), fl.ctypes.data_as(_lib.u64p),
-                                              len(fo), ctypes.byref(p)), self.h)
+        t = ctypes.c_uint64()
+        check(self._L.bw_submit_device(self.h, ctypes.c_void_p(d_ptr), data_len, fo.ctypes.data_as(_lib.u64p),
+                                       fl.ctypes.data_as(_lib.u64p), len(fo), ctypes.byref(p), ctypes.byref(t)),
+              self.h)
+        return t.value
 
-    def results(self, cap=None):
+    def submit_host(self, data, file_off, file_len, params=None, data_len=None):
+        """Enqueue a batch whose bytes are in host memory -> its ticket.  `data` is a numpy array
+        (pageable: staged through pinned chunks before the call returns) or the address of pinned
+        memory (an int, e.g. a pinned torch tensor's data_ptr(), with data_len), which must stay
+        unchanged until wait(ticket)."""
+        fo = np.ascontiguousarray(file_off, dtype=np.uint64)
+        fl = np.ascontiguousarray(file_len, dtype=np.uint64)
+        if isinstance(data, int):
+            ptr, n = ctypes.c_void_p(data), int(data_len)
+        else:
+            buf = _as_u8(data)
+            ptr, n = _ptr(buf), buf.size
+        p = params or make_params()
+        t = ctypes.c_uint64()
+        check(self._L.bw_submit_host(self.h, ptr, n, fo.ctypes.data_as(_lib.u64p), fl.ctypes.data_as(_lib.u64p),
+                                     len(fo), ctypes.byref(p), ctypes.byref(t)), self.h)
+        return t.value
+
+    def _fetch(self, fn, cap, out=None):
         n = ctypes.c_uint64()
-        if cap is None:
-            rc = self._L.bw_results(self.h, None, 0, ctypes.byref(n))
+        if out is not None:
+            assert out.dtype == BLOB_DTYPE and out.flags.c_contiguous
+            cap = out.size
+        elif cap is None:
+            rc = fn(None, 0, ctypes.byref(n))
             if rc not in (_lib.BW_OK, _lib.BW_ENOSPC):
                 check(rc, self.h)
             cap = n.value
-        out = np.zeros(max(cap, 1), dtype=BLOB_DTYPE)
-        check(self._L.bw_results(self.h, out.ctypes.data_as(ctypes.POINTER(BwBlob)), cap, ctypes.byref(n)), self.h)
+        if out is None:
+            out = np.zeros(max(cap, 1), dtype=BLOB_DTYPE)
+        check(fn(out.ctypes.data_as(ctypes.POINTER(BwBlob)), cap, ctypes.byref(n)), self.h)
         return out[:n.value]
+
+    def wait(self, ticket, cap=None, out=None):
+        """Results of batch `ticket` (blocks until it is done); `out` = a reusable BLOB_DTYPE array."""
+        return self._fetch(lambda o, c, n: self._L.bw_wait(self.h, ticket, o, c, n), cap, out)
+
+    def results(self, cap=None):
+        """Results of the most recently submitted batch."""
+        return self._fetch(lambda o, c, n: self._L.bw_results(self.h, o, c, n), cap)
+
+    def set_option(self, option, value):
+        check(self._L.bw_set_option(self.h, option, int(value)), self.h)
+
+    def attach_index(self, index):
+        """Gate this context's batches through a shared Index (None: the private one)."""
+        check(self._L.bw_attach_index(self.h, index.h if index is not None else None), self.h)
+        self._index = index
 
     def device_views(self):
         n = ctypes.c_uint64()

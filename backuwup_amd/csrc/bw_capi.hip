@@ -2,12 +2,22 @@
 //
 // The host side only turns file sizes into small metadata tables (segments, canonical units);
 // every byte of file data is read on the GPU.  A batch is enqueued on one HIP stream with no
-// host synchronisation until results are requested, so a caller can keep batches in flight.
+// host synchronisation until results are requested, so a caller can keep batches in flight:
+//   * a context keeps the outputs of its last `depth` batches in a ring of slots, addressed by
+//     the ticket bw_submit_* returns (bw_wait), so batch k+1 can be queued before batch k is read;
+//   * bw_submit_host copies a batch from host memory on the context's copy stream, into the slot's
+//     own HBM buffer, while the previous batch computes (pinned memory is DMA'd directly, pageable
+//     memory goes through a ring of pinned staging chunks);
+//   * one dedup index (bw_index) can be shared by several contexts on several streams: every
+//     index operation waits for the index's previous operation (an event chain), so the batches of
+//     one backup session are gated in submission order whichever stream runs them.
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -31,21 +41,65 @@ struct PinBuf {
     size_t cap = 0;
 };
 
+constexpr int MAX_DEPTH = 8;
+constexpr int STAGE_RING = 4;
+
+// One batch's outputs (kept until the ring wraps) and its host-streamed input.
+struct Slot {
+    DevBuf ctr, digests, is_dup, packed, input;
+    PinBuf meta;                      // pinned metadata staging of this slot's batch
+    hipEvent_t meta_done = nullptr;   // `meta` reusable once this fired
+    hipEvent_t input_free = nullptr;  // the batch's last read of its input (BLAKE3) finished
+    hipEvent_t copied = nullptr;      // host-streamed input arrived in `input`
+    bool meta_pending = false, input_used = false;
+    uint64_t ticket = 0;  // 0: empty
+    uint64_t max_blobs = 0;
+    bool dedup = false;
+};
+
 }  // namespace
+
+// The seen-chunk index (BlobIndex, blob_index.rs:44-57): a digest log + an open-addressing table
+// in HBM.  Shared by every context attached to it; operations are serialized by `mu` on the host
+// and by the `tail` event on the GPU (each one waits for the previous one, on whatever stream).
+struct bw_index {
+    int device = 0;
+    std::mutex mu;
+    std::atomic<int> refs{1};
+    DevBuf table, log, dstate;
+    uint64_t table_cap = 0, log_cap = 0;
+    uint64_t log_hi = 0;     // host upper bound of the log length, in-flight appends included
+    uint64_t enq_total = 0;  // sum of the upper bounds of every append ever enqueued
+    hipEvent_t tail = nullptr;
+    bool tail_set = false;
+};
 
 struct bw_ctx {
     int device = 0;
-    hipStream_t own = nullptr, stream = nullptr;
+    hipStream_t own = nullptr, stream = nullptr, copy = nullptr;
     std::string err;
-    hipEvent_t meta_done = nullptr;  // staging buffer reusable once this fired
-    bool meta_pending = false;
 
-    // per-batch device buffers
-    DevBuf tile_count, tile_slots, tile_off, tile_btot, cand, ovf, ctr;
+    // per-batch device workspace (shared by the slots: batches run one after another on `stream`)
+    DevBuf tile_count, tile_slots, tile_off, tile_btot, cand, ovf;
     DevBuf segs, cfiles, units, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
-    DevBuf cv, cv2, digests, is_dup, packed, fstart, data, scratch, ucnt, ubtot;
-    PinBuf stage;
+    DevBuf cv, cv2, fstart, data, scratch, ucnt, ubtot;
+
+    // batches in flight: ring of result slots addressed by ticket
+    Slot slots[MAX_DEPTH];
+    int depth = 2;
+    uint64_t next_ticket = 1, last_ticket = 0;
+
+    // pageable host input: ring of pinned staging chunks on the copy stream
+    PinBuf ring[STAGE_RING];
+    hipEvent_t ring_ev[STAGE_RING] = {};
+    bool ring_set[STAGE_RING] = {};
+    uint64_t stage_chunk = 64ull << 20;
+
+    // options (bw_set_option)
+    uint64_t scan_small_bytes = SCAN_SMALL_BYTES;
+    uint64_t cand_cap_forced = 0;
+    uint64_t cand_override = 0;  // raised when a batch found more candidates than its array held
 
     // blob sealing (bw_seal.hip): item table staging + per-item key material + piece partials
     DevBuf seal_items, seal_keys, seal_parts, seal_ok, seal_io;
@@ -63,9 +117,10 @@ struct bw_ctx {
     // many small messages (tree blobs): pinned staging of the serialized bytes
     PinBuf msg_stage;
 
-    // persistent dedup index
-    DevBuf table, log, dstate;
-    uint64_t table_cap = 0, log_cap = 0, log_hi = 0;  // log_hi: host upper bound of log length
+    // dedup index: `idx` is `own` unless the context is attached to a shared one
+    bw_index* own_idx = nullptr;
+    bw_index* idx = nullptr;
+    uint64_t idx_mark = 0;  // idx->enq_total right after this context's last append
 
     // stage timing: two event sets, alternated per batch so recording never waits on the GPU
     bool prof = false;
@@ -74,17 +129,6 @@ struct bw_ctx {
     int ev_set = 0;
     double stage_ms[BW_N_STAGES] = {};
     uint64_t prof_batches = 0;
-
-    // last batch (kept so a batch whose candidate array overflowed can be re-run exactly)
-    uint64_t cand_override = 0;
-    const uint8_t* last_data = nullptr;
-    uint64_t last_len = 0;
-    std::vector<uint64_t> last_off, last_flen;
-    bw_params last_prm{};
-    bool pending = false;
-    uint64_t last_max_blobs = 0;
-    uint64_t last_nfiles = 0;
-    bool last_dedup = false;
 };
 
 // ------------------------------------------------------------------ helpers
@@ -103,6 +147,7 @@ static int ensure(bw_ctx* c, DevBuf& b, size_t bytes) {
     if (b.cap >= bytes) return BW_OK;
     if (b.p) {
         hipStreamSynchronize(c->stream);
+        if (c->copy) hipStreamSynchronize(c->copy);
         hipFree(b.p);
         b.p = nullptr;
         b.cap = 0;
@@ -117,22 +162,30 @@ static int ensure(bw_ctx* c, DevBuf& b, size_t bytes) {
     return BW_OK;
 }
 
-static int ensure_pinned(bw_ctx* c, PinBuf& b, size_t bytes) {
-    if (c->meta_pending) {
-        hipEventSynchronize(c->meta_done);
-        c->meta_pending = false;
-    }
+static int ensure_host(bw_ctx* c, PinBuf& b, size_t bytes) {
     if (b.cap >= bytes) return BW_OK;
     if (b.p) hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
     size_t want = bytes + bytes / 4 + 4096;
     if (hipHostMalloc(&b.p, want, hipHostMallocDefault) != hipSuccess) {
-        c->err = "hipHostMalloc failed";
-        b.p = nullptr;
-        b.cap = 0;
+        c->err = "hipHostMalloc(" + std::to_string(want) + ") failed";
         return BW_ENOMEM;
     }
     b.cap = want;
     return BW_OK;
+}
+
+static void free_dev(DevBuf& b) {
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+static void free_host(PinBuf& b) {
+    if (b.p) hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
 }
 
 template <typename T>
@@ -184,6 +237,145 @@ static void prof_mark(bw_ctx* c, int stage) {
     if (c->prof) hipEventRecord(c->ev[c->ev_set][stage], c->stream);
 }
 
+// ------------------------------------------------------------------ the index object
+
+static int index_init(bw_index* x, int device) {
+    x->device = device;
+    if (hipSetDevice(device) != hipSuccess) return BW_EHIP;
+    if (hipEventCreateWithFlags(&x->tail, hipEventDisableTiming) != hipSuccess) return BW_EHIP;
+    if (hipMalloc(&x->dstate.p, D_COUNT * 8) != hipSuccess) return BW_ENOMEM;
+    x->dstate.cap = D_COUNT * 8;
+    if (hipMemset(x->dstate.p, 0, D_COUNT * 8) != hipSuccess) return BW_EHIP;
+    return BW_OK;
+}
+
+static void index_release(bw_index* x) {
+    if (!x || --x->refs > 0) return;
+    hipSetDevice(x->device);
+    if (x->tail_set) hipEventSynchronize(x->tail);
+    free_dev(x->table);
+    free_dev(x->log);
+    free_dev(x->dstate);
+    if (x->tail) hipEventDestroy(x->tail);
+    delete x;
+}
+
+// Scope of one index operation issued on context c's stream: holds the index lock, makes the
+// stream wait for the previous operation (from any context) and records this one as the new tail.
+struct IndexOp {
+    bw_ctx* c;
+    bw_index* x;
+    std::lock_guard<std::mutex> lk;
+    explicit IndexOp(bw_ctx* cc) : c(cc), x(cc->idx), lk(cc->idx->mu) {
+        if (x->tail_set) hipStreamWaitEvent(c->stream, x->tail, 0);
+    }
+    ~IndexOp() {
+        hipEventRecord(x->tail, c->stream);
+        x->tail_set = true;
+    }
+};
+
+// Room for `incoming` more log entries (lock held).  Growth waits for every earlier operation of
+// the index (its tail) before the old buffers are replaced; sessions pre-size with bw_index_reset.
+static int index_capacity(bw_ctx* c, uint64_t incoming) {
+    bw_index* x = c->idx;
+    const uint64_t need_log = x->log_hi + incoming;
+    if (need_log > x->log_cap) {
+        uint64_t cap = x->log_cap ? x->log_cap : 1 << 16;
+        while (cap < need_log) cap *= 2;
+        DevBuf nb;
+        if (hipMalloc(&nb.p, cap * 32) != hipSuccess) {
+            c->err = "hipMalloc of the index log failed";
+            return BW_ENOMEM;
+        }
+        nb.cap = cap * 32;
+        if (x->log.p) {
+            HIPCHK(c, hipMemcpyAsync(nb.p, x->log.p, x->log_cap * 32, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            hipFree(x->log.p);
+        }
+        x->log = nb;
+        x->log_cap = cap;
+    }
+    // keep the table at most half full (upper bound: every logged digest distinct)
+    if (need_log * 2 > x->table_cap) {
+        uint64_t cap = x->table_cap ? x->table_cap : 1 << 16;
+        while (cap < need_log * 2) cap *= 2;
+        if (x->table.p) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            hipFree(x->table.p);
+            x->table.p = nullptr;
+        }
+        if (hipMalloc(&x->table.p, cap * 16) != hipSuccess) {
+            c->err = "hipMalloc of the index table failed";
+            return BW_ENOMEM;
+        }
+        x->table.cap = cap * 16;
+        const uint64_t old = x->table_cap;
+        x->table_cap = cap;
+        launch_table_clear(c->stream, P<uint64_t>(x->table), cap);
+        if (old) launch_rehash(c->stream, P<uint64_t>(x->table), cap, P<uint8_t>(x->log), P<uint64_t>(x->dstate),
+                               x->log_hi);
+    }
+    return BW_OK;
+}
+
+static int index_reset_locked(bw_ctx* c, uint64_t hint) {
+    bw_index* x = c->idx;
+    x->log_hi = 0;
+    HIPCHK(c, hipMemsetAsync(x->dstate.p, 0, D_COUNT * 8, c->stream));
+    if (int rc = index_capacity(c, hint ? hint : 1024)) return rc;
+    launch_table_clear(c->stream, P<uint64_t>(x->table), x->table_cap);
+    HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+// Append + gate n digests (n read on the device from n_dev when given; max_n bounds it).
+static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
+                        uint8_t* d_is_dup) {
+    IndexOp op(c);
+    bw_index* x = c->idx;
+    if (!x->table_cap)
+        if (int rc = index_reset_locked(c, 0)) return rc;
+    if (int rc = index_capacity(c, max_n)) return rc;
+    launch_dedup(c->stream, P<uint64_t>(x->table), x->table_cap, P<uint8_t>(x->log), P<uint64_t>(x->dstate),
+                 d_digests, n_dev, n_host, max_n, d_is_dup);
+    x->log_hi += max_n;
+    x->enq_total += max_n;
+    c->idx_mark = x->enq_total;
+    HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+// Read the index state (synchronizes the context stream): after every operation issued so far
+// from any context (all = true), or after this context's own last one (all = false: reading a
+// batch's results must not wait for batches queued behind it on other streams).
+static int read_index_state(bw_ctx* c, uint64_t st[D_COUNT], bool all) {
+    bw_index* x = c->idx;
+    uint64_t mark = c->idx_mark;  // appends at or before the read position
+    if (all) {
+        std::lock_guard<std::mutex> lk(x->mu);
+        if (x->tail_set) hipStreamWaitEvent(c->stream, x->tail, 0);
+        mark = x->enq_total;
+    }
+    HIPCHK(c, hipMemcpyAsync(st, x->dstate.p, D_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // tighten the host bound: appends enqueued after the read position add at most their bounds
+    std::lock_guard<std::mutex> lk(x->mu);
+    x->log_hi = std::min(x->log_hi, st[D_LOGLEN] + (x->enq_total - std::min(x->enq_total, mark)));
+    return BW_OK;
+}
+
+static int check_collision(bw_ctx* c, bool all = false) {
+    uint64_t st[D_COUNT];
+    if (int rc = read_index_state(c, st, all)) return rc;
+    if (st[D_COLLIDE]) {
+        c->err = "64-bit key collision between distinct digests";
+        return BW_ECOLLISION;
+    }
+    return BW_OK;
+}
+
 // ------------------------------------------------------------------ C ABI: basics
 
 extern "C" void bw_params_default(bw_params* p) {
@@ -214,18 +406,26 @@ extern "C" int bw_create(int device, bw_ctx** out) {
     *out = nullptr;
     bw_ctx* c = new bw_ctx();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->meta_done, hipEventDisableTiming) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return BW_EHIP;
     }
     c->stream = c->own;
-    if (ensure(c, c->dstate, D_COUNT * 8) || ensure(c, c->ctr, C_COUNT * 8)) {
-        delete c;
-        return BW_ENOMEM;
+    c->own_idx = new bw_index();
+    c->idx = c->own_idx;
+    if (int rc = index_init(c->own_idx, device)) {
+        bw_destroy(c);
+        return rc;
     }
-    hipMemsetAsync(c->dstate.p, 0, D_COUNT * 8, c->stream);
-    hipMemsetAsync(c->ctr.p, 0, C_COUNT * 8, c->stream);
+    for (int s = 0; s < MAX_DEPTH; s++) {
+        Slot& sl = c->slots[s];
+        if (hipEventCreateWithFlags(&sl.meta_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.input_free, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) != hipSuccess) {
+            bw_destroy(c);
+            return BW_EHIP;
+        }
+    }
     *out = c;
     return BW_OK;
 }
@@ -234,25 +434,40 @@ extern "C" void bw_destroy(bw_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->ctr, &c->segs,
+    if (c->copy) hipStreamSynchronize(c->copy);
+    DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->segs,
                      &c->cfiles, &c->units, &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
-                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->digests,
-                     &c->is_dup, &c->packed, &c->fstart, &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->table,
-                     &c->log, &c->dstate, &c->seal_items, &c->seal_keys, &c->seal_parts, &c->seal_ok,
-                     &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr,
-                     &c->pk_src, &c->pk_out, &c->ix_io, &c->ix_tab, &c->ix_dig};
-    for (DevBuf* b : all)
-        if (b->p) hipFree(b->p);
-    if (c->stage.p) hipHostFree(c->stage.p);
-    if (c->seal_stage.p) hipHostFree(c->seal_stage.p);
-    if (c->msg_stage.p) hipHostFree(c->msg_stage.p);
+                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->fstart,
+                     &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
+                     &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
+                     &c->ix_io, &c->ix_tab, &c->ix_dig};
+    for (DevBuf* b : all) free_dev(*b);
+    for (Slot& s : c->slots) {
+        free_dev(s.ctr);
+        free_dev(s.digests);
+        free_dev(s.is_dup);
+        free_dev(s.packed);
+        free_dev(s.input);
+        free_host(s.meta);
+        if (s.meta_done) hipEventDestroy(s.meta_done);
+        if (s.input_free) hipEventDestroy(s.input_free);
+        if (s.copied) hipEventDestroy(s.copied);
+    }
+    for (int r = 0; r < STAGE_RING; r++) {
+        free_host(c->ring[r]);
+        if (c->ring_ev[r]) hipEventDestroy(c->ring_ev[r]);
+    }
+    free_host(c->seal_stage);
+    free_host(c->msg_stage);
     if (c->seal_done) hipEventDestroy(c->seal_done);
     if (c->pk_done) hipEventDestroy(c->pk_done);
-    if (c->meta_done) hipEventDestroy(c->meta_done);
     for (int k = 0; k < 2; k++)
         for (int i = 0; i <= BW_N_STAGES; i++)
             if (c->ev[k][i]) hipEventDestroy(c->ev[k][i]);
+    if (c->idx != c->own_idx) index_release(c->idx);
+    index_release(c->own_idx);
+    if (c->copy) hipStreamDestroy(c->copy);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
 }
@@ -268,77 +483,70 @@ extern "C" int bw_set_stream(bw_ctx* c, void* s) {
 
 extern "C" void* bw_get_stream(bw_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-// ------------------------------------------------------------------ dedup index
+extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
+    if (!c) return BW_EINVAL;
+    switch (opt) {
+        case BW_OPT_DEPTH:
+            if (v < 1 || v > MAX_DEPTH) return BW_EINVAL;
+            hipSetDevice(c->device);
+            hipStreamSynchronize(c->stream);
+            if (c->copy) hipStreamSynchronize(c->copy);
+            c->depth = (int)v;
+            for (Slot& s : c->slots) s.ticket = 0;  // earlier tickets are no longer addressable
+            c->last_ticket = 0;
+            return BW_OK;
+        case BW_OPT_SCAN_SMALL_BYTES: c->scan_small_bytes = v; return BW_OK;
+        case BW_OPT_CAND_CAP: c->cand_cap_forced = v; return BW_OK;
+        case BW_OPT_STAGE_CHUNK:
+            if (v < 4096) return BW_EINVAL;
+            hipSetDevice(c->device);
+            if (c->copy) hipStreamSynchronize(c->copy);
+            for (int r = 0; r < STAGE_RING; r++) free_host(c->ring[r]);
+            c->stage_chunk = v;
+            return BW_OK;
+        default: return BW_EINVAL;
+    }
+}
 
-static int index_capacity(bw_ctx* c, uint64_t incoming) {
-    const uint64_t need_log = c->log_hi + incoming;
-    if (need_log > c->log_cap) {
-        uint64_t cap = c->log_cap ? c->log_cap : 1 << 16;
-        while (cap < need_log) cap *= 2;
-        DevBuf nb;
-        if (hipMalloc(&nb.p, cap * 32) != hipSuccess) return BW_ENOMEM;
-        nb.cap = cap * 32;
-        if (c->log.p) {
-            hipMemcpyAsync(nb.p, c->log.p, c->log_cap * 32, hipMemcpyDeviceToDevice, c->stream);
-            hipStreamSynchronize(c->stream);
-            hipFree(c->log.p);
-        }
-        c->log = nb;
-        c->log_cap = cap;
+// ------------------------------------------------------------------ dedup index (C ABI)
+
+extern "C" int bw_index_create(int device, bw_index** out) {
+    if (!out) return BW_EINVAL;
+    *out = nullptr;
+    bw_index* x = new bw_index();
+    if (int rc = index_init(x, device)) {
+        index_release(x);
+        return rc;
     }
-    // keep the table at most half full (upper bound: every logged digest distinct)
-    if (need_log * 2 > c->table_cap) {
-        uint64_t cap = c->table_cap ? c->table_cap : 1 << 16;
-        while (cap < need_log * 2) cap *= 2;
-        if (c->table.p) {
-            hipStreamSynchronize(c->stream);
-            hipFree(c->table.p);
-            c->table.p = nullptr;
-        }
-        if (hipMalloc(&c->table.p, cap * 16) != hipSuccess) return BW_ENOMEM;
-        c->table.cap = cap * 16;
-        const uint64_t old = c->table_cap;
-        c->table_cap = cap;
-        launch_table_clear(c->stream, P<uint64_t>(c->table), cap);
-        if (old) launch_rehash(c->stream, P<uint64_t>(c->table), cap, P<uint8_t>(c->log), P<uint64_t>(c->dstate),
-                               c->log_hi);
+    *out = x;
+    return BW_OK;
+}
+
+extern "C" void bw_index_destroy(bw_index* x) { index_release(x); }
+
+extern "C" int bw_attach_index(bw_ctx* c, bw_index* x) {
+    if (!c) return BW_EINVAL;
+    if (!x) x = c->own_idx;
+    if (x->device != c->device) {
+        c->err = "index and context live on different devices";
+        return BW_EINVAL;
     }
+    if (x == c->idx) return BW_OK;
+    hipSetDevice(c->device);
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // this context's work on the old index is done
+    bw_index* old = c->idx;
+    if (x != c->own_idx) x->refs++;
+    c->idx = x;
+    c->idx_mark = 0;
+    if (old != c->own_idx) index_release(old);
     return BW_OK;
 }
 
 extern "C" int bw_index_reset(bw_ctx* c, uint64_t hint) {
     if (!c) return BW_EINVAL;
     hipSetDevice(c->device);
-    c->log_hi = 0;
-    hipMemsetAsync(c->dstate.p, 0, D_COUNT * 8, c->stream);
-    if (int rc = index_capacity(c, hint ? hint : 1024)) return rc;
-    launch_table_clear(c->stream, P<uint64_t>(c->table), c->table_cap);
-    HIPCHK(c, hipGetLastError());
-    return BW_OK;
-}
-
-static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
-                        uint8_t* d_is_dup) {
-    if (!c->table_cap)
-        if (int rc = bw_index_reset(c, 0)) return rc;
-    if (int rc = index_capacity(c, max_n)) return rc;
-    launch_dedup(c->stream, P<uint64_t>(c->table), c->table_cap, P<uint8_t>(c->log), P<uint64_t>(c->dstate),
-                 d_digests, n_dev, n_host, max_n, d_is_dup);
-    c->log_hi += max_n;
-    HIPCHK(c, hipGetLastError());
-    return BW_OK;
-}
-
-static int check_collision(bw_ctx* c) {
-    uint64_t st[D_COUNT];
-    HIPCHK(c, hipMemcpyAsync(st, c->dstate.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->log_hi = st[D_LOGLEN];  // tighten the host bound
-    if (st[D_COLLIDE]) {
-        c->err = "64-bit key collision between distinct digests";
-        return BW_ECOLLISION;
-    }
-    return BW_OK;
+    IndexOp op(c);
+    return index_reset_locked(c, hint);
 }
 
 extern "C" int bw_index_seed(bw_ctx* c, const uint8_t* sorted, uint64_t n) {
@@ -370,35 +578,54 @@ extern "C" int bw_index_check_insert_device(bw_ctx* c, const uint8_t* d_digests,
     return dedup_device(c, d_digests, nullptr, n, n, d_is_dup);
 }
 
+extern "C" int bw_index_check(bw_ctx* c) {
+    if (!c) return BW_EINVAL;
+    hipSetDevice(c->device);
+    return check_collision(c, true);
+}
+
 extern "C" int bw_index_size(bw_ctx* c, uint64_t* n) {
     if (!c || !n) return BW_EINVAL;
+    hipSetDevice(c->device);
     uint64_t st[D_COUNT];
-    HIPCHK(c, hipMemcpyAsync(st, c->dstate.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = read_index_state(c, st, true)) return rc;
     *n = st[D_NUNIQUE];
     return BW_OK;
 }
 
 // ------------------------------------------------------------------ the batch pipeline
 
-static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff, const uint64_t* flen,
-                  uint64_t nf, const bw_params* prm) {
-    Masks mk;
-    if (int rc = make_masks(prm->min_size, prm->avg_size, prm->max_size, &mk)) {
+static Slot* slot_of(bw_ctx* c, uint64_t ticket) {
+    if (!ticket || ticket >= c->next_ticket) return nullptr;
+    Slot* s = &c->slots[(ticket - 1) % (uint64_t)c->depth];
+    return s->ticket == ticket ? s : nullptr;
+}
+
+static int validate_batch(bw_ctx* c, uint64_t data_len, const uint64_t* foff, const uint64_t* flen, uint64_t nf,
+                          const bw_params* prm, Masks* mk) {
+    if (int rc = make_masks(prm->min_size, prm->avg_size, prm->max_size, mk)) {
         c->err = "fastcdc parameters out of range";
         return rc;
     }
     if (nf && (!foff || !flen)) return BW_EINVAL;
-    if (data_len && !d_data) return BW_EINVAL;
-    if (((uintptr_t)d_data & 15) != 0) {
-        c->err = "device data pointer must be 16-byte aligned";
-        return BW_EINVAL;
-    }
     for (uint64_t f = 0; f < nf; f++)
         if (foff[f] > data_len || flen[f] > data_len - foff[f]) {
             c->err = "file " + std::to_string(f) + " lies outside the data buffer";
             return BW_EINVAL;
         }
+    return BW_OK;
+}
+
+// Enqueue one batch (bytes at d_data, in HBM) into slot `s` on the context stream.
+static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
+                  const uint64_t* flen, uint64_t nf, const bw_params* prm) {
+    Masks mk;
+    if (int rc = validate_batch(c, data_len, foff, flen, nf, prm, &mk)) return rc;
+    if (data_len && !d_data) return BW_EINVAL;
+    if (((uintptr_t)d_data & 15) != 0) {
+        c->err = "device data pointer must be 16-byte aligned";
+        return BW_EINVAL;
+    }
     hipSetDevice(c->device);
     const bool force_serial = (prm->flags & BW_F_SERIAL_RESOLVE) != 0;
     const bool do_hash = !(prm->flags & BW_F_NO_HASH);
@@ -462,10 +689,8 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     const int max_leaves = (int)std::min<uint64_t>((max_blob_len + 1023) / 1024, 1u << 30);
     // small batches scan half-size tiles: with one 128 KiB tile per wave the per-tile start
     // costs dominate (C1: 0.50 -> 0.33 ms per GiB); large ones keep the longer strips
-    // (BW_SCAN_SMALL_BYTES overrides the threshold, so the tests can run either tile size on any input)
-    const char* sb = getenv("BW_SCAN_SMALL_BYTES");
-    const uint64_t small_bytes = sb ? strtoull(sb, nullptr, 10) : SCAN_SMALL_BYTES;
-    mk.tile_shift = data_len < small_bytes ? SCAN_TILE_SHIFT - 1 : SCAN_TILE_SHIFT;
+    // (BW_OPT_SCAN_SMALL_BYTES moves the threshold, so the tests can run either tile size on any input)
+    mk.tile_shift = data_len < c->scan_small_bytes ? SCAN_TILE_SHIFT - 1 : SCAN_TILE_SHIFT;
     const uint64_t tile_bytes = 1ull << mk.tile_shift;
     const uint64_t n_tiles = ncf ? (data_len + tile_bytes - 1) / tile_bytes : 0;
 
@@ -497,27 +722,34 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     rc |= ensure(c, c->b_ghash, max_blobs * 8);
     rc |= ensure(c, c->cv, max_groups * 32);
     rc |= ensure(c, c->cv2, max_leaves > 64 ? max_groups * 32 : 16);
-    rc |= ensure(c, c->digests, max_blobs * 32);
-    rc |= ensure(c, c->is_dup, max_blobs);
-    rc |= ensure(c, c->packed, max_blobs * sizeof(bw_blob));
+    rc |= ensure(c, s.ctr, C_COUNT * 8);
+    rc |= ensure(c, s.digests, max_blobs * 32);
+    rc |= ensure(c, s.is_dup, max_blobs);
+    rc |= ensure(c, s.packed, max_blobs * sizeof(bw_blob));
     rc |= ensure(c, c->fstart, nf * 8);
     rc |= ensure(c, c->ucnt, 2 * nunits * 8);
     rc |= ensure(c, c->ubtot, 2 * (nunits / 1024 + 2) * 8);
     if (rc) return BW_ENOMEM;
-    // candidate array: 4x the expected count (2^-popcount(mask) per byte) plus slack; a batch
-    // that finds more is re-run by bw_results with the exact count (pathological inputs only)
+    // candidate array: 4x the expected count (2^-popcount(mask) per byte) plus slack.  A batch that
+    // finds more stays exact (the walkers test the bytes past the array's end, C_TRUNC) and the
+    // next batch gets the room it would have needed.
     uint64_t cand_cap = 16;
     if (ncf) {
         const int bits = __builtin_popcountll(mk.mask_pre);
         cand_cap = 4 * (data_len >> bits) + 2 * n_tiles + 4096;
         cand_cap = std::max(cand_cap, c->cand_override);
+        if (c->cand_cap_forced) cand_cap = c->cand_cap_forced;
     }
     if (int r2 = ensure(c, c->cand, cand_cap * 8)) return r2;
 
-    // ---- metadata upload through pinned staging
+    // ---- metadata upload through the slot's pinned staging
     const size_t meta_bytes = nseg * sizeof(SegDesc) + ncf * sizeof(CFileDesc) + nunits * sizeof(UnitDesc) + nf * 8;
-    if (int r3 = ensure_pinned(c, c->stage, meta_bytes + 64)) return r3;
-    uint8_t* sp = (uint8_t*)c->stage.p;
+    if (s.meta_pending) {
+        hipEventSynchronize(s.meta_done);
+        s.meta_pending = false;
+    }
+    if (int r3 = ensure_host(c, s.meta, meta_bytes + 64)) return r3;
+    uint8_t* sp = (uint8_t*)s.meta.p;
     size_t o = 0;
     auto up = [&](DevBuf& dst, const void* src, size_t bytes) -> hipError_t {
         if (!bytes) return hipSuccess;
@@ -530,9 +762,9 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     HIPCHK(c, up(c->cfiles, cfs.data(), ncf * sizeof(CFileDesc)));
     HIPCHK(c, up(c->units, units.data(), nunits * sizeof(UnitDesc)));
     HIPCHK(c, up(c->fstart, foff, nf * 8));
-    hipEventRecord(c->meta_done, c->stream);
-    c->meta_pending = true;
-    HIPCHK(c, hipMemsetAsync(c->ctr.p, 0, C_COUNT * 8, c->stream));
+    HIPCHK(c, hipEventRecord(s.meta_done, c->stream));
+    s.meta_pending = true;
+    HIPCHK(c, hipMemsetAsync(s.ctr.p, 0, C_COUNT * 8, c->stream));
 
     if (c->prof) {
         c->ev_set ^= 1;
@@ -541,13 +773,16 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     prof_mark(c, BW_STAGE_SCAN);
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash)};
-    uint64_t* ctr = P<uint64_t>(c->ctr);
+    uint64_t* ctr = P<uint64_t>(s.ctr);
     hipStream_t st = c->stream;
 
     // ---- chunking
     if (ncf) {
-        launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
-                    P<uint32_t>(c->ovf), ctr);
+        if (!launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
+                         P<uint32_t>(c->ovf), ctr)) {
+            c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
+            return BW_EINVAL;
+        }
         prof_mark(c, BW_STAGE_COMPACT);
         launch_compact(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
                        P<uint64_t>(c->tile_off), P<uint64_t>(c->cand), cand_cap, P<uint32_t>(c->ovf), ctr,
@@ -576,78 +811,179 @@ static int submit(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uin
     prof_mark(c, BW_STAGE_B3LEAF);
     if (do_hash) {
         launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint32_t>(c->cv2),
-                      P<uint8_t>(c->digests), max_leaves, c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : nullptr);
+                      P<uint8_t>(s.digests), max_leaves, c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : nullptr);
     } else {
         prof_mark(c, BW_STAGE_B3TREE);
-        HIPCHK(c, hipMemsetAsync(c->digests.p, 0, max_blobs * 32, st));
+        HIPCHK(c, hipMemsetAsync(s.digests.p, 0, max_blobs * 32, st));
     }
+    HIPCHK(c, hipEventRecord(s.input_free, st));  // no kernel of this batch reads d_data after here
     prof_mark(c, BW_STAGE_DEDUP);
     if (do_dedup) {
-        if (int r4 = dedup_device(c, P<uint8_t>(c->digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(c->is_dup)))
+        if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup)))
             return r4;
     }
     prof_mark(c, BW_STAGE_PACK);
-    launch_pack(st, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(c->digests), do_dedup ? P<uint8_t>(c->is_dup) : nullptr,
-                P<uint8_t>(c->packed), max_blobs);
+    launch_pack(st, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
+                P<uint8_t>(s.packed), max_blobs);
     prof_mark(c, BW_N_STAGES);
     if (c->prof) c->ev_pending[c->ev_set] = true;
     HIPCHK(c, hipGetLastError());
-    c->pending = true;
-    c->last_data = d_data;
-    c->last_len = data_len;
-    c->last_off.assign(foff, foff + nf);
-    c->last_flen.assign(flen, flen + nf);
-    c->last_prm = *prm;
-    c->last_max_blobs = max_blobs;
-    c->last_nfiles = nf;
-    c->last_dedup = do_dedup;
+    s.max_blobs = max_blobs;
+    s.dedup = do_dedup;
+    return BW_OK;
+}
+
+// Claim the next slot of the ring (the batch it held, if any, is dropped) and give it a ticket.
+static Slot& claim_slot(bw_ctx* c, uint64_t* ticket) {
+    const uint64_t t = c->next_ticket++;
+    Slot& s = c->slots[(t - 1) % (uint64_t)c->depth];
+    s.ticket = t;
+    c->last_ticket = t;
+    if (ticket) *ticket = t;
+    return s;
+}
+
+static const bw_params* params_or_default(const bw_params* prm, bw_params* def) {
+    if (prm) return prm;
+    bw_params_default(def);
+    return def;
+}
+
+extern "C" int bw_submit_device(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
+                                const uint64_t* flen, uint64_t nf, const bw_params* prm, uint64_t* ticket) {
+    if (!c) return BW_EINVAL;
+    if (ticket) *ticket = 0;
+    bw_params def;
+    prm = params_or_default(prm, &def);
+    Slot& s = claim_slot(c, ticket);
+    if (int rc = submit(c, s, d_data, data_len, foff, flen, nf, prm)) {
+        s.ticket = 0;
+        if (ticket) *ticket = 0;
+        return rc;
+    }
     return BW_OK;
 }
 
 extern "C" int bw_process_files_device(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
                                        const uint64_t* flen, uint64_t nf, const bw_params* prm) {
-    if (!c) return BW_EINVAL;
-    bw_params def;
-    if (!prm) {
-        bw_params_default(&def);
-        prm = &def;
+    return bw_submit_device(c, d_data, data_len, foff, flen, nf, prm, nullptr);
+}
+
+static bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: clear the sticky error
+        return false;
     }
-    return submit(c, d_data, data_len, foff, flen, nf, prm);
+    return a.type == hipMemoryTypeHost;
+}
+
+// H2D of a host batch into s.input on the copy stream (ordered after the slot's previous batch
+// stopped reading that buffer); the compute stream then waits for it.  Pinned or registered
+// memory is DMA'd directly; pageable memory is copied chunk by chunk into a ring of pinned
+// staging buffers (16 host threads per chunk) while the previous chunks are in flight.
+static int stream_in(bw_ctx* c, Slot& s, const uint8_t* data, uint64_t len) {
+    if (!c->copy) HIPCHK(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    if (int rc = ensure(c, s.input, len + 64)) return rc;
+    if (s.input_used) HIPCHK(c, hipStreamWaitEvent(c->copy, s.input_free, 0));
+    uint8_t* dst = P<uint8_t>(s.input);
+    if (len && is_pinned(data)) {
+        HIPCHK(c, hipMemcpyAsync(dst, data, len, hipMemcpyHostToDevice, c->copy));
+    } else {
+        for (uint64_t off = 0, k = 0; off < len; off += c->stage_chunk, k++) {
+            const int r = (int)(k % STAGE_RING);
+            const uint64_t n = std::min<uint64_t>(c->stage_chunk, len - off);
+            if (!c->ring_ev[r]) HIPCHK(c, hipEventCreateWithFlags(&c->ring_ev[r], hipEventDisableTiming));
+            if (c->ring_set[r]) HIPCHK(c, hipEventSynchronize(c->ring_ev[r]));
+            if (int rc = ensure_host(c, c->ring[r], c->stage_chunk)) return rc;
+            uint8_t* pin = (uint8_t*)c->ring[r].p;
+            parallel_ranges(
+                n, [&](uint64_t lo, uint64_t hi) { memcpy(pin + lo, data + off + lo, hi - lo); }, n / 16);
+            HIPCHK(c, hipMemcpyAsync(dst + off, pin, n, hipMemcpyHostToDevice, c->copy));
+            HIPCHK(c, hipEventRecord(c->ring_ev[r], c->copy));
+            c->ring_set[r] = true;
+        }
+    }
+    HIPCHK(c, hipEventRecord(s.copied, c->copy));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, s.copied, 0));
+    s.input_used = true;
+    return BW_OK;
+}
+
+extern "C" int bw_submit_host(bw_ctx* c, const uint8_t* data, uint64_t data_len, const uint64_t* foff,
+                              const uint64_t* flen, uint64_t nf, const bw_params* prm, uint64_t* ticket) {
+    if (!c || (data_len && !data)) return BW_EINVAL;
+    if (ticket) *ticket = 0;
+    bw_params def;
+    prm = params_or_default(prm, &def);
+    Masks mk;
+    if (int rc = validate_batch(c, data_len, foff, flen, nf, prm, &mk)) return rc;
+    hipSetDevice(c->device);
+    Slot& s = claim_slot(c, ticket);
+    int rc = stream_in(c, s, data, data_len);
+    if (!rc) rc = submit(c, s, P<uint8_t>(s.input), data_len, foff, flen, nf, prm);
+    if (rc) {
+        s.ticket = 0;
+        if (ticket) *ticket = 0;
+    }
+    return rc;
+}
+
+extern "C" int bw_host_register(void* p, uint64_t len) {
+    if (!p || !len) return BW_EINVAL;
+    return hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess ? BW_OK : BW_EHIP;
+}
+
+extern "C" int bw_host_unregister(void* p) {
+    if (!p) return BW_EINVAL;
+    return hipHostUnregister(p) == hipSuccess ? BW_OK : BW_EHIP;
+}
+
+// Results of the batch in slot s (waits for it).  Repeatable until the ring reuses the slot.
+static int slot_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t* n_out) {
+    hipSetDevice(c->device);
+    uint64_t ctr[C_COUNT];
+    HIPCHK(c, hipMemcpyAsync(ctr, s.ctr.p, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ctr[C_CANDTOTAL] > ctr[C_NCAND])  // exact anyway; give later batches the room they need
+        c->cand_override = std::max(c->cand_override, ctr[C_CANDTOTAL] + 1024);
+    *n_out = ctr[C_NBLOBS];
+    if (s.dedup)
+        if (int rc = check_collision(c)) return rc;
+    if (ctr[C_NBLOBS] > cap) return BW_ENOSPC;
+    if (ctr[C_NBLOBS] && out)
+        HIPCHK(c, hipMemcpy(out, s.packed.p, ctr[C_NBLOBS] * sizeof(bw_blob), hipMemcpyDeviceToHost));
+    return BW_OK;
+}
+
+extern "C" int bw_wait(bw_ctx* c, uint64_t ticket, bw_blob* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return BW_EINVAL;
+    Slot* s = slot_of(c, ticket);
+    if (!s) {
+        c->err = "ticket " + std::to_string(ticket) + " is not (or no longer) held by the context";
+        return BW_ESTATE;
+    }
+    return slot_results(c, *s, out, cap, n_out);
 }
 
 extern "C" int bw_results(bw_ctx* c, bw_blob* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return BW_EINVAL;
-    if (!c->pending) return BW_ESTATE;
-    hipSetDevice(c->device);
-    uint64_t ctr[C_COUNT];
-    HIPCHK(c, hipMemcpyAsync(ctr, c->ctr.p, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (ctr[C_CANDTOTAL] > ctr[C_NCAND]) {
-        // candidate array overflowed: the chunk lists are incomplete -> re-run with exact room.
-        // (k_assemble handed 0 blobs to the index, so the re-run sees the same index.)
-        c->cand_override = ctr[C_CANDTOTAL] + 1024;
-        std::vector<uint64_t> fo = c->last_off, fl = c->last_flen;
-        if (int rc = submit(c, c->last_data, c->last_len, fo.data(), fl.data(), fo.size(), &c->last_prm)) return rc;
-        return bw_results(c, out, cap, n_out);
-    }
-    *n_out = ctr[C_NBLOBS];
-    if (c->last_dedup)
-        if (int rc = check_collision(c)) return rc;
-    if (ctr[C_NBLOBS] > cap) return BW_ENOSPC;
-    if (ctr[C_NBLOBS] && out)
-        HIPCHK(c, hipMemcpy(out, c->packed.p, ctr[C_NBLOBS] * sizeof(bw_blob), hipMemcpyDeviceToHost));
-    return BW_OK;
+    Slot* s = slot_of(c, c->last_ticket);
+    if (!s) return BW_ESTATE;
+    return slot_results(c, *s, out, cap, n_out);
 }
 
 extern "C" int bw_batch_device_views(bw_ctx* c, uint64_t* n_blobs, const uint8_t** d_digests, uint8_t** d_is_dup) {
     if (!c) return BW_EINVAL;
-    if (!c->pending) return BW_ESTATE;
+    Slot* s = slot_of(c, c->last_ticket);
+    if (!s) return BW_ESTATE;
+    hipSetDevice(c->device);
     uint64_t n = 0;
-    HIPCHK(c, hipMemcpyAsync(&n, (uint64_t*)c->ctr.p + C_NBLOBS, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&n, (uint64_t*)s->ctr.p + C_NBLOBS, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (n_blobs) *n_blobs = n;
-    if (d_digests) *d_digests = P<uint8_t>(c->digests);
-    if (d_is_dup) *d_is_dup = P<uint8_t>(c->is_dup);
+    if (d_digests) *d_digests = P<uint8_t>(s->digests);
+    if (d_is_dup) *d_is_dup = P<uint8_t>(s->is_dup);
     return BW_OK;
 }
 
@@ -714,15 +1050,7 @@ uint8_t* bw::message_stage(bw_ctx* c, size_t bytes) {
     hipSetDevice(c->device);
     if (c->msg_stage.cap < bytes) {
         hipStreamSynchronize(c->stream);
-        if (c->msg_stage.p) hipHostFree(c->msg_stage.p);
-        c->msg_stage.p = nullptr;
-        c->msg_stage.cap = 0;
-        const size_t want = bytes + bytes / 4 + 4096;
-        if (hipHostMalloc(&c->msg_stage.p, want, hipHostMallocDefault) != hipSuccess) {
-            c->err = "hipHostMalloc failed";
-            return nullptr;
-        }
-        c->msg_stage.cap = want;
+        if (ensure_host(c, c->msg_stage, bytes)) return nullptr;
     }
     return (uint8_t*)c->msg_stage.p;
 }
@@ -736,11 +1064,14 @@ int bw::hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const ui
     bw_params_default(&p);
     p.flags = dedup ? 0 : BW_F_NO_DEDUP;
     p.small_file_threshold = ~0ull;  // every message is one whole blob, in the order given
-    if (int rc = submit(c, P<uint8_t>(c->data), total, offs, lens, n, &p)) return rc;
-    HIPCHK(c, hipMemcpyAsync(hashes, c->digests.p, n * 32, hipMemcpyDeviceToHost, c->stream));
-    if (dedup) HIPCHK(c, hipMemcpyAsync(dup, c->is_dup.p, n, hipMemcpyDeviceToHost, c->stream));
+    Slot& s = claim_slot(c, nullptr);
+    if (int rc = submit(c, s, P<uint8_t>(c->data), total, offs, lens, n, &p)) {
+        s.ticket = 0;
+        return rc;
+    }
+    HIPCHK(c, hipMemcpyAsync(hashes, s.digests.p, n * 32, hipMemcpyDeviceToHost, c->stream));
+    if (dedup) HIPCHK(c, hipMemcpyAsync(dup, s.is_dup.p, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->pending = false;
     return dedup ? check_collision(c) : BW_OK;
 }
 
@@ -824,18 +1155,7 @@ static int seal_submit(bw_ctx* c, bool dec, const uint8_t* prk, const uint8_t* d
         c->seal_pending = false;
     }
     const size_t bytes = n * sizeof(SealItem);
-    if (c->seal_stage.cap < bytes) {
-        if (c->seal_stage.p) hipHostFree(c->seal_stage.p);
-    if (c->msg_stage.p) hipHostFree(c->msg_stage.p);
-        c->seal_stage.p = nullptr;
-        c->seal_stage.cap = 0;
-        const size_t want = bytes + bytes / 4 + 4096;
-        if (hipHostMalloc(&c->seal_stage.p, want, hipHostMallocDefault) != hipSuccess) {
-            c->err = "hipHostMalloc failed";
-            return BW_ENOMEM;
-        }
-        c->seal_stage.cap = want;
-    }
+    if (int rc = ensure_host(c, c->seal_stage, bytes)) return rc;
     SealItem* it = (SealItem*)c->seal_stage.p;
     std::vector<uint64_t> piece0(n);
     uint64_t pieces = 0;
@@ -1005,7 +1325,13 @@ static int pack_submit(bw_ctx* c, const uint8_t* prk, const uint8_t* d_src, cons
         }
     }
     for (uint64_t i = 0; i < n; i++)
-        if (kinds[i] > BW_BLOB_TREE || ((flags & BW_PACK_ZSTD_STORE) && src_len[i] > (1ull << 31))) return BW_EINVAL;
+        if (kinds[i] > BW_BLOB_TREE) return BW_EINVAL;
+        else if ((flags & BW_PACK_ZSTD_STORE) && src_len[i] > BW_BLOB_MAX_UNCOMPRESSED_SIZE) {
+            // add_blob rejects it (PackfileError::BlobTooLarge, pack.rs:32-34) and the reader
+            // decompresses into a 3 MiB buffer (unpack.rs:67)
+            c->err = "blob " + std::to_string(i) + " exceeds BLOB_MAX_UNCOMPRESSED_SIZE";
+            return BW_EINVAL;
+        }
     if (!n) return BW_OK;
     if (!c->pk_done) HIPCHK(c, hipEventCreateWithFlags(&c->pk_done, hipEventDisableTiming));
     if (c->pk_pending) {

@@ -278,13 +278,16 @@ static void launch_scan_t(hipStream_t st, const uint8_t* data, uint64_t n_bytes,
                        n_tiles, mk, tile_count, tile_slots, ovf, ctr);
 }
 
-void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
+bool launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                  uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf, uint64_t* ctr) {
-    if (!n_tiles) return;
+    if (!n_tiles) return true;
     if (64ull * SCAN_STRIP == 1ull << mk.tile_shift)
         launch_scan_t<SCAN_BLOCK, SCAN_STRIP>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
     else if (64ull * SCAN_STRIP_SMALL == 1ull << mk.tile_shift)
         launch_scan_t<SCAN_BLOCK, SCAN_STRIP_SMALL>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
+    else
+        return false;  // a tile size no kernel was built for: the caller reports BW_EINVAL
+    return true;
 }
 
 // ======================================================================== block scan helpers
@@ -369,17 +372,24 @@ __global__ __launch_bounds__(BLK) void k_tile_top(uint64_t* __restrict__ btot, u
         off[n_tiles] = total;
         ctr[C_NCAND] = total < cap ? total : cap;
         ctr[C_CANDTOTAL] = total;
+        ctr[C_TRUNC] = BW_NONE;  // lowered by k_compact when the array cannot hold every candidate
     }
 }
 
+// A tile whose candidates do not all fit below `cap` marks the candidate array as incomplete from
+// its first byte on (C_TRUNC = the lowest such tile start); the boundary walkers then test the
+// bytes at and beyond that position themselves (walk_next), so an undersized array never changes
+// a boundary and a batch never has to be re-run (which would break the dedup order of a shared
+// index).
 __global__ void k_compact(const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ slots,
                           uint64_t* __restrict__ off, const uint64_t* __restrict__ bbase, uint64_t n_tiles,
-                          uint64_t* __restrict__ cand, uint64_t cap) {
+                          uint64_t* __restrict__ cand, uint64_t cap, uint32_t tile_shift, uint64_t* ctr) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
     const uint64_t o = off[t] + bbase[t / (4 * TS_BLOCK)];
     off[t] = o;  // final offset: the walkers start their candidate cursor here
     const uint32_t c = cnt[t];
+    if (o + (c & ~TILE_OVF) > cap) atomicMin((unsigned long long*)&ctr[C_TRUNC], (unsigned long long)(t << tile_shift));
     if (!(c & TILE_OVF)) {  // overflowed tiles are written by k_rescan<true>
         for (uint32_t i = 0; i < c; i++)
             if (o + i < cap) cand[o + i] = slots[t * SCAN_CAP + i];
@@ -442,7 +452,7 @@ void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint6
     hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, tile_count, n_tiles, tile_off, btot);
     hipLaunchKernelGGL(k_tile_top, dim3(1), dim3(BLK), 0, st, btot, nb, n_tiles, tile_off, cand_cap, ctr);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count, tile_slots,
-                       tile_off, btot, n_tiles, cand, cand_cap);
+                       tile_off, btot, n_tiles, cand, cand_cap, mk.tile_shift, ctr);
     hipLaunchKernelGGL(k_rescan<true>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
                        cand, cand_cap, tile_count, ctr);
 }
@@ -455,7 +465,29 @@ struct Walker {
     uint64_t ncand;
     const uint64_t* lgear;  // plain 256-entry table in LDS
     Masks mk;
+    uint64_t trunc;         // ctr[C_TRUNC]: candidates are complete only below this position
 };
+
+// First position p in [a, hi) whose windowed gear hash passes its region's mask (mask_s below
+// c2a, mask_l from c2a on), or BW_NONE; the whole wave tests 64 positions per step.  Used where
+// the candidate array is incomplete (p >= trunc).  Requires a >= chunk start + s0 + 47 (so the
+// 64-byte window is inside the hashed range) and a >= 64.
+__device__ uint64_t direct_scan(const Walker& W, uint64_t a, uint64_t hi, uint64_t c2a) {
+    const int lane = bw_lane();
+    // h_{a-1} from the 64 bytes before a (only its low 48 bits matter)
+    uint64_t carry = bw_shfl64(bw_gear_scan(W.lgear[W.data[a - 64 + lane]]), 63);
+    for (uint64_t b = a; b < hi; b += 64) {
+        const uint64_t p = b + (uint64_t)lane;
+        const bool valid = p < hi;
+        const uint64_t g = valid ? W.lgear[W.data[p]] : 0;
+        const uint64_t h = bw_gear_scan(g) + ((carry << lane) << 1);
+        const uint64_t mask = p < c2a ? W.mk.mask_s : W.mk.mask_l;
+        const uint64_t hb = __ballot(valid && (h & mask) == 0);
+        if (hb) return b + (uint64_t)__builtin_ctzll(hb);
+        carry = bw_shfl64(h, 63);
+    }
+    return BW_NONE;
+}
 
 // One step of fastcdc::v2020::cut for the chunk starting at s in a file ending at fe, executed by a
 // whole wavefront (all 64 lanes, wave-uniform control flow).  Returns the next chunk start.
@@ -479,26 +511,33 @@ __device__ uint64_t walk_next(const Walker& W, uint64_t s, uint64_t fe, uint64_t
     const uint64_t hb = __ballot(valid && (h & mask) == 0);
     if (hb) return s + s0 + (uint64_t)__builtin_ctzll(hb);
 
-    // Body: first candidate in [s+s0+47, s+r2) that passes its region's mask.
+    // Body: first candidate in [s+s0+47, s+r2) that passes its region's mask.  The candidate array
+    // answers for positions below W.trunc; from there on the bytes are tested directly.
     const uint64_t lo = s + s0 + 47, hi = s + r2, c2a = s + c2;
+    const uint64_t hc = hi < W.trunc ? hi : W.trunc;
     for (;;) {
         const uint64_t idx = cptr + (uint64_t)lane;
         const uint64_t c = idx < W.ncand ? W.cand[idx] : BW_NONE;
         const uint64_t pos = c == BW_NONE ? BW_NONE : BW_CAND_POS(c);
         const uint64_t below = __ballot(pos < lo);
-        const bool match = pos >= lo && pos < hi && ((pos < c2a) ? (c & BW_CAND_S) != 0 : (c & BW_CAND_L) != 0);
+        const bool match = pos >= lo && pos < hc && ((pos < c2a) ? (c & BW_CAND_S) != 0 : (c & BW_CAND_L) != 0);
         const uint64_t mb = __ballot(match);
         if (mb) {
             const uint64_t cut = bw_shfl64(pos, __builtin_ctzll(mb));
             cptr += (uint64_t)__popcll(below);
             return cut;
         }
-        if (__ballot(pos >= hi) != 0) {  // window exhausted (also covers the array end)
+        if (__ballot(pos >= hc) != 0) {  // window exhausted (also covers the array end)
             cptr += (uint64_t)__popcll(below);
-            return s + remaining;
+            break;
         }
         cptr += 64;
     }
+    if (hc < hi) {
+        const uint64_t cut = direct_scan(W, lo > hc ? lo : hc, hi, c2a);
+        if (cut != BW_NONE) return cut;
+    }
+    return s + remaining;
 }
 
 __device__ __forceinline__ void load_lgear(uint64_t* lg) {
@@ -519,6 +558,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_chains(Walker W, const
     load_lgear(lg);
     W.lgear = lg;
     W.ncand = ctr[C_NCAND];
+    W.trunc = ctr[C_TRUNC];
     const uint64_t j = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
     if (j >= nseg) return;
     const SegDesc sd = segs[j];
@@ -547,6 +587,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_extend(Walker W, const
     load_lgear(lg);
     W.lgear = lg;
     W.ncand = ctr[C_NCAND];
+    W.trunc = ctr[C_TRUNC];
     const uint64_t j = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
     if (j >= nseg) return;
     const int lane = bw_lane();
@@ -659,6 +700,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_fallback(Walker W, con
     load_lgear(lg);
     W.lgear = lg;
     W.ncand = ctr[C_NCAND];
+    W.trunc = ctr[C_TRUNC];
     const uint64_t f = (uint64_t)blockIdx.x * WAVES_PER_BLOCK + threadIdx.x / 64;
     if (f >= ncf || !cf_invalid[f]) return;
     const CFileDesc cf = cfiles[f];
@@ -823,7 +865,7 @@ __global__ __launch_bounds__(BLK) void k_unit_top(uint64_t* __restrict__ bt_b, u
     if (threadIdx.x == 0) {
         ctr[C_NBLOBS] = totb;
         ctr[C_NGROUPS] = totg;
-        ctr[C_DEDUPN] = ctr[C_CANDTOTAL] > ctr[C_NCAND] ? 0 : totb;  // incomplete lists never reach the index
+        ctr[C_DEDUPN] = totb;
     }
 }
 

@@ -39,10 +39,14 @@ enum Ctr : int {
     C_COLLIDE = 5,   // 64-bit key collision seen by the index
     C_NINVALID = 6,  // files that needed the serial boundary walker
     C_NUNIQUE = 7,   // distinct digests in the index
-    C_CANDTOTAL = 8, // gear candidates found (> C_NCAND: capacity too small, batch re-run)
-    C_DEDUPN = 9,    // blobs handed to the index (0 when the batch must be re-run)
+    C_CANDTOTAL = 8, // gear candidates found (> C_NCAND: the array was too small, see C_TRUNC)
+    C_DEDUPN = 9,    // blobs handed to the index
+    C_TRUNC = 10,    // first byte position whose candidates did not fit the array (BW_NONE: all fit);
+                     // the walkers scan the bytes themselves from there on
     C_COUNT = 16
 };
+static_assert(SCAN_STRIP_SMALL % (4 * SCAN_STEP) == 0, "k_scan consumes four 64-byte steps per iteration");
+static_assert(SCAN_STRIP % (4 * SCAN_STEP) == 0, "k_scan consumes four 64-byte steps per iteration");
 
 struct Masks {
     uint32_t min, avg, max, s0;  // s0 = 2 * (min / 2): first position the crate hashes
@@ -86,7 +90,8 @@ struct BlobArrays {
 };
 
 // ------------------------------------------------------------------ launchers (bw_cdc.hip)
-void launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
+// returns false (nothing launched) when mk.tile_shift names no compiled tile size
+bool launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
                  const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf_list,
                  uint64_t* ctr);
 void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,

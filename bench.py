@@ -88,7 +88,8 @@ def make_workload(name, gib, rank, dev, n_files):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: about 3 s of work for the workload)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--gib", type=float, default=None,
@@ -113,6 +114,8 @@ def main():
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = {"c1": 3000, "c2": 320, "c3": 80, "c4": 200, "c5": 5}[args.workload]
     if args.gib is None:
         args.gib = {"c1": 1.0, "c2": 16.0, "c3": 4.0, "c4": 0.0, "c5": 4.0}[args.workload]
     if args.cpu_sample_gib is None:
@@ -124,7 +127,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from backuwup_amd import Context, make_params
+    from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
     from backuwup_amd._lib import BW_F_NO_DEDUP, STAGES
 
     rank = int(os.environ.get("RANK", 0))
@@ -146,40 +149,47 @@ def main():
     processed = int(np.sum(np.asarray(file_len, dtype=np.uint64)))  # file bytes per step (C4 copies alias)
     log("rank %d: %s -- generated in %.1f s" % (rank, desc, time.time() - t0))
 
-    # N > 1: two contexts, so batch k's chunk+hash runs while batch k-1's digests are exchanged
-    nctx = 2 if (args.host_stream or multi) else max(1, args.streams)
+    # One backup session: every batch is gated by ONE index (bw_index) shared by the contexts.
+    # Device-resident: consecutive batches alternate between two contexts on two streams (one
+    # batch's HBM-bound scan beside the other's VALU-bound BLAKE3), the index event chain keeps
+    # their dedup in submission order, and batch k's results are read after batch k+1 is queued.
+    # Host-streamed: one context; its copy stream brings batch k+1 from pinned host memory while
+    # batch k computes (bw_submit_host).  N > 1: the local pass skips the index; each batch's
+    # digests go through the RCCL exchange to their owner's index while the next batch computes.
+    nctx = 1 if args.host_stream and not multi else (2 if multi else max(1, args.streams))
+    index = Index(local)
     ctxs, streams = [], []
     for k in range(nctx):
         c = Context(local)
         st = torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)
         c.set_stream(st.cuda_stream)
+        c.attach_index(index)
         ctxs.append(c)
         streams.append(st)
     ctx = ctxs[0]
     flags = BW_F_NO_DEDUP if multi else 0
     params = make_params(flags=flags)
-    index_hint = 2 * (processed // (256 << 10)) + len(file_len) + 1024
+    max_blobs = sum(int(x) // (256 << 10) + 2 if int(x) > (1 << 20) else 1 for x in file_len)
+    total_batches = args.warmup + args.steps + 4 + (3 if nctx > 1 else 0)
+    # the host's bound of the log grows by max_blobs per batch until a result read tightens it
+    index_hint = total_batches * max_blobs + 1024
     owner_bits = world.bit_length() - 1
     assert world == 1 << owner_bits, "world size must be a power of two (digest-prefix owners)"
 
     from backuwup_amd.sharded import DeviceShardOps, exchange_dedup
 
-    # host-streamed mode: the batch lives in pinned host memory; batch k+1's copy (copy stream)
-    # overlaps batch k's processing; the two contexts alternate between two HBM buffers
     host = None
     if args.host_stream:
+        # the batch lives in pinned host memory; the library copies it in on its copy stream
         host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
         host.copy_(data)
-        bufs = [data, torch.empty_like(data)]
-        copy_stream = torch.cuda.Stream(dev)
-        copied = [torch.cuda.Event() for _ in range(2)]
-        done = [torch.cuda.Event() for _ in range(2)]
-        for e in done:
-            e.record(torch.cuda.current_stream(dev))
+        torch.cuda.synchronize()
 
     step_no = [0]
     host_ms = [0.0]  # host time inside the library's submit calls (metadata build + upload)
+    inflight = []  # (context, ticket) of batches whose results are not read yet
     pending = [None]  # N > 1: the context whose batch still awaits its digest exchange
+    out_buf = np.zeros(max_blobs + 1, dtype=BLOB_DTYPE)
 
     def exchange(k):
         # digest all-to-all by owner = digest[0] >> (8 - log2 N); verdicts come back (RCCL on the
@@ -193,31 +203,32 @@ def main():
         if pending[0] is not None:
             exchange(pending[0])
             pending[0] = None
+        while inflight:
+            c, t = inflight.pop(0)
+            c.wait(t, out=out_buf)
 
     def step():
         k = step_no[0] % len(ctxs)
         step_no[0] += 1
         c = ctxs[k]
-        src = data
-        if host is not None:
-            b = k
-            copy_stream.wait_event(done[b])
-            with torch.cuda.stream(copy_stream):
-                bufs[b].copy_(host, non_blocking=True)
-                copied[b].record(copy_stream)
-            streams[k].wait_event(copied[b])
-            src = bufs[b]
         with torch.cuda.stream(streams[k]):
             th = time.perf_counter()
-            c.index_reset(index_hint)
-            c.submit_device(src.data_ptr(), n, file_off, file_len, params)
-            host_ms[0] += (time.perf_counter() - th) * 1e3
             if host is not None:
-                done[k].record(streams[k])
+                t = c.submit_host(host.data_ptr(), file_off, file_len, params, data_len=n)
+            else:
+                t = c.submit_device(data.data_ptr(), n, file_off, file_len, params)
+            host_ms[0] += (time.perf_counter() - th) * 1e3
         if multi:
-            drain()  # the previous batch's exchange, while this batch computes
+            if pending[0] is not None:
+                exchange(pending[0])  # the previous batch's exchange, while this batch computes
             pending[0] = k
+        else:
+            inflight.append((c, t))
+            if len(inflight) > 1:  # two batches in flight: read batch k-1 while batch k runs
+                c0, t0 = inflight.pop(0)
+                c0.wait(t0, out=out_buf)
 
+    ctx.index_reset(index_hint)
     for _ in range(args.warmup):
         step()
     drain()
@@ -248,6 +259,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    ctx.index_check()  # no 64-bit key collision anywhere in the session
     stage_ms, nbatch = ctx.profile_read()
     per = {s: stage_ms[s] / max(nbatch, 1) for s in STAGES}
     iso = None
@@ -257,7 +269,6 @@ def main():
         ctx.profile_enable(True)
         for _ in range(3):
             with torch.cuda.stream(streams[0]):
-                ctx.index_reset(index_hint)
                 ctx.submit_device(data.data_ptr(), n, file_off, file_len, params)
             torch.cuda.synchronize()
         iso_ms, iso_n = ctx.profile_read()
@@ -338,7 +349,8 @@ def main():
                            "bytes_per_gpu": processed, "blobs_per_gpu": int(len(res)),
                            "files_per_gpu": len(file_len),
                            "parallelism": "dp%d (files sharded, index by digest prefix)" % world,
-                           "batches_in_flight": len(ctxs)},
+                           "batches_in_flight": 2 if (len(ctxs) > 1 or host is not None) else 1,
+                           "index": "one shared index for every batch (a single backup session)"},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": check}
         if trees:
             line["file_trees"] = trees

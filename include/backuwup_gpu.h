@@ -19,9 +19,9 @@
  * unwinds across the boundary.  Where the fastcdc crate panics on an assert (parameter ranges)
  * this returns BW_EINVAL.  Output arrays are caller-owned; when one is too small BW_ENOSPC is
  * returned and *n_out holds the required count.  Device buffers, streams and the dedup table
- * are owned by the opaque bw_ctx.  A context is not thread-safe: the reference serializes
- * index access under the packer mutex (packfile/mod.rs:77); callers hashing from several
- * threads use one context per thread.
+ * are owned by the opaque bw_ctx.  A context is not thread-safe: callers hashing from several
+ * threads use one context per thread, all attached to one shared bw_index (the reference
+ * serializes index access under the packer mutex, packfile/mod.rs:77; so does bw_index).
  *
  * Scalars: "device pointer" arguments are HIP device addresses (e.g. from hipMalloc or a
  * torch tensor's data_ptr()), 16-byte aligned; everything else is host memory.
@@ -130,22 +130,70 @@ int bw_index_check_insert(bw_ctx* ctx, const uint8_t* digests, uint64_t n, uint8
 /* number of distinct digests currently in the index */
 int bw_index_size(bw_ctx* ctx, uint64_t* n);
 
+/* Any index error is sticky: BW_ECOLLISION if two distinct digests sharing a 64-bit key were
+ * ever seen since the last reset (synchronizes; the device-side gate below does not check). */
+int bw_index_check(bw_ctx* ctx);
+
+/* ---- one index shared by several contexts (one backup session, several batches in flight) ----
+ * The reference keeps one BlobIndex behind the packer mutex (packfile/mod.rs:77, blob_index.rs:
+ * 44-57) and every task of a backup gates against it.  A context owns a private index; attached
+ * to a shared one, every index operation of every attached context (reset, seed, gate of a batch,
+ * check_insert) is ordered on the GPU after the previous one, in the order the host issued them
+ * (an event chain across the contexts' streams), so the batches of a session are gated in
+ * submission order whichever stream runs them.  Index calls through different contexts may come
+ * from different threads; each context itself stays single-threaded. */
+typedef struct bw_index bw_index;
+int bw_index_create(int device, bw_index** out);
+/* Drops the caller's reference; the index lives on while contexts are attached to it. */
+void bw_index_destroy(bw_index* index);
+/* Gate this context's batches through `index` (NULL: back to the context's private index).
+ * Waits for the context's pending work first. */
+int bw_attach_index(bw_ctx* ctx, bw_index* index);
+
+/* ---- context options ---- */
+enum {
+    BW_OPT_DEPTH = 1,            /* batches a context keeps addressable (result slots), 1..8; default 2 */
+    BW_OPT_SCAN_SMALL_BYTES = 2, /* batches below this many bytes scan half-size tiles (default 4 GiB) */
+    BW_OPT_CAND_CAP = 3,         /* test hook: fixed candidate array capacity (0 = sized per batch)  */
+    BW_OPT_STAGE_CHUNK = 4       /* pinned staging chunk for pageable bw_submit_host input (64 MiB)  */
+};
+int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
+
 /* Whole front end for a batch of files stored back to back in a host buffer: chunk -> hash
  * -> dedup; synchronous; results in canonical order. */
 int bw_process_files(bw_ctx* ctx, const uint8_t* data, uint64_t data_len,
                      const uint64_t* file_off, const uint64_t* file_len, uint64_t n_files,
                      const bw_params* params, bw_blob* out, uint64_t cap, uint64_t* n_out);
 
-/* Same with the bytes already resident in HBM (d_data = device pointer, 16-byte aligned).
- * File tables are host arrays.  Asynchronous on the context stream: nothing is copied back
- * until bw_results(). */
+/* ---- pipelined batches ----
+ * A context holds the results of its last BW_OPT_DEPTH batches, each addressed by the ticket its
+ * submit returned; submitting into a full ring drops the oldest batch (its ticket then gives
+ * BW_ESTATE).  Batches of one context run one after another on its stream; batch k+1 can be
+ * queued before batch k's results are read.  File tables are host arrays, copied at submit. */
+/* Bytes already resident in HBM (d_data = device pointer, 16-byte aligned).  Asynchronous. */
+int bw_submit_device(bw_ctx* ctx, const uint8_t* d_data, uint64_t data_len, const uint64_t* file_off,
+                     const uint64_t* file_len, uint64_t n_files, const bw_params* params, uint64_t* ticket);
+/* Bytes in host memory (the mmap'd files of dir_packer.rs:247-266, gathered back to back).  The
+ * batch is copied to HBM on the context's copy stream while earlier batches compute: pinned or
+ * bw_host_register'ed memory by DMA straight from `data`; pageable memory through a ring of
+ * pinned staging chunks (the call returns once every byte is staged).  `data` must stay
+ * unchanged until the call returns (pageable) or until bw_wait(ticket) returns (pinned). */
+int bw_submit_host(bw_ctx* ctx, const uint8_t* data, uint64_t data_len, const uint64_t* file_off,
+                   const uint64_t* file_len, uint64_t n_files, const bw_params* params, uint64_t* ticket);
+/* Wait for batch `ticket` and copy its blobs out (repeatable while the ticket is held). */
+int bw_wait(bw_ctx* ctx, uint64_t ticket, bw_blob* out, uint64_t cap, uint64_t* n_out);
+/* Page-lock a host range (e.g. an mmap'd file) so bw_submit_host DMAs it without staging. */
+int bw_host_register(void* ptr, uint64_t len);
+int bw_host_unregister(void* ptr);
+
+/* bw_submit_device without a ticket (results via bw_results). */
 int bw_process_files_device(bw_ctx* ctx, const uint8_t* d_data, uint64_t data_len,
                             const uint64_t* file_off, const uint64_t* file_len, uint64_t n_files,
                             const bw_params* params);
-/* Wait for the last submitted batch and copy its blobs out. */
+/* Wait for the most recently submitted batch and copy its blobs out. */
 int bw_results(bw_ctx* ctx, bw_blob* out, uint64_t cap, uint64_t* n_out);
-/* Device views of the last batch (valid until the next submit): n blobs (synchronizes),
- * digests (n x 32 B, canonical order) and is_dup bytes. */
+/* Device views of the most recent batch (valid until the ring reuses its slot): n blobs
+ * (synchronizes), digests (n x 32 B, canonical order) and is_dup bytes. */
 int bw_batch_device_views(bw_ctx* ctx, uint64_t* n_blobs, const uint8_t** d_digests,
                           uint8_t** d_is_dup);
 

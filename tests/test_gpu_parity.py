@@ -286,13 +286,21 @@ def _dense_input():
     return data
 
 
-@pytest.mark.parametrize("small_bytes", ["0", "18446744073709551615"])
-def test_scan_tile_sizes(ctx, oracle, monkeypatch, small_bytes):
-    """Batches below 4 GiB scan half-size tiles (bw_capi.hip submit): force each tile size on the
-    same inputs -- ragged ends, the candidate-dense overflow/rescan path, many small-parameter
-    files and a multi-file corpus -- and compare with the oracle."""
+@pytest.mark.parametrize("small_bytes", [0, 2**64 - 1])
+def test_scan_tile_sizes(oracle, small_bytes):
+    """Batches below 4 GiB scan half-size tiles (bw_capi.hip submit): force each tile size
+    (BW_OPT_SCAN_SMALL_BYTES) on the same inputs -- ragged ends, the candidate-dense
+    overflow/rescan path, many small-parameter files and a multi-file corpus -- and compare with
+    the oracle."""
+    from backuwup_amd import Context
+    from backuwup_amd._lib import BW_OPT_SCAN_SMALL_BYTES
+    with Context(0) as ctx:
+        ctx.set_option(BW_OPT_SCAN_SMALL_BYTES, small_bytes)
+        _scan_tile_sizes(ctx, oracle)
+
+
+def _scan_tile_sizes(ctx, oracle):
     from backuwup_amd.synth import tree_corpus
-    monkeypatch.setenv("BW_SCAN_SMALL_BYTES", small_bytes)
     for n, p in [(1, SMALL), (64 * 1024 + 1, SMALL), ((3 << 20) + 12345, MID), ((40 << 20) + 7, BK)]:
         data = splitmix_bytes(n, n)
         assert ctx.fastcdc_chunks(data, *p) == chunks_oracle(oracle, data, p), n

@@ -1,0 +1,272 @@
+"""Pipelined batches on the GPU, all through the C ABI and compared bit for bit with the oracle:
+
+  * tickets: several batches queued on one context before any is read (ring of result slots)
+  * bw_submit_host (BASELINE C5): batches copied from pinned host memory on
+    the copy stream while the previous batch computes; pageable memory through pinned staging
+  * one index shared by two contexts on two streams: one backup session with batches in flight,
+    gated in submission order (BlobIndex behind the packer mutex, packfile/mod.rs:77,
+    blob_index.rs:130-148)
+  * an undersized candidate array: the walkers test the bytes past its end, no re-run
+  * index errors of the device-side gate, and the ADVICE r1 staging regression
+The dedup oracle over several batches is one oracle.Index fed the batches in order: the canonical
+order of a session is batch order, then file order, then chunk offset.
+"""
+import numpy as np
+import pytest
+
+from backuwup_amd import Context, Index, make_params, make_tree
+from backuwup_amd._lib import (BW_ECOLLISION, BW_ESTATE, BW_F_NO_DEDUP, BW_OPT_CAND_CAP, BW_OPT_DEPTH,
+                               BW_OPT_STAGE_CHUNK, BwError)
+from backuwup_amd.synth import small_files, splitmix_bytes, tree_corpus, vm_image_variants
+
+pytestmark = pytest.mark.gpu
+
+BK = (262144, 1048576, 3145728)
+SMALL = (64, 256, 1024)
+MID = (4096, 16384, 65536)
+
+
+def blobs_equal(a, b, what=""):
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    for f in ("file", "offset", "length", "gear_hash", "is_dup"):
+        assert np.array_equal(a[f], b[f]), (what, f)
+    assert np.array_equal(a["digest"], b["digest"]), what
+
+
+def oracle_session(oracle, batches, seed_digests=b"", params=BK):
+    """The oracle over consecutive batches gated by one index."""
+    ix = oracle.Index(seed_digests)
+    return [oracle.process_files(d, o, l, *params, index=ix, threads=8) for d, o, l in batches]
+
+
+def _slices(data, offs, lens, bounds):
+    """Batches of files [a, b) as (bytes, file_off relative to the batch, file_len)."""
+    out = []
+    for a, b in bounds:
+        lo, hi = int(offs[a]), int(offs[b - 1] + lens[b - 1])
+        out.append((np.ascontiguousarray(data[lo:hi]), (offs[a:b] - np.uint64(lo)).astype(np.uint64),
+                    lens[a:b].astype(np.uint64)))
+    return out
+
+
+def test_tickets_ring(oracle):
+    import torch
+    data, offs, lens = small_files(4000, seed=31)
+    batches = _slices(data, offs, lens, [(0, 1000), (1000, 2000), (2000, 3000), (3000, 4000)])
+    want = oracle_session(oracle, batches)
+    devs = [torch.from_numpy(d).cuda() for d, _, _ in batches]
+    torch.cuda.synchronize()
+    with Context(0) as c:
+        c.set_option(BW_OPT_DEPTH, 3)
+        c.index_reset()
+        tickets = [c.submit_device(t.data_ptr(), d.size, o, l) for t, (d, o, l) in zip(devs, batches)]
+        assert tickets == sorted(tickets) and len(set(tickets)) == 4
+        with pytest.raises(BwError) as e:  # the ring holds 3: the first batch was dropped
+            c.wait(tickets[0])
+        assert e.value.rc == BW_ESTATE
+        for k in (3, 1, 2, 3):  # any order, repeatable
+            blobs_equal(c.wait(tickets[k]), want[k], k)
+        blobs_equal(c.results(), want[3])  # bw_results = the most recent batch
+        with pytest.raises(BwError):
+            c.wait(tickets[3] + 1)
+
+
+def test_shared_index_two_contexts_six_batches(oracle):
+    """One session, two contexts on two streams, one index: six batches of C1 (tree corpus) and C4
+    (small files) data with duplicates across batches and contexts, submitted back to back (batch
+    k+1 queued before batch k is read); verdicts equal the oracle over the concatenated batches."""
+    import torch
+    t_data, t_offs, t_lens = tree_corpus(48 << 20, seed=77, max_file=6 << 20)
+    s_data, s_offs, s_lens = small_files(3000, seed=78)
+    nt, ns = len(t_lens), len(s_lens)
+    b = _slices(t_data, t_offs, t_lens, [(0, nt // 2), (nt // 2, nt)]) + \
+        _slices(s_data, s_offs, s_lens, [(0, ns // 2), (ns // 2, ns)])
+    batches = [b[0], b[2], b[1], b[3], b[2], b[0]]  # the last two repeat batches first run by the other context
+    seed = b"".join(sorted(bytes(x) for x in oracle.process_files(*b[3])["digest"][::5]))
+    want = oracle_session(oracle, batches, seed)
+    devs = [torch.from_numpy(d).cuda() for d, _, _ in batches]
+    torch.cuda.synchronize()
+    ix = Index(0)
+    ca, cb = Context(0), Context(0)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        ca.set_stream(sa.cuda_stream)
+        cb.set_stream(sb.cuda_stream)
+        ca.attach_index(ix)
+        cb.attach_index(ix)
+        ca.index_reset(1 << 16)
+        cb.index_seed(np.frombuffer(seed, dtype=np.uint8).reshape(-1, 32))
+        got, pending = [None] * len(batches), []
+        for k, (t, (d, o, l)) in enumerate(zip(devs, batches)):
+            c = (ca, cb)[k % 2]
+            pending.append((k, c, c.submit_device(t.data_ptr(), d.size, o, l)))
+            if len(pending) > 1:
+                j, cj, tj = pending.pop(0)
+                got[j] = cj.wait(tj)
+        for j, cj, tj in pending:
+            got[j] = cj.wait(tj)
+        for k in range(len(batches)):
+            blobs_equal(got[k], want[k], k)
+        assert got[4]["is_dup"].all() and got[5]["is_dup"].all()
+        uniq = {bytes(x) for w in want for x in w["digest"]} | {seed[i:i + 32] for i in range(0, len(seed), 32)}
+        assert ca.index_size() == cb.index_size() == len(uniq)
+        ca.index_check()
+    finally:
+        ca.close()
+        cb.close()
+        ix.close()
+
+
+def test_submit_host_c5_shaped(oracle):
+    """C5's layout at a size the oracle covers: one VM-image family (64 MiB base + 15 variants),
+    files 0-7 on rank 2f and 8-15 on rank 2f+1; here both ranks' files go through one context as
+    four batches from pinned host memory, each queued while the previous one computes.  Then the
+    same batches from pageable memory through small, odd-sized staging chunks."""
+    import torch
+    # C3's edit density per byte would touch nearly every chunk of a 64 MiB image: fewer edits
+    data, offs, lens = vm_image_variants(64 << 20, 16, seed=5, n_indels=4, n_overwrites=2)
+    batches = _slices(data, offs, lens, [(0, 4), (4, 8), (8, 12), (12, 16)])
+    want = oracle_session(oracle, batches)
+    assert sum(int(w["is_dup"].sum()) for w in want) > 0.5 * sum(len(w) for w in want)
+    pinned = []
+    for d, _, _ in batches:
+        t = torch.empty(d.size, dtype=torch.uint8, pin_memory=True)
+        t.numpy()[:] = d
+        pinned.append(t)
+    with Context(0) as c:
+        c.index_reset(1 << 14)
+        tickets = [c.submit_host(t.data_ptr(), o, l, data_len=d.size) for t, (d, o, l) in zip(pinned[:2], batches)]
+        got = [c.wait(tickets[0])]
+        tickets.append(c.submit_host(pinned[2].data_ptr(), batches[2][1], batches[2][2], data_len=batches[2][0].size))
+        got.append(c.wait(tickets[1]))
+        tickets.append(c.submit_host(pinned[3].data_ptr(), batches[3][1], batches[3][2], data_len=batches[3][0].size))
+        got += [c.wait(tickets[2]), c.wait(tickets[3])]
+        for k in range(4):
+            blobs_equal(got[k], want[k], ("pinned", k))
+    with Context(0) as c:
+        c.set_option(BW_OPT_STAGE_CHUNK, (3 << 20) + 4097)
+        c.index_reset(1 << 14)
+        tickets = [c.submit_host(d, o, l) for d, o, l in batches]
+        for k, t in enumerate(tickets[-2:], start=2):
+            blobs_equal(c.wait(t), want[k], ("pageable", k))
+
+
+def test_submit_host_registered_and_small_params(oracle):
+    """A page-locked (bw_host_register) numpy buffer is DMA'd in place; small parameters."""
+    import ctypes
+    from backuwup_amd import host_register, host_unregister
+    rng = np.random.default_rng(41)
+    lens = rng.integers(0, 200_000, 60).astype(np.uint64)
+    data = splitmix_bytes(42, int(lens.sum()) + 4096)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    want = oracle.process_files(data, offs, lens, *SMALL)
+    host_register(data.ctypes.data, data.nbytes)
+    try:
+        with Context(0) as c:
+            c.index_reset()
+            t = c.submit_host(data.ctypes.data, offs, lens, make_params(*SMALL), data_len=data.size)
+            blobs_equal(c.wait(t), want)
+    finally:
+        host_unregister(data.ctypes.data)
+
+
+@pytest.mark.parametrize("cap", [16, 1000, 20000])
+def test_candidate_array_truncation(oracle, cap):
+    """BW_OPT_CAND_CAP forces a candidate array far too small: every position past the first
+    truncated tile is tested by the walkers directly (C_TRUNC), and boundaries stay exact."""
+    with Context(0) as c:
+        c.set_option(BW_OPT_CAND_CAP, cap)
+        for n, p in [((3 << 20) + 11, SMALL), ((8 << 20) + 5, MID), ((40 << 20) + 7, BK)]:
+            d = splitmix_bytes(n + cap, n)
+            assert c.fastcdc_chunks(d, *p) == oracle.fastcdc(d, *p), (n, p)
+        z = np.concatenate([splitmix_bytes(9, 300_000), np.zeros(2_000_000, np.uint8)])
+        assert c.fastcdc_chunks(z, *MID) == oracle.fastcdc(z, *MID)
+        data, offs, lens = tree_corpus(40 << 20, seed=13, max_file=9 << 20)
+        c.index_reset()
+        blobs_equal(c.process_files(data, offs, lens, make_params(*MID)),
+                    oracle.process_files(data, offs, lens, *MID, threads=8))
+
+
+def test_device_gate_reports_collisions():
+    """Two distinct digests sharing the 64-bit table key: the device-side gate (the sharded
+    owner's path) writes verdict 2 and bw_index_check raises BW_ECOLLISION afterwards."""
+    import torch
+    a = np.random.default_rng(1).integers(0, 256, (3, 32), dtype=np.uint8)
+    a[1, :8] = a[0, :8]
+    with Context(0) as c:
+        c.index_reset()
+        d = torch.from_numpy(a.reshape(-1)).cuda()
+        v = torch.zeros(3, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        c.index_check_insert_device(d.data_ptr(), 3, v.data_ptr())
+        with pytest.raises(BwError) as e:
+            c.index_check()
+        assert e.value.rc == BW_ECOLLISION
+        torch.cuda.synchronize()
+        assert v.cpu().tolist()[1] == 2
+        c.index_reset()
+        c.index_check()  # a reset clears it
+
+
+def test_tree_pack_tree_on_one_context(oracle):
+    """tree blobs, then sealing/packing, then tree blobs again on one context, then
+    destroy (the pinned message staging used to be freed by the sealing path)."""
+    from oracle import pack_oracle as po
+    rng = np.random.default_rng(6)
+    specs = [(0, "f%d" % i, 100 + i, 1700000000, None, rng.integers(0, 256, 32 * (i % 5), dtype=np.uint8).tobytes())
+             for i in range(3000)]
+    prk = bytes(range(32))
+    c = Context(0)
+    try:
+        for rnd in range(2):
+            c.index_reset()
+            hashes, _ = c.tree_blobs([make_tree(*s) for s in specs], dedup=False)
+            for i in (0, 1, 1234, 2999):
+                assert bytes(hashes[i]) == oracle.split_serialize_tree(*specs[i])[0][1], (rnd, i)
+            blobs = [splitmix_bytes(50 + k + 100 * rnd, 70000 + 999 * k) for k in range(40)]
+            lens = np.array([b.size for b in blobs], dtype=np.uint64)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+            hs = np.array([np.frombuffer(oracle.blake3(b), np.uint8) for b in blobs])
+            nonces = rng.integers(0, 256, (40, 12), dtype=np.uint8)
+            plan, total = c.pack_plan(lens)
+            ids = rng.integers(0, 256, (len(plan), 12), dtype=np.uint8)
+            out = c.pack_build(prk, np.concatenate(blobs), offs, lens, hs, np.zeros(40, np.uint8), nonces, plan,
+                               total, ids)
+            p = plan[0]
+            want = po.serialize_packfile(prk, bytes(ids[0]), [
+                (bytes(hs[i]), 0, bytes(nonces[i]), po.seal_blob_payload(prk, hs[i], nonces[i], po.zstd_store(blobs[i])))
+                for i in range(int(p["first_blob"]), int(p["first_blob"] + p["n_blobs"]))])
+            assert out[int(p["offset"]):int(p["offset"] + p["size"])].tobytes() == want
+    finally:
+        c.close()
+
+
+def test_pack_rejects_blob_over_3mib():
+    from backuwup_amd._lib import BW_EINVAL
+    with Context(0) as c:
+        n = (3 << 20) + 1
+        plan, total = c.pack_plan([n])
+        with pytest.raises(BwError) as e:
+            c.pack_build(bytes(32), np.zeros(n, np.uint8), [0], [n], np.zeros((1, 32), np.uint8), [0],
+                         np.zeros((1, 12), np.uint8), plan, total, np.zeros((1, 12), np.uint8))
+        assert e.value.rc == BW_EINVAL
+
+
+def test_no_dedup_batches_leave_shared_index_alone(oracle):
+    """BW_F_NO_DEDUP batches (the sharded path's local pass) append nothing to the shared index."""
+    import torch
+    data, offs, lens = small_files(500, seed=90)
+    t = torch.from_numpy(data).cuda()
+    torch.cuda.synchronize()
+    ix = Index(0)
+    try:
+        with Context(0) as c:
+            c.attach_index(ix)
+            c.index_reset()
+            tk = c.submit_device(t.data_ptr(), data.size, offs, lens, make_params(flags=BW_F_NO_DEDUP))
+            r = c.wait(tk)
+            assert not r["is_dup"].any() and c.index_size() == 0
+            want = oracle.process_files(data, offs, lens)
+            assert np.array_equal(r["digest"], want["digest"])
+    finally:
+        ix.close()

@@ -137,6 +137,7 @@ int main() {
     mk.min = 262144; mk.avg = 1048576; mk.max = 3145728; mk.s0 = 262144;
     mk.mask_s = 0x0000d91767537000ull; mk.mask_l = 0x0000d91707537000ull; mk.mask_pre = mk.mask_l;
     mk.pre_shift = 16; mk.pre_hi = (uint32_t)((mk.mask_pre << 16) >> 32);
+    mk.tile_shift = SCAN_TILE_SHIFT;  // launch_scan picks the kernel by tile size
     const double gb = n / 1e9;
     float t;
     t = timeit([&] { hipLaunchKernelGGL(copy_strided, dim3(1024), dim3(512), 0, 0, d, n, out); });

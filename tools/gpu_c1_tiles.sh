@@ -5,6 +5,6 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 for i in 1 2 3 4; do
-  BW_SCAN_SMALL_BYTES=0 timeout -k 10 300 python bench.py --workload c1 --no-cpu-baseline --no-check > gpurun_out/c1_full_$i.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py --workload c1 --no-cpu-baseline --no-check > gpurun_out/c1_full_$i.log 2>&1 || exit 1
   timeout -k 10 300 python bench.py --workload c1 --no-cpu-baseline --no-check > gpurun_out/c1_half_$i.log 2>&1 || exit 1
 done

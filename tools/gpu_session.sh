@@ -9,13 +9,13 @@ MODE="${1:-all}"
 run() { local name=$1 t=$2; shift 2; echo "== $name" >&2; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc" | tee -a "$OUT/summary.txt"; return $rc; }
 : > "$OUT/summary.txt"
 if [[ "$MODE" == *tests* || "$MODE" == all ]]; then
-  run pytest_gpu 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider || exit 1
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread || exit 1
 fi
 if [[ "$MODE" == *smoke* || "$MODE" == all ]]; then
   run smoke 300 python __graft_entry__.py || exit 1
 fi
 if [[ "$MODE" == *bench* || "$MODE" == all ]]; then
-  run bench 600 python bench.py || exit 1
+  run bench 600 python bench.py ${BENCH_ARGS:-} || exit 1
 fi
 if [[ "$MODE" == *prof* || "$MODE" == all ]]; then
   cd /tmp && export TMPDIR=/tmp
