@@ -104,6 +104,12 @@ SIGNATURES = [
     ("bw_partition_by_owner", ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, u64p]),
     ("bw_index_check_insert_device", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),
     ("bw_scatter_verdicts", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, vp]),
+    ("bw_batch_views", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                      ctypes.POINTER(vp), u64p]),
+    ("bw_partition_buckets", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, vp, vp,
+                                            vp]),
+    ("bw_index_check_insert_buckets", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]),
+    ("bw_scatter_buckets", ctypes.c_int, [vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]),
     ("bw_tree_serialize", ctypes.c_int, [ctypes.POINTER(BwTree), vp, vp, ctypes.c_uint64, u64p]),
     ("bw_tree_blobs", ctypes.c_int, [vp, ctypes.POINTER(BwTree), ctypes.c_uint64, ctypes.c_uint32, vp,
                                      ctypes.POINTER(BwTreeBlob), ctypes.c_uint64, u64p]),

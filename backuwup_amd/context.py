@@ -459,6 +459,26 @@ class Context:
         check(self._L.bw_index_check_insert_device(self.h, ctypes.c_void_p(d_digests), n,
                                                    ctypes.c_void_p(d_is_dup)), self.h)
 
+    def batch_views(self, ticket=0):
+        """(d_n_blobs, d_digests, d_is_dup, max_blobs) of a batch, no synchronization."""
+        n, d, dup, mx = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        check(self._L.bw_batch_views(self.h, ticket, ctypes.byref(n), ctypes.byref(d), ctypes.byref(dup),
+                                     ctypes.byref(mx)), self.h)
+        return n.value, d.value, dup.value, mx.value
+
+    def partition_buckets(self, d_digests, d_n, max_n, cap, n_owners, d_buckets, d_perm, d_counts):
+        check(self._L.bw_partition_buckets(self.h, ctypes.c_void_p(d_digests), ctypes.c_void_p(d_n), max_n, cap,
+                                           n_owners, ctypes.c_void_p(d_buckets), ctypes.c_void_p(d_perm),
+                                           ctypes.c_void_p(d_counts)), self.h)
+
+    def index_check_insert_buckets(self, d_buckets, d_counts, n_src, cap, d_verdicts):
+        check(self._L.bw_index_check_insert_buckets(self.h, ctypes.c_void_p(d_buckets), ctypes.c_void_p(d_counts),
+                                                    n_src, cap, ctypes.c_void_p(d_verdicts)), self.h)
+
+    def scatter_buckets(self, d_verdicts, d_perm, d_counts, n_owners, cap, d_is_dup):
+        check(self._L.bw_scatter_buckets(self.h, ctypes.c_void_p(d_verdicts), ctypes.c_void_p(d_perm),
+                                         ctypes.c_void_p(d_counts), n_owners, cap, ctypes.c_void_p(d_is_dup)), self.h)
+
     def scatter_verdicts(self, d_verdict, d_perm, n, d_is_dup):
         check(self._L.bw_scatter_verdicts(self.h, ctypes.c_void_p(d_verdict), ctypes.c_void_p(d_perm), n,
                                           ctypes.c_void_p(d_is_dup)), self.h)

@@ -84,6 +84,7 @@ struct bw_ctx {
     DevBuf segs, cfiles, units, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
     DevBuf cv, cv2, fstart, data, scratch, ucnt, ubtot;
+    DevBuf bk_blk, bk_pack, bk_v;  // multi-GPU exchange buckets (bw_partition_buckets, ...)
 
     // batches in flight: ring of result slots addressed by ticket
     Slot slots[MAX_DEPTH];
@@ -373,6 +374,10 @@ static int check_collision(bw_ctx* c, bool all = false) {
         c->err = "64-bit key collision between distinct digests";
         return BW_ECOLLISION;
     }
+    if (st[D_BUCKET_OVF]) {
+        c->err = "a batch had more blobs than its exchange bucket capacity (verdicts incomplete)";
+        return BW_ENOSPC;
+    }
     return BW_OK;
 }
 
@@ -441,7 +446,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->fstart,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
-                     &c->ix_io, &c->ix_tab, &c->ix_dig};
+                     &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v};
     for (DevBuf* b : all) free_dev(*b);
     for (Slot& s : c->slots) {
         free_dev(s.ctr);
@@ -476,8 +481,11 @@ extern "C" const char* bw_last_error(const bw_ctx* c) { return c ? c->err.c_str(
 
 extern "C" int bw_set_stream(bw_ctx* c, void* s) {
     if (!c) return BW_EINVAL;
-    hipStreamSynchronize(c->stream);
-    c->stream = s ? (hipStream_t)s : c->own;
+    hipStream_t want = s ? (hipStream_t)s : c->own;
+    if (want == c->stream) return BW_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);  // work queued on the old stream is done before the switch
+    c->stream = want;
     return BW_OK;
 }
 
@@ -1092,6 +1100,60 @@ extern "C" int bw_partition_by_owner(bw_ctx* c, const uint8_t* d_digests, uint64
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(h_counts, c->scratch.p, n_owners * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BW_OK;
+}
+
+extern "C" int bw_batch_views(bw_ctx* c, uint64_t ticket, const uint64_t** d_n_blobs, const uint8_t** d_digests,
+                              uint8_t** d_is_dup, uint64_t* max_blobs) {
+    if (!c) return BW_EINVAL;
+    Slot* s = slot_of(c, ticket ? ticket : c->last_ticket);
+    if (!s) return BW_ESTATE;
+    if (d_n_blobs) *d_n_blobs = P<uint64_t>(s->ctr) + C_NBLOBS;
+    if (d_digests) *d_digests = P<uint8_t>(s->digests);
+    if (d_is_dup) *d_is_dup = P<uint8_t>(s->is_dup);
+    if (max_blobs) *max_blobs = s->max_blobs;
+    return BW_OK;
+}
+
+static bool owners_ok(uint32_t n) { return n >= 1 && n <= 256 && (n & (n - 1)) == 0; }
+
+extern "C" int bw_partition_buckets(bw_ctx* c, const uint8_t* d_digests, const uint64_t* d_n, uint64_t max_n,
+                                    uint64_t cap, uint32_t n_owners, uint8_t* d_buckets, uint64_t* d_perm,
+                                    uint64_t* d_counts) {
+    if (!c || !d_n || !d_counts || !owners_ok(n_owners) || (cap && (!d_buckets || !d_perm))) return BW_EINVAL;
+    if (max_n && !d_digests) return BW_EINVAL;
+    hipSetDevice(c->device);
+    const uint64_t nblk = (max_n + 4095) / 4096;
+    if (int rc = ensure(c, c->bk_blk, (nblk + 1) * n_owners * 8)) return rc;
+    launch_bucket_partition(c->stream, d_digests, d_n, max_n, n_owners, cap, d_buckets, d_perm, d_counts,
+                            P<uint64_t>(c->bk_blk), P<uint64_t>(c->idx->dstate) + D_BUCKET_OVF);
+    HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+extern "C" int bw_index_check_insert_buckets(bw_ctx* c, const uint8_t* d_buckets, const uint64_t* d_counts,
+                                             uint32_t n_src, uint64_t cap, uint8_t* d_verdicts) {
+    if (!c || !d_counts || !n_src || (cap && (!d_buckets || !d_verdicts))) return BW_EINVAL;
+    const uint64_t total = (uint64_t)n_src * cap;
+    if (!total) return BW_OK;
+    hipSetDevice(c->device);
+    if (int rc = ensure(c, c->bk_pack, total * 32 + 16)) return rc;
+    if (int rc = ensure(c, c->bk_v, total)) return rc;
+    uint8_t* pack = P<uint8_t>(c->bk_pack);
+    uint64_t* n_dev = (uint64_t*)(pack + total * 32);
+    launch_bucket_gather(c->stream, d_buckets, d_counts, n_src, cap, pack, n_dev);
+    if (int rc = dedup_device(c, pack, n_dev, 0, total, P<uint8_t>(c->bk_v))) return rc;
+    launch_bucket_expand(c->stream, d_counts, n_src, cap, P<uint8_t>(c->bk_v), d_verdicts);
+    HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+extern "C" int bw_scatter_buckets(bw_ctx* c, const uint8_t* d_verdicts, const uint64_t* d_perm,
+                                  const uint64_t* d_counts, uint32_t n_owners, uint64_t cap, uint8_t* d_is_dup) {
+    if (!c || !d_counts || !owners_ok(n_owners) || (cap && (!d_verdicts || !d_perm || !d_is_dup))) return BW_EINVAL;
+    hipSetDevice(c->device);
+    launch_bucket_scatter(c->stream, d_verdicts, d_perm, d_counts, n_owners, cap, d_is_dup);
+    HIPCHK(c, hipGetLastError());
     return BW_OK;
 }
 

@@ -200,6 +200,161 @@ void launch_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, verdict, perm, n, is_dup);
 }
 
+// ------------------------------------------------------------------ fixed-capacity owner buckets
+// The exchange without host round trips: every rank sends every owner a bucket of `cap` slots
+// (an upper bound of its batch's blob count agreed once per session), so the all-to-alls have
+// equal splits and the counts travel on the device.  Bucket o holds the digests owned by o in
+// canonical order; perm maps each slot back to its blob.
+constexpr int BP_THREADS = 256, BP_ITEMS = 16, BP_CHUNK = BP_THREADS * BP_ITEMS;
+
+template <int T>
+__device__ __forceinline__ uint64_t block_excl_sum_u64(uint64_t v, uint64_t* s, uint64_t* total) {
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < T; d <<= 1) {
+        const uint64_t a = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0;
+        __syncthreads();
+        s[threadIdx.x] += a;
+        __syncthreads();
+    }
+    const uint64_t incl = s[threadIdx.x];
+    *total = s[T - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__device__ __forceinline__ uint32_t owner_of(const uint8_t* d, uint32_t shift) { return shift >= 8 ? 0 : d[0] >> shift; }
+
+// Per block: for owner o, each thread's count of its 16 items, block-scanned.  WRITE: place them.
+template <bool WRITE>
+__global__ __launch_bounds__(BP_THREADS) void k_bucket_pass(const uint8_t* __restrict__ digests, const uint64_t* n_dev,
+                                                            uint32_t n_owners, uint32_t shift, uint64_t cap,
+                                                            uint64_t* __restrict__ blk /* [blocks][n_owners] */,
+                                                            uint8_t* __restrict__ out, uint64_t* __restrict__ perm) {
+    __shared__ uint64_t s[BP_THREADS];
+    const uint64_t n = *n_dev;
+    const uint64_t i0 = (uint64_t)blockIdx.x * BP_CHUNK + (uint64_t)threadIdx.x * BP_ITEMS;
+    if ((uint64_t)blockIdx.x * BP_CHUNK >= n) return;  // whole block past the end (uniform)
+    uint32_t own[BP_ITEMS];
+#pragma unroll
+    for (int k = 0; k < BP_ITEMS; k++) own[k] = i0 + k < n ? owner_of(digests + (i0 + k) * 32, shift) : ~0u;
+    for (uint32_t o = 0; o < n_owners; o++) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int k = 0; k < BP_ITEMS; k++) c += own[k] == o;
+        uint64_t total;
+        uint64_t pos = block_excl_sum_u64<BP_THREADS>(c, s, &total);
+        if (!WRITE) {
+            if (threadIdx.x == 0) blk[(uint64_t)blockIdx.x * n_owners + o] = total;
+        } else {
+            pos += blk[(uint64_t)blockIdx.x * n_owners + o];
+#pragma unroll
+            for (int k = 0; k < BP_ITEMS; k++)
+                if (own[k] == o) {
+                    if (pos < cap) {
+                        const uint4* a = (const uint4*)(digests + (i0 + k) * 32);
+                        uint4* d = (uint4*)(out + ((uint64_t)o * cap + pos) * 32);
+                        d[0] = a[0];
+                        d[1] = a[1];
+                        perm[(uint64_t)o * cap + pos] = i0 + k;
+                    }
+                    pos++;
+                }
+        }
+    }
+}
+
+// Per owner: exclusive scan of the block totals (in place) and the bucket count.
+__global__ void k_bucket_top(uint64_t* __restrict__ blk, uint64_t nblk, uint32_t n_owners, const uint64_t* n_dev,
+                             uint64_t cap, uint64_t* __restrict__ counts, uint64_t* err) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n_owners) return;
+    const uint64_t used = (*n_dev + BP_CHUNK - 1) / BP_CHUNK;
+    uint64_t run = 0;
+    for (uint64_t b = 0; b < used && b < nblk; b++) {
+        const uint64_t t = blk[b * n_owners + o];
+        blk[b * n_owners + o] = run;
+        run += t;
+    }
+    counts[o] = run < cap ? run : cap;
+    if (run > cap) atomicOr((unsigned long long*)err, 1ull);
+}
+
+void launch_bucket_partition(hipStream_t st, const uint8_t* digests, const uint64_t* n_dev, uint64_t max_n,
+                             uint32_t n_owners, uint64_t cap, uint8_t* out, uint64_t* perm, uint64_t* counts,
+                             uint64_t* blk, uint64_t* err) {
+    const uint32_t bits = 31 - __builtin_clz(n_owners | 1);
+    const uint32_t shift = 8 - bits;
+    const uint64_t nblk = (max_n + BP_CHUNK - 1) / BP_CHUNK;
+    if (nblk)
+        hipLaunchKernelGGL(k_bucket_pass<false>, dim3((unsigned)nblk), dim3(BP_THREADS), 0, st, digests, n_dev,
+                           n_owners, shift, cap, blk, out, perm);
+    hipLaunchKernelGGL(k_bucket_top, dim3((n_owners + 255) / 256), dim3(256), 0, st, blk, nblk, n_owners, n_dev, cap,
+                       counts, err);
+    if (nblk)
+        hipLaunchKernelGGL(k_bucket_pass<true>, dim3((unsigned)nblk), dim3(BP_THREADS), 0, st, digests, n_dev,
+                           n_owners, shift, cap, blk, out, perm);
+}
+
+// Owner side: the received buckets (source-major = canonical) packed contiguously, n on device.
+__global__ void k_bucket_gather(const uint8_t* __restrict__ buckets, const uint64_t* __restrict__ counts,
+                                uint32_t n_src, uint64_t cap, uint8_t* __restrict__ out, uint64_t* __restrict__ n_out,
+                                int expand, const uint8_t* __restrict__ v_in, uint8_t* __restrict__ v_out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t s = i / cap, k = i % cap;
+    if (s >= n_src) return;
+    uint64_t base = 0;
+    for (uint32_t j = 0; j < s; j++) base += counts[j];
+    if (!expand && i == 0) {
+        uint64_t t = 0;
+        for (uint32_t j = 0; j < n_src; j++) t += counts[j];
+        *n_out = t;
+    }
+    if (k >= counts[s]) return;
+    if (!expand) {
+        const uint4* a = (const uint4*)(buckets + i * 32);
+        uint4* d = (uint4*)(out + (base + k) * 32);
+        d[0] = a[0];
+        d[1] = a[1];
+    } else {
+        v_out[i] = v_in[base + k];  // verdicts back into the bucket layout
+    }
+}
+
+void launch_bucket_gather(hipStream_t st, const uint8_t* buckets, const uint64_t* counts, uint32_t n_src, uint64_t cap,
+                          uint8_t* out, uint64_t* n_out) {
+    const uint64_t n = (uint64_t)n_src * cap;
+    if (!n) return;
+    hipLaunchKernelGGL(k_bucket_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, buckets, counts, n_src, cap,
+                       out, n_out, 0, nullptr, nullptr);
+}
+
+void launch_bucket_expand(hipStream_t st, const uint64_t* counts, uint32_t n_src, uint64_t cap, const uint8_t* v_in,
+                          uint8_t* v_out) {
+    const uint64_t n = (uint64_t)n_src * cap;
+    if (!n) return;
+    hipLaunchKernelGGL(k_bucket_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nullptr, counts, n_src,
+                       cap, nullptr, nullptr, 1, v_in, v_out);
+}
+
+// Source side: verdicts of my buckets back to blob order.
+__global__ void k_bucket_scatter(const uint8_t* __restrict__ verdict, const uint64_t* __restrict__ perm,
+                                 const uint64_t* __restrict__ counts, uint32_t n_owners, uint64_t cap,
+                                 uint8_t* __restrict__ is_dup) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t o = i / cap, k = i % cap;
+    if (o >= n_owners || k >= counts[o]) return;
+    is_dup[perm[i]] = verdict[i];
+}
+
+void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, const uint64_t* counts,
+                           uint32_t n_owners, uint64_t cap, uint8_t* is_dup) {
+    const uint64_t n = (uint64_t)n_owners * cap;
+    if (!n) return;
+    hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, verdict, perm, counts,
+                       n_owners, cap, is_dup);
+}
+
 // ------------------------------------------------------------------ result records
 
 __global__ void k_pack(const uint64_t* ctr, BlobArrays b, const uint64_t* __restrict__ file_start,

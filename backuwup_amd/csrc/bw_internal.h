@@ -125,7 +125,8 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
 // ------------------------------------------------------------------ launchers (bw_dedup.hip)
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),
 // st[1] = distinct digests, st[2] = collision flag.
-enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_COLLIDE = 2, D_COUNT = 4 };
+// st[3] = an exchange bucket overflowed (a batch had more blobs than the agreed capacity).
+enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_COLLIDE = 2, D_BUCKET_OVF = 3, D_COUNT = 4 };
 void launch_table_clear(hipStream_t st, uint64_t* table, uint64_t cap);
 // Append n digests (n from *n_dev if non-null, else n_host) to the log and decide them in
 // order: is_dup[i] (may be null) = digest seen at an earlier log position.
@@ -139,6 +140,17 @@ void launch_partition(hipStream_t st, const uint8_t* digests, uint64_t n, uint32
                       uint8_t* out, uint64_t* perm, uint64_t* counts_dev);
 void launch_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, uint64_t n,
                     uint8_t* is_dup);
+// fixed-capacity owner buckets (multi-GPU exchange without host round trips); blk holds
+// ceil(max_n / 4096) * n_owners u64, err is set when a bucket would exceed cap
+void launch_bucket_partition(hipStream_t st, const uint8_t* digests, const uint64_t* n_dev, uint64_t max_n,
+                             uint32_t n_owners, uint64_t cap, uint8_t* out, uint64_t* perm, uint64_t* counts,
+                             uint64_t* blk, uint64_t* err);
+void launch_bucket_gather(hipStream_t st, const uint8_t* buckets, const uint64_t* counts, uint32_t n_src, uint64_t cap,
+                          uint8_t* out, uint64_t* n_out);
+void launch_bucket_expand(hipStream_t st, const uint64_t* counts, uint32_t n_src, uint64_t cap, const uint8_t* v_in,
+                          uint8_t* v_out);
+void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, const uint64_t* counts,
+                           uint32_t n_owners, uint64_t cap, uint8_t* is_dup);
 void launch_pack(hipStream_t st, const uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
                  const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs);
 

@@ -4,18 +4,24 @@ One process per GPU.  Files are sharded rank-major (rank r holds canonical files
 [F_r, F_{r+1})), so (rank, local blob index) order IS the canonical order.  Each step:
 
   1. every rank chunks + hashes its own files (no collective on the data path);
-  2. its digests are stably partitioned by owner = digest[0] >> (8 - log2 N);
-  3. one all-to-all of the per-owner counts, one all-to-all of the 32-byte digests (RCCL over
-     xGMI on MI355X; ~13.5k digests = 432 KiB per 16 GiB stream, latency-bound);
-  4. each owner decides its slice against its shard of the index -- the received buffer is
-     source-rank-major, i.e. canonical, so first occurrence = first position;
+  2. its digests are stably partitioned by owner = digest[0] >> (8 - log2 N) into N buckets of a
+     fixed capacity `cap` (one bound agreed per session), with the per-owner counts on the device;
+  3. one all-to-all of the counts and one of the buckets (RCCL over xGMI on MI355X; equal splits,
+     so nothing has to come back to the host first);
+  4. each owner gates the received buckets against its shard of the index in source-rank-major
+     order -- the canonical order, so first occurrence = first position;
   5. one all-to-all returns the verdict bytes, scattered back to local blob order.
+
+Nothing in the sequence waits on the host: it is enqueued on the batch's stream behind the
+batch's kernels, and the next batch (another stream) computes meanwhile.  The bucket capacity
+trades bytes for the host round trip: N x cap x 32 B per rank per batch (C2: 65,538 slots -> 2 MiB
+per owner), which xGMI moves in tens of microseconds.
 
 This replaces the reference's single in-process BlobIndex (blob_index.rs:44-148), whose
 `blobs_queued` HashSet and sorted `items` become the union of the N shards.
 
 The collective sequence is written once against a small ops interface so the same code runs
-on the GPU (DeviceShardOps, backed by libbackuwup_amd.so) and in the world-size-2 gloo tests.
+on the GPU (DeviceShardOps, backed by libbackuwup_amd.so) and in the world-size-2/4 gloo tests.
 """
 import torch
 import torch.distributed as dist
@@ -27,43 +33,65 @@ def owner_of(first_byte, world):
 
 
 class DeviceShardOps:
-    """GPU implementation of the three local steps (all device-resident)."""
+    """GPU implementation of the three local steps (all device-resident, no synchronization).
+    A batch is the tuple Context.batch_views(ticket) returns: (d_n, d_digests, d_is_dup, max_n)."""
 
     def __init__(self, ctx, device):
         # the collectives run on torch's current stream; the library must use the same stream so
         # its kernels and the all-to-alls are ordered
         self.ctx, self.device = ctx, device
-        ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        handle = torch.cuda.current_stream(device).cuda_stream
+        if not handle:  # the null stream does not order against the library's non-blocking streams
+            raise ValueError("run the exchange under a torch.cuda.Stream (not the default stream)")
+        ctx.set_stream(handle)
 
-    def partition(self, digests_ptr, n, world):
-        out = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=self.device)
-        perm = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
-        counts = self.ctx.partition_by_owner(digests_ptr, n, world, out.data_ptr(), perm.data_ptr())
-        return out, perm, [int(c) for c in counts]
+    def partition(self, batch, cap, world):
+        d_n, d_dig, _, max_n = batch
+        buckets = torch.empty(world * cap * 32, dtype=torch.uint8, device=self.device)
+        perm = torch.empty(world * cap, dtype=torch.int64, device=self.device)
+        counts = torch.empty(world, dtype=torch.int64, device=self.device)
+        self.ctx.partition_buckets(d_dig, d_n, max_n, cap, world, buckets.data_ptr(), perm.data_ptr(),
+                                   counts.data_ptr())
+        return buckets, perm, counts
 
-    def decide(self, recv, n):
-        verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
-        if n:
-            self.ctx.index_check_insert_device(recv.data_ptr(), n, verdict.data_ptr())
+    def decide(self, recv, recv_counts, world, cap):
+        verdict = torch.empty(world * cap, dtype=torch.uint8, device=self.device)
+        self.ctx.index_check_insert_buckets(recv.data_ptr(), recv_counts.data_ptr(), world, cap, verdict.data_ptr())
         return verdict
 
-    def scatter(self, back, perm, n, is_dup_ptr):
-        if n:
-            self.ctx.scatter_verdicts(back.data_ptr(), perm.data_ptr(), n, is_dup_ptr)
+    def scatter(self, back, perm, counts, world, cap, batch):
+        self.ctx.scatter_buckets(back.data_ptr(), perm.data_ptr(), counts.data_ptr(), world, cap, batch[2])
 
 
-def exchange_dedup(ops, digests_ptr, n, is_dup_ptr, world, device, group=None):
-    """Steps 2-5 above for one batch; returns (sent per owner, received per source)."""
-    out, perm, sc = ops.partition(digests_ptr, n, world)
-    send_counts = torch.tensor(sc, dtype=torch.int64, device=device)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    rc = [int(x) for x in recv_counts.cpu().tolist()]
-    nr = sum(rc)
-    recv = torch.empty(max(nr, 1) * 32, dtype=torch.uint8, device=device)
-    dist.all_to_all_single(recv[:nr * 32], out[:n * 32], [x * 32 for x in rc], [x * 32 for x in sc], group=group)
-    verdict = ops.decide(recv, nr)
-    back = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
-    dist.all_to_all_single(back[:n], verdict[:nr], sc, rc, group=group)
-    ops.scatter(back, perm, n, is_dup_ptr)
-    return sc, rc
+def exchange_dedup(ops, batch, world, cap, group=None, all_to_all=None):
+    """Steps 2-5 above for one batch; verdicts land in the batch's is_dup.  Returns the per-owner
+    counts tensor (device) for diagnostics.  all_to_all(out, inp, group) defaults to
+    dist.all_to_all_single (RCCL for device tensors)."""
+    a2a = all_to_all or (lambda out, inp, group: dist.all_to_all_single(out, inp, group=group))
+    buckets, perm, counts = ops.partition(batch, cap, world)
+    recv_counts = torch.empty_like(counts)
+    a2a(recv_counts, counts, group)
+    recv = torch.empty_like(buckets)
+    a2a(recv, buckets, group)
+    verdict = ops.decide(recv, recv_counts, world, cap)
+    back = torch.empty_like(verdict)
+    a2a(back, verdict, group)
+    ops.scatter(back, perm, counts, world, cap, batch)
+    return counts
+
+
+def session_capacity(max_blobs, device, group=None):
+    """The bucket capacity of a session: the largest per-batch blob bound over the ranks (one
+    all-reduce when the session starts, never per batch)."""
+    t = torch.tensor([int(max_blobs)], dtype=torch.int64, device=device)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def staged_all_to_all(out, inp, group=None):
+    """all_to_all_single for a backend without device collectives (gloo): the tensors go through
+    host memory.  Used to run the device exchange with several ranks on one GPU (tests)."""
+    o = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(o, inp.cpu(), group=group)
+    out.copy_(o)

@@ -128,7 +128,7 @@ def main():
     import torch.distributed as dist
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
-    from backuwup_amd._lib import BW_F_NO_DEDUP, STAGES
+    from backuwup_amd._lib import BW_F_NO_DEDUP, BW_OPT_DEPTH, STAGES
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -161,9 +161,11 @@ def main():
     ctxs, streams = [], []
     for k in range(nctx):
         c = Context(local)
-        st = torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)
+        st = torch.cuda.Stream(dev)
         c.set_stream(st.cuda_stream)
         c.attach_index(index)
+        if args.host_stream and nctx > 1:
+            c.set_option(BW_OPT_DEPTH, 1)  # contexts alternate: one HBM input buffer each is enough
         ctxs.append(c)
         streams.append(st)
     ctx = ctxs[0]
@@ -172,11 +174,12 @@ def main():
     max_blobs = sum(int(x) // (256 << 10) + 2 if int(x) > (1 << 20) else 1 for x in file_len)
     total_batches = args.warmup + args.steps + 4 + (3 if nctx > 1 else 0)
     # the host's bound of the log grows by max_blobs per batch until a result read tightens it
-    index_hint = total_batches * max_blobs + 1024
+    # (N > 1: by the N received buckets of max_blobs slots each, and nothing tightens it)
+    index_hint = total_batches * max_blobs * (world if multi else 1) + 1024
     owner_bits = world.bit_length() - 1
     assert world == 1 << owner_bits, "world size must be a power of two (digest-prefix owners)"
 
-    from backuwup_amd.sharded import DeviceShardOps, exchange_dedup
+    from backuwup_amd.sharded import DeviceShardOps, exchange_dedup, session_capacity
 
     host = None
     if args.host_stream:
@@ -188,21 +191,27 @@ def main():
     step_no = [0]
     host_ms = [0.0]  # host time inside the library's submit calls (metadata build + upload)
     inflight = []  # (context, ticket) of batches whose results are not read yet
-    pending = [None]  # N > 1: the context whose batch still awaits its digest exchange
     out_buf = np.zeros(max_blobs + 1, dtype=BLOB_DTYPE)
 
-    def exchange(k):
-        # digest all-to-all by owner = digest[0] >> (8 - log2 N); verdicts come back (RCCL on the
-        # batch's own stream, beside the next batch's kernels on the other stream)
+    cap = [None]
+    shard_ops = []
+    if multi:
+        for k, c in enumerate(ctxs):
+            with torch.cuda.stream(streams[k]):
+                shard_ops.append(DeviceShardOps(c, dev))
+
+    def exchange(k, t):
+        # digest all-to-all by owner = digest[0] >> (8 - log2 N), verdicts back: enqueued on the
+        # batch's own stream behind its kernels, no host round trip; the next batch computes on
+        # the other stream meanwhile
         c = ctxs[k]
         with torch.cuda.stream(streams[k]):
-            nb, d_dig, d_dup = c.device_views()
-            exchange_dedup(DeviceShardOps(c, dev), d_dig, nb, d_dup, world, dev)
+            batch = c.batch_views(t)
+            if cap[0] is None:
+                cap[0] = session_capacity(batch[3], dev)
+            exchange_dedup(shard_ops[k], batch, world, cap[0])
 
     def drain():
-        if pending[0] is not None:
-            exchange(pending[0])
-            pending[0] = None
         while inflight:
             c, t = inflight.pop(0)
             c.wait(t, out=out_buf)
@@ -219,9 +228,7 @@ def main():
                 t = c.submit_device(data.data_ptr(), n, file_off, file_len, params)
             host_ms[0] += (time.perf_counter() - th) * 1e3
         if multi:
-            if pending[0] is not None:
-                exchange(pending[0])  # the previous batch's exchange, while this batch computes
-            pending[0] = k
+            exchange(k, t)
         else:
             inflight.append((c, t))
             if len(inflight) > 1:  # two batches in flight: read batch k-1 while batch k runs
@@ -311,35 +318,8 @@ def main():
     pack = time_pack(ctx, data, res, file_off, args.steps) if args.pack else None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "c2":
-        # many files: the reference runs one task per file (dir_packer.rs:166), so the port runs
-        # them on all the cores this GPU's share of the box offers
-        from oracle import oracle
-        threads = min(16, os.cpu_count() or 1)
-        fo = np.asarray(file_off, dtype=np.uint64)
-        fl = np.asarray(file_len, dtype=np.uint64)
-        k = max(1, int(np.searchsorted(np.cumsum(fl), int(args.cpu_sample_gib * (1 << 30)))))
-        end = int(np.max(fo[:k] + fl[:k]))
-        hb = data[:end].cpu().numpy()
-        t1 = time.perf_counter()
-        r = oracle.process_files(hb, fo[:k], fl[:k], threads=threads)
-        ct = time.perf_counter() - t1
-        m = int(np.sum(fl[:k]))
-        cpu = {"value": round(m / ct / 1e9, 4), "unit": "GB/s", "cores": min(threads, k), "kind": "port",
-               "sample": "first %d files (%.2f GB, %d blobs) of the workload, oracle/bw_oracle.c "
-                         "FastCDC+BLAKE3+index, one file per task like the reference" % (k, m / 1e9, len(r)),
-               "seconds": round(ct, 2)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
-        from oracle import oracle
-        m = int(args.cpu_sample_gib * (1 << 30))
-        hb = data[:m].cpu().numpy()
-        t1 = time.perf_counter()
-        r = oracle.process_files(hb, [0], [m], threads=1)
-        ct = time.perf_counter() - t1
-        cpu = {"value": round(m / ct / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-               "sample": "first %.0f GiB of the C2 stream as one file (%d blobs), oracle/bw_oracle.c "
-                         "FastCDC+BLAKE3+index, serial within a file like the reference" % (args.cpu_sample_gib, len(r)),
-               "seconds": round(ct, 2)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, data, file_off, file_len)
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -361,6 +341,70 @@ def main():
         print(json.dumps(line), flush=True)
     if multi:
         dist.destroy_process_group()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, data, file_off, file_len, reps=5):
+    """The reference's CPU path restated (oracle/bw_oracle.c FastCDC + index, with the crate's
+    16-way SIMD BLAKE3 strategy, bw_oracle_simd.c), timed on this box's host cores: the median of
+    `reps` runs on all the cores this GPU's share offers (16) and on one core.  Threading follows
+    the reference: one task per file, serial within a file (dir_packer.rs:148-166); a single
+    stream (C2) is cut into 16 files for the all-core figure, which moves the cuts of those
+    files' heads but not the work per byte.  About 10-20 s of CPU time in total."""
+    import numpy as np
+    from oracle import oracle
+    simd = oracle.set_blake3_simd(True)
+    threads = min(16, os.cpu_count() or 1)
+    fo = np.asarray(file_off, dtype=np.uint64)
+    fl = np.asarray(file_len, dtype=np.uint64)
+
+    def timed(host, offs, lens, t):
+        runs = []
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            r = oracle.process_files(host, offs, lens, threads=t)
+            runs.append(time.perf_counter() - t1)
+        m = float(np.sum(np.asarray(lens, dtype=np.uint64)))
+        return m, sorted(runs)[len(runs) // 2], len(r)
+
+    try:
+        if args.workload == "c2":
+            one = int(1 << 30)
+            allc = int(min(args.cpu_sample_gib, 8.0) * (1 << 30))
+            host = data[:max(one, allc)].cpu().numpy()
+            m1, t1, b1 = timed(host, [0], [one], 1)
+            per = allc // threads
+            offs = np.arange(threads, dtype=np.uint64) * np.uint64(per)
+            mA, tA, bA = timed(host, offs, np.full(threads, per, dtype=np.uint64), threads)
+            sample = ("C2 stream: one core = its first 1 GiB as one file (%d blobs); all cores = its first %.0f GiB "
+                      "cut into %d files of %.2f GiB, one per task (%d blobs)" % (b1, allc / 2**30, threads,
+                                                                                 per / 2**30, bA))
+        else:
+            cum = np.cumsum(fl)
+            kA = max(1, int(np.searchsorted(cum, int(min(args.cpu_sample_gib, 8.0) * (1 << 30)))))
+            k1 = max(1, int(np.searchsorted(cum, 1 << 30)))
+            end = int(np.max(fo[:kA] + fl[:kA]))
+            host = data[:end].cpu().numpy()
+            m1, t1, b1 = timed(host, fo[:k1], fl[:k1], 1)
+            mA, tA, bA = timed(host, fo[:kA], fl[:kA], threads)
+            sample = ("first %d files (%.2f GB, %d blobs) on all cores, one file per task; first %d files "
+                      "(%.2f GB) on one core" % (kA, mA / 1e9, bA, k1, m1 / 1e9))
+    finally:
+        oracle.set_blake3_simd(False)
+    return {"value": round(mA / tA / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": sample, "stat": "median of %d runs" % reps, "seconds": round(tA, 3),
+            "one_core": {"value": round(m1 / t1 / 1e9, 3), "seconds": round(t1, 3)},
+            "blake3": "16-way AVX-512 (the crate's hash_many strategy)" if simd else "scalar (no AVX-512 here)",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count()}
 
 
 def time_file_trees(ctx, res, file_len, reps):

@@ -212,6 +212,28 @@ int bw_index_check_insert_device(bw_ctx* ctx, const uint8_t* d_digests, uint64_t
 int bw_scatter_verdicts(bw_ctx* ctx, const uint8_t* d_verdict, const uint64_t* d_perm,
                         uint64_t n, uint8_t* d_is_dup);
 
+/* Exchange without host round trips (what the multi-GPU path uses per batch).  Every rank sends
+ * every owner a bucket of `cap` digest slots, so the all-to-alls have equal splits and the counts
+ * stay on the device; cap is agreed once per session (>= the largest batch's max_blobs makes
+ * overflow impossible; a smaller cap that a batch exceeds sets a sticky error that
+ * bw_index_check reports as BW_ENOSPC).
+ * Device views of batch `ticket` (0 = the most recent), no synchronization: d_n_blobs points at
+ * the batch's blob count in HBM; *max_blobs = its host-side upper bound. */
+int bw_batch_views(bw_ctx* ctx, uint64_t ticket, const uint64_t** d_n_blobs, const uint8_t** d_digests,
+                   uint8_t** d_is_dup, uint64_t* max_blobs);
+/* d_buckets[n_owners][cap][32] = digests by owner, canonical order inside each bucket;
+ * d_perm[n_owners][cap] = source index; d_counts[n_owners] (device u64).  n = *d_n (device),
+ * max_n its host bound. */
+int bw_partition_buckets(bw_ctx* ctx, const uint8_t* d_digests, const uint64_t* d_n, uint64_t max_n, uint64_t cap,
+                         uint32_t n_owners, uint8_t* d_buckets, uint64_t* d_perm, uint64_t* d_counts);
+/* Owner: gate the received buckets (n_src x cap, counts d_counts[n_src] on the device) in
+ * source-major order; d_verdicts in the same bucket layout. */
+int bw_index_check_insert_buckets(bw_ctx* ctx, const uint8_t* d_buckets, const uint64_t* d_counts, uint32_t n_src,
+                                  uint64_t cap, uint8_t* d_verdicts);
+/* Source: d_is_dup[d_perm[o][i]] = d_verdicts[o][i] for i < d_counts[o]. */
+int bw_scatter_buckets(bw_ctx* ctx, const uint8_t* d_verdicts, const uint64_t* d_perm, const uint64_t* d_counts,
+                       uint32_t n_owners, uint64_t cap, uint8_t* d_is_dup);
+
 /* ---- tree blobs: split_serialize_tree + add_tree_to_blobs, dir_packer.rs:314-390 ----
  * Tree { kind: TreeKind, name: String, metadata: TreeMetadata { size, mtime, ctime: Option<u64> },
  *        children: Vec<BlobHash>, next_sibling: Option<BlobHash> }   (filesystem/mod.rs:63-77)

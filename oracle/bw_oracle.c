@@ -267,6 +267,14 @@ static void b3_subtree(const uint8_t* in, size_t len, uint64_t t, int root, uint
     b3_parent_cv(l, r, root ? B3_ROOT : 0, out);
 }
 
+void orc_blake3_chunk_cv(const uint8_t* in, size_t len, uint64_t t, uint32_t out[8]) { b3_chunk_cv(in, len, t, 0, out); }
+
+void orc_blake3_parent_cv(const uint32_t l[8], const uint32_t r[8], uint32_t flags, uint32_t out[8]) {
+    uint32_t tmp[8];
+    b3_parent_cv(l, r, flags, tmp);
+    memcpy(out, tmp, sizeof tmp);
+}
+
 void orc_blake3(const uint8_t* data, size_t len, uint8_t out[32]) {
     uint32_t cv[8];
     b3_subtree(data, len, 0, 1, cv);
@@ -384,6 +392,15 @@ typedef struct {
     int err;
 } orc_job;
 
+/* the baseline's BLAKE3: the scalar restatement, or the 16-way SIMD one (bw_oracle_simd.c) that
+ * mirrors the crate's hash_many backends (orc_set_blake3_simd) */
+static void (*b3_hash)(const uint8_t*, size_t, uint8_t*) = orc_blake3;
+
+int orc_set_blake3_simd(int on) {
+    b3_hash = on && orc_blake3_simd_available() ? orc_blake3_fast : orc_blake3;
+    return b3_hash == orc_blake3_fast;
+}
+
 /* dir_packer.rs:231-282 process_file + :285-311 add_file_blob (hash part) for one file */
 static int process_one_file(orc_job* j, size_t f) {
     const uint8_t* src = j->data + j->foff[f];
@@ -403,7 +420,7 @@ static int process_one_file(orc_job* j, size_t f) {
             b[i].gear_hash = h[i];
             b[i].offset = h[cap + i];
             b[i].length = h[2 * cap + i];
-            orc_blake3(src + b[i].offset, b[i].length, b[i].digest);
+            b3_hash(src + b[i].offset, b[i].length, b[i].digest);
         }
         free(h);
         j->per_file[f] = b;
@@ -412,7 +429,7 @@ static int process_one_file(orc_job* j, size_t f) {
         orc_blob* b = (orc_blob*)calloc(1, sizeof(orc_blob));
         b->file = f;
         b->length = len;
-        orc_blake3(src, len, b->digest);
+        b3_hash(src, len, b->digest);
         j->per_file[f] = b;
         j->per_file_n[f] = 1;
     }

@@ -48,6 +48,16 @@ int orc_fastcdc_chunks(const uint8_t* src, size_t len, uint32_t min, uint32_t av
                        uint64_t* out_hash, uint64_t* out_off, uint64_t* out_len, size_t cap,
                        size_t* n_out);
 void orc_blake3(const uint8_t* data, size_t len, uint8_t out[32]);
+/* tree pieces of orc_blake3 (for bw_oracle_simd.c) */
+void orc_blake3_chunk_cv(const uint8_t* in, size_t len, uint64_t t, uint32_t out[8]);
+void orc_blake3_parent_cv(const uint32_t l[8], const uint32_t r[8], uint32_t flags, uint32_t out[8]);
+/* The crate's SIMD strategy (16 chunks / parents per AVX-512 compression), bit-identical to
+ * orc_blake3; falls back to it without AVX-512 (bw_oracle_simd.c). */
+void orc_blake3_fast(const uint8_t* data, size_t len, uint8_t out[32]);
+int orc_blake3_simd_available(void);
+/* orc_process_files hashes with orc_blake3_fast (1) or orc_blake3 (0, default); returns the
+ * mode in effect. */
+int orc_set_blake3_simd(int on);
 
 orc_index* orc_index_new(const uint8_t* sorted_digests, size_t n);
 void orc_index_free(orc_index* ix);

@@ -41,6 +41,8 @@ def lib():
         L.orc_fastcdc_chunks.argtypes = [ctypes.c_void_p, ctypes.c_size_t] + [ctypes.c_uint32] * 3 + \
             [u64p, u64p, u64p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.orc_blake3.argtypes = [ctypes.c_void_p, ctypes.c_size_t, u8p]
+        L.orc_blake3_fast.argtypes = [ctypes.c_void_p, ctypes.c_size_t, u8p]
+        L.orc_set_blake3_simd.argtypes = [ctypes.c_int]
         L.orc_index_new.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
         L.orc_index_new.restype = ctypes.c_void_p
         L.orc_index_free.argtypes = [ctypes.c_void_p]
@@ -107,6 +109,23 @@ def blake3(data):
     out = (ctypes.c_uint8 * 32)()
     lib().orc_blake3(ptr, n, out)
     return bytes(out)
+
+
+def blake3_fast(data):
+    """The 16-way SIMD restatement of the crate's hash_many strategy (bit-identical to blake3)."""
+    ptr, n, keep = _buf(data)
+    out = (ctypes.c_uint8 * 32)()
+    lib().orc_blake3_fast(ptr, n, out)
+    return bytes(out)
+
+
+def simd_available():
+    return bool(lib().orc_blake3_simd_available())
+
+
+def set_blake3_simd(on):
+    """process_files hashes with the SIMD restatement (True) or the scalar one; returns the mode."""
+    return bool(lib().orc_set_blake3_simd(1 if on else 0))
 
 
 class Index:

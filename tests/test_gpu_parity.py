@@ -335,7 +335,8 @@ def test_exchange_dedup_rccl_world1(ctx, oracle):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        _exchange_world1(ctx, torch, DeviceShardOps, exchange_dedup, small_files)
+        with torch.cuda.stream(torch.cuda.Stream()):
+            _exchange_world1(ctx, torch, DeviceShardOps, exchange_dedup, small_files)
     finally:
         if owned:
             dist.destroy_process_group()
@@ -349,13 +350,12 @@ def _exchange_world1(ctx, torch, DeviceShardOps, exchange_dedup, small_files):
     ctx.index_reset()
     dev = torch.from_numpy(data).cuda()
     torch.cuda.synchronize()
-    ctx.submit_device(dev.data_ptr(), data.size, offs, lens, make_params(flags=BW_F_NO_DEDUP))
-    nb, d_dig, _ = ctx.device_views()
-    is_dup = torch.zeros(nb, dtype=torch.uint8, device="cuda")
-    exchange_dedup(DeviceShardOps(ctx, torch.device("cuda", 0)), d_dig, nb, is_dup.data_ptr(), 1,
-                   torch.device("cuda", 0))
-    torch.cuda.synchronize()
-    host = is_dup.cpu().numpy()
+    t = ctx.submit_device(dev.data_ptr(), data.size, offs, lens, make_params(flags=BW_F_NO_DEDUP))
+    d_n, d_dig, _, max_n = ctx.batch_views(t)
+    is_dup = torch.zeros(max_n, dtype=torch.uint8, device="cuda")
+    exchange_dedup(DeviceShardOps(ctx, torch.device("cuda", 0)), (d_n, d_dig, is_dup.data_ptr(), max_n), 1, max_n)
+    nb = int(ctx.wait(t).shape[0])
+    host = is_dup[:nb].cpu().numpy()
     ctx.set_stream(0)  # back to the context's own stream
     assert np.array_equal(host, want["is_dup"])
     assert host.sum() > 0

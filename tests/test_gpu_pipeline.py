@@ -270,3 +270,69 @@ def test_no_dedup_batches_leave_shared_index_alone(oracle):
             assert np.array_equal(r["digest"], want["digest"])
     finally:
         ix.close()
+
+
+def _two_rank_worker(rank, world, port, q):
+    """One rank of a 2-process exchange on the single GPU: its own context chunks + hashes its
+    share of the files (BW_F_NO_DEDUP), then the device shard ops (bucket partition, owner gate,
+    verdict scatter kernels) run with the collectives staged through host memory over gloo."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from backuwup_amd.sharded import DeviceShardOps, exchange_dedup, session_capacity, staged_all_to_all
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data, offs, lens = small_files(6000, seed=55)
+        per = len(lens) // world
+        out = []
+        with Context(0) as c, torch.cuda.stream(torch.cuda.Stream()):
+            ops = DeviceShardOps(c, torch.device("cuda", 0))
+            c.index_reset(1 << 16)
+            for batch in range(2):  # two batches per rank: batch-major, then rank-major canonical order
+                lo = (batch * world + rank) * per // 2
+                hi = lo + per // 2
+                b = _slices(data, offs, lens, [(lo, hi)])[0]
+                t_dev = torch.from_numpy(b[0]).cuda()
+                tk = c.submit_device(t_dev.data_ptr(), b[0].size, b[1], b[2], make_params(flags=BW_F_NO_DEDUP))
+                d_n, d_dig, _, max_n = c.batch_views(tk)
+                cap = session_capacity(max_n, "cpu")
+                is_dup = torch.zeros(max_n, dtype=torch.uint8, device="cuda")
+                exchange_dedup(ops, (d_n, d_dig, is_dup.data_ptr(), max_n), world, cap, all_to_all=staged_all_to_all)
+                res = c.wait(tk)
+                out.append((lo, hi, res["digest"].copy(), is_dup[:len(res)].cpu().numpy()))
+            c.index_check()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_device_shard_ops_two_ranks_one_gpu(oracle):
+    """Unmeasured on xGMI: two processes share the one GPU, gloo carries the collectives, and the
+    device kernels of the sharded exchange decide every blob exactly as one global index would."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data, offs, lens = small_files(6000, seed=55)
+    ix = oracle.Index()
+    n_checked = 0
+    for batch in range(2):
+        for r in range(2):
+            lo, hi, dig, dup = got[r][batch]
+            b = _slices(data, offs, lens, [(lo, hi)])[0]
+            want = oracle.process_files(*b, index=ix)
+            assert np.array_equal(dig, want["digest"]) and np.array_equal(dup, want["is_dup"]), (batch, r)
+            n_checked += int(want["is_dup"].sum())
+    assert n_checked > 0

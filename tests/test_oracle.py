@@ -161,3 +161,30 @@ def test_golden_generator_agrees_on_small_cases():
     for v in VEC["blake3"][:12]:
         assert mg.blake3_py(bytes(i % 251 for i in range(v["len"]))).hex() == v["digest"]
 
+
+
+def test_blake3_simd_baseline_is_bit_exact(oracle):
+    """The CPU baseline's 16-way BLAKE3 (bw_oracle_simd.c: the crate's hash_many strategy) equals
+    the scalar restatement at every tree shape: 16-chunk groups, leftover chunks, odd parent
+    levels, the 16-parent SIMD groups, counters past one group."""
+    from backuwup_amd.synth import splitmix_bytes
+    if not oracle.simd_available():
+        pytest.skip("no AVX-512 on this host (the baseline falls back to the scalar restatement)")
+    data = splitmix_bytes(99, (40 << 20) + 777)
+    lens = [0, 1, 1023, 1024, 1025, 2047, 2048, 2049, 15 * 1024, 16 * 1024, 16 * 1024 + 1, 17 * 1024,
+            31 * 1024 + 5, 32 * 1024, 33 * 1024, 64 * 1024 - 1, 257 * 1024, 262144, 1 << 20, (1 << 20) + 1,
+            3 << 20, (3 << 20) - 1, 1000 * 1024 + 3, 40 << 20]
+    for n in lens:
+        for off in (0, 3):
+            m = data[off:off + n]
+            assert oracle.blake3_fast(m) == oracle.blake3(m), (n, off)
+    # and through the batch driver, as the bench runs it
+    offs = np.array([0, 5, 5000000, 9000001], dtype=np.uint64)
+    lensb = np.array([5, 4999995, 4000001, 31 << 20], dtype=np.uint64)
+    a = oracle.process_files(data, offs, lensb)
+    try:
+        assert oracle.set_blake3_simd(True)
+        b = oracle.process_files(data, offs, lensb)
+    finally:
+        oracle.set_blake3_simd(False)
+    assert np.array_equal(a, b)

@@ -12,34 +12,45 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from backuwup_amd.sharded import exchange_dedup, owner_of
+from backuwup_amd.sharded import exchange_dedup, owner_of, session_capacity
 
 
 class CpuShardOps:
-    """Test stand-in: numpy partition / a Python set as this rank's index shard."""
+    """Test stand-in: numpy buckets / a Python set as this rank's index shard.  A batch is
+    (n, digests tensor, is_dup tensor, max_n), mirroring Context.batch_views."""
 
     def __init__(self):
         self.shard = set()
 
-    def partition(self, digests, n, world):
+    def partition(self, batch, cap, world):
+        n, digests, _, _ = batch
         d = digests.numpy().reshape(-1, 32)[:n]
         owners = np.array([owner_of(int(x[0]), world) for x in d], dtype=np.int64)
-        perm = np.argsort(owners, kind="stable")
-        counts = [int((owners == o).sum()) for o in range(world)]
-        out = torch.from_numpy(np.ascontiguousarray(d[perm]).reshape(-1).copy())
-        return out, torch.from_numpy(perm.astype(np.int64)), counts
+        buckets = np.zeros((world, cap, 32), dtype=np.uint8)
+        perm = np.zeros((world, cap), dtype=np.int64)
+        counts = np.zeros(world, dtype=np.int64)
+        for i, o in enumerate(owners):  # stable: canonical order inside each bucket
+            buckets[o, counts[o]] = d[i]
+            perm[o, counts[o]] = i
+            counts[o] += 1
+        return torch.from_numpy(buckets.reshape(-1)), torch.from_numpy(perm.reshape(-1)), torch.from_numpy(counts)
 
-    def decide(self, recv, n):
-        d = recv.numpy().reshape(-1, 32)[:n]
-        v = np.zeros(max(n, 1), dtype=np.uint8)
-        for i, x in enumerate(d):
-            k = x.tobytes()
-            v[i] = k in self.shard
-            self.shard.add(k)
-        return torch.from_numpy(v)
+    def decide(self, recv, recv_counts, world, cap):
+        b = recv.numpy().reshape(world, cap, 32)
+        v = np.zeros((world, cap), dtype=np.uint8)
+        for s in range(world):  # source-major = canonical
+            for i in range(int(recv_counts[s])):
+                k = b[s, i].tobytes()
+                v[s, i] = k in self.shard
+                self.shard.add(k)
+        return torch.from_numpy(v.reshape(-1))
 
-    def scatter(self, back, perm, n, is_dup):
-        is_dup[perm[:n]] = back[:n]
+    def scatter(self, back, perm, counts, world, cap, batch):
+        is_dup = batch[2]
+        b, p = back.numpy().reshape(world, cap), perm.numpy().reshape(world, cap)
+        for o in range(world):
+            for i in range(int(counts[o])):
+                is_dup[int(p[o, i])] = int(b[o, i])
 
 
 def make_digests(rank, batch, n):
@@ -57,7 +68,8 @@ def worker(rank, world, port, q):
         n = 100 + 37 * rank + batch
         d = make_digests(rank, batch, n)
         is_dup = torch.zeros(n, dtype=torch.uint8)
-        exchange_dedup(ops, torch.from_numpy(d.reshape(-1).copy()), n, is_dup, world, "cpu")
+        cap = session_capacity(100 + 37 * (world - 1) + 2, "cpu")
+        exchange_dedup(ops, (n, torch.from_numpy(d.reshape(-1).copy()), is_dup, n), world, cap)
         results.append(is_dup.numpy().tolist())
     q.put((rank, results))
     dist.destroy_process_group()
