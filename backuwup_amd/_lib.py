@@ -122,6 +122,8 @@ SIGNATURES = [
     ("bw_zstd_store_size", ctypes.c_uint64, [ctypes.c_uint64]),
     ("bw_pack_plan", ctypes.c_int, [u64p, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(BwPackfile),
                                     ctypes.c_uint64, u64p, u64p]),
+    ("bw_pack_plan_session", ctypes.c_int, [vp, vp, u64p, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.POINTER(BwPackfile), ctypes.c_uint64, u64p, u64p, u64p]),
     ("bw_pack_build_device", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint32,
                                             ctypes.POINTER(BwPackfile), ctypes.c_uint64, vp, vp]),
     ("bw_pack_build", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint32,

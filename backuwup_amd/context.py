@@ -370,6 +370,25 @@ class Context:
                                    ctypes.byref(total)))
         return out[:n.value], total.value
 
+    @staticmethod
+    def pack_plan_session(digests, is_dup, payload_len, flags=_lib.BW_PACK_ZSTD_STORE):
+        """The reference's write cadence over a session's blobs in canonical order (all of them,
+        duplicates included): PACKFILE_DTYPE records over the is_dup == 0 blobs, total bytes."""
+        d = np.ascontiguousarray(np.asarray(digests, dtype=np.uint8).reshape(-1, 32))
+        dup = np.ascontiguousarray(is_dup, dtype=np.uint8)
+        pl = np.ascontiguousarray(payload_len, dtype=np.uint64)
+        assert d.shape[0] == dup.size == pl.size
+        n, total, nu = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        args = [_ptr(d), _ptr(dup), pl.ctypes.data_as(_lib.u64p), pl.size, flags]
+        L = _lib.load()
+        rc = L.bw_pack_plan_session(*args, None, 0, ctypes.byref(n), ctypes.byref(total), ctypes.byref(nu))
+        if rc not in (_lib.BW_OK, _lib.BW_ENOSPC):
+            check(rc)
+        out = np.zeros(max(n.value, 1), dtype=PACKFILE_DTYPE)
+        check(L.bw_pack_plan_session(*args, out.ctypes.data_as(ctypes.POINTER(_lib.BwPackfile)), n.value,
+                                           ctypes.byref(n), ctypes.byref(total), ctypes.byref(nu)))
+        return out[:n.value], total.value
+
     def _pack_args(self, prk, src_off, src_len, hashes, kinds, nonces, plan, packfile_ids):
         so = np.ascontiguousarray(src_off, dtype=np.uint64)
         sl = np.ascontiguousarray(src_len, dtype=np.uint64)

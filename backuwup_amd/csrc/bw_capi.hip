@@ -19,6 +19,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/backuwup_gpu.h"
@@ -1327,13 +1328,15 @@ static uint64_t entry_len(uint64_t sealed, uint64_t section_off) {
     return 32 + 1 + 1 + varint_len(sealed) + varint_len(section_off);
 }
 
-static void plan_packfiles(const uint64_t* payload_len, uint64_t n, uint32_t flags, std::vector<bw_packfile>& out) {
-    uint64_t i = 0, off = 0;
-    while (i < n) {
+// write_packfiles' drain (pack.rs:123-148) over queue positions [i, to): packfiles close when their
+// blob section reaches PACKFILE_TARGET_SIZE or PACKFILE_MAX_BLOBS blobs; the last may be a remainder.
+static void plan_range(const uint64_t* payload_len, uint64_t i, uint64_t to, uint32_t flags,
+                       std::vector<bw_packfile>& out, uint64_t& off) {
+    while (i < to) {
         bw_packfile p{};
         p.first_blob = i;
         uint64_t written = 0, hdr = 0;
-        while (i < n) {
+        while (i < to) {
             const uint64_t sealed = sealed_len_of(payload_len[i], flags);
             hdr += entry_len(sealed, written);
             written += sealed + BW_BLOB_NONCE_SIZE;
@@ -1348,6 +1351,108 @@ static void plan_packfiles(const uint64_t* payload_len, uint64_t n, uint32_t fla
         off += p.size;
         out.push_back(p);
     }
+}
+
+static void plan_packfiles(const uint64_t* payload_len, uint64_t n, uint32_t flags, std::vector<bw_packfile>& out) {
+    uint64_t off = 0;
+    plan_range(payload_len, 0, n, flags, out, off);
+}
+
+// A plan is acceptable if it is what write_packfiles could have produced for this queue: packfiles
+// cover the queue in order, none closes later than the target size / blob count allows (earlier
+// is a remainder: a drain ended there), and every size and offset is consistent.
+static bool plan_valid(const uint64_t* payload_len, uint64_t n, uint32_t flags, const bw_packfile* plan, uint64_t npf,
+                       std::string& why) {
+    uint64_t next = 0, off = 0;
+    for (uint64_t p = 0; p < npf; p++) {
+        const bw_packfile& f = plan[p];
+        if (f.first_blob != next || f.n_blobs == 0 || f.n_blobs > n - next || f.offset != off) {
+            why = "packfile " + std::to_string(p) + " does not continue the queue";
+            return false;
+        }
+        uint64_t written = 0, hdr = 0;
+        for (uint64_t k = 0; k < f.n_blobs; k++) {
+            if (k && (written >= BW_PACKFILE_TARGET_SIZE || k >= BW_PACKFILE_MAX_BLOBS)) {
+                why = "packfile " + std::to_string(p) + " holds blobs past its close point";
+                return false;
+            }
+            const uint64_t sealed = sealed_len_of(payload_len[f.first_blob + k], flags);
+            hdr += entry_len(sealed, written);
+            written += sealed + BW_BLOB_NONCE_SIZE;
+        }
+        const uint64_t header_len = hdr + varint_len(f.n_blobs) + BW_SEAL_TAG_BYTES;
+        if (f.header_len != header_len || f.size != 8 + header_len + written) {
+            why = "packfile " + std::to_string(p) + " sizes do not match its blobs";
+            return false;
+        }
+        next += f.n_blobs;
+        off += f.size;
+    }
+    if (next != n) {
+        why = "the plan does not cover every blob";
+        return false;
+    }
+    return true;
+}
+
+namespace {
+struct DigestKey {
+    const uint8_t* d;
+    bool operator==(const DigestKey& o) const { return memcmp(d, o.d, 32) == 0; }
+};
+struct DigestHash {
+    size_t operator()(const DigestKey& k) const {
+        uint64_t v;
+        memcpy(&v, k.d, 8);
+        return (size_t)v;
+    }
+};
+}  // namespace
+
+extern "C" int bw_pack_plan_session(const uint8_t* digests, const uint8_t* is_dup, const uint64_t* payload_len,
+                                    uint64_t n, uint32_t flags, bw_packfile* out, uint64_t cap, uint64_t* n_out,
+                                    uint64_t* total_bytes, uint64_t* n_unique) {
+    if (!n_out || !total_bytes || (n && (!digests || !is_dup || !payload_len)) || (cap && !out)) return BW_EINVAL;
+    // the queue = the blobs the gate found new (is_dup == 0), in canonical order
+    std::vector<uint64_t> ulen;
+    std::unordered_map<DigestKey, uint64_t, DigestHash> first;  // digest -> its queue position
+    ulen.reserve(n);
+    for (uint64_t i = 0; i < n; i++)
+        if (!is_dup[i]) {
+            first.emplace(DigestKey{digests + 32 * i}, ulen.size());
+            ulen.push_back(payload_len[i]);
+        }
+    // Manager::add_blob + trigger_write_if_desired (pack.rs:31-55, 92-113) in canonical order: a
+    // copy of a blob that is still pending passes add_blob's gate and is queued too (it counts
+    // toward the trigger and is dropped when its drain reaches it); a copy of a written or seeded
+    // blob is dropped at once.  Between drains the index does not change, so the trigger's rescan
+    // of the queue is a running sum.
+    std::vector<bw_packfile> pl;
+    uint64_t off = 0, placed = 0, queued_to = 0, pend_bytes = 0, pend_cnt = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t sealed;
+        if (!is_dup[i]) {
+            sealed = sealed_len_of(ulen[queued_to++], flags);
+        } else {
+            auto it = first.find(DigestKey{digests + 32 * i});
+            if (it == first.end() || it->second < placed) continue;  // seeded or already written
+            sealed = sealed_len_of(ulen[it->second], flags);
+        }
+        pend_bytes += sealed;
+        pend_cnt++;
+        if (pend_bytes >= BW_PACKFILE_TARGET_SIZE || pend_cnt >= BW_PACKFILE_MAX_BLOBS) {
+            plan_range(ulen.data(), placed, queued_to, flags, pl, off);  // write_packfiles(true)
+            placed = queued_to;
+            pend_bytes = pend_cnt = 0;
+        }
+    }
+    plan_range(ulen.data(), placed, queued_to, flags, pl, off);  // Manager::flush
+    *n_out = pl.size();
+    *total_bytes = off;
+    if (n_unique) *n_unique = ulen.size();
+    if (pl.size() > cap) return BW_ENOSPC;
+    std::copy(pl.begin(), pl.end(), out);
+    return BW_OK;
 }
 
 extern "C" int bw_pack_plan(const uint64_t* payload_len, uint64_t n, uint32_t flags, bw_packfile* out, uint64_t cap,
@@ -1370,22 +1475,18 @@ static int pack_submit(bw_ctx* c, const uint8_t* prk, const uint8_t* d_src, cons
     if (n && (!d_src || !src_off || !src_len || !hashes || !kinds || !nonces)) return BW_EINVAL;
     if (npf && (!plan || !ids || !d_out)) return BW_EINVAL;
     hipSetDevice(c->device);
-    // the plan must be the reference's grouping of exactly these blobs
-    std::vector<bw_packfile> want;
-    plan_packfiles(src_len, n, flags, want);
-    if (want.size() != npf) return BW_EINVAL;
-    for (uint64_t p = 0; p < npf; p++) {
-        const bw_packfile &a = want[p], &b = plan[p];
-        if (a.first_blob != b.first_blob || a.n_blobs != b.n_blobs || a.offset != b.offset || a.size != b.size ||
-            a.header_len != b.header_len) {
-            c->err = "packfile plan does not match the blobs (use bw_pack_plan)";
-            return BW_EINVAL;
-        }
-        if (a.size > BW_PACKFILE_MAX_SIZE) {
+    // the plan must be a grouping write_packfiles could produce for exactly these blobs
+    // (bw_pack_plan: one drain; bw_pack_plan_session: the reference's cadence)
+    std::string why;
+    if (!plan_valid(src_len, n, flags, plan, npf, why)) {
+        c->err = "packfile plan does not match the blobs: " + why;
+        return BW_EINVAL;
+    }
+    for (uint64_t p = 0; p < npf; p++)
+        if (plan[p].size > BW_PACKFILE_MAX_SIZE) {
             c->err = "bug: violated packfile size limit";  // pack.rs:152-156 asserts
             return BW_EINVAL;
         }
-    }
     for (uint64_t i = 0; i < n; i++)
         if (kinds[i] > BW_BLOB_TREE) return BW_EINVAL;
         else if ((flags & BW_PACK_ZSTD_STORE) && src_len[i] > BW_BLOB_MAX_UNCOMPRESSED_SIZE) {

@@ -344,10 +344,21 @@ uint64_t bw_zstd_store_size(uint64_t len);
  * cap is too small; *total_bytes = the output buffer size. */
 int bw_pack_plan(const uint64_t* payload_len, uint64_t n, uint32_t flags, bw_packfile* out, uint64_t cap,
                  uint64_t* n_out, uint64_t* total_bytes);
+/* The reference's write cadence over one session (Manager::add_blob -> trigger_write_if_desired ->
+ * write_packfiles, then Manager::flush; pack.rs:31-55, 82-162): n blobs in canonical (add) order
+ * with their gate verdicts (bw_blob.is_dup) and payload lengths.  The packfiles hold the blobs with
+ * is_dup == 0 in that order (*n_unique of them; first_blob counts among them), cut where the
+ * reference cuts: a drain starts when the pending queue -- including copies of still-pending blobs,
+ * which add_blob does not catch -- reaches BW_PACKFILE_TARGET_SIZE sealed bytes or
+ * BW_PACKFILE_MAX_BLOBS blobs, and drains everything queued (its last packfile is a remainder);
+ * the final flush drains the rest.  Host only. */
+int bw_pack_plan_session(const uint8_t* digests, const uint8_t* is_dup, const uint64_t* payload_len, uint64_t n,
+                         uint32_t flags, bw_packfile* out, uint64_t cap, uint64_t* n_out, uint64_t* total_bytes,
+                         uint64_t* n_unique);
 /* Build the planned packfiles.  Blob i: payload d_src + src_off[i] (src_len[i] bytes), hashes
  * 32 B, kinds 1 B (BW_BLOB_*), nonces 12 B; packfile_ids 12 B per packfile (host arrays).
  * d_out (device, plan's total_bytes) receives the packfiles.  Asynchronous on the context
- * stream; BW_EINVAL when the plan does not match the blobs or a packfile exceeds
+ * stream; plan = bw_pack_plan's or bw_pack_plan_session's; BW_EINVAL when the plan does not match the blobs or a packfile exceeds
  * BW_PACKFILE_MAX_SIZE (the reference's assert, pack.rs:152-156). */
 int bw_pack_build_device(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* d_src, const uint64_t* src_off,
                          const uint64_t* src_len, uint64_t n, const uint8_t* hashes, const uint8_t* kinds,

@@ -140,6 +140,53 @@ def plan_packfiles(sealed_lens):
     return groups
 
 
+def session_packfiles(blobs, seeded=()):
+    """The reference's write cadence for one packer session, restated literally: blobs =
+    [(hash, sealed_len)] in add order (canonical order), seeded = hashes of prior backups.
+      add_blob (pack.rs:31-55): a hash already in the index (seeded or written to a packfile) is
+        dropped; otherwise it joins the pending queue -- even when an equal blob is still pending;
+      trigger_write_if_desired (pack.rs:92-113): rescans the queue for blobs not in the index and
+        writes once their sealed bytes reach PACKFILE_TARGET_SIZE or their count PACKFILE_MAX_BLOBS;
+      write_packfiles (pack.rs:116-162): drains the whole queue into packfiles, skipping blobs
+        that became duplicates, closing each at the target size or blob count (so the last one of
+        a drain is a remainder), adding every written blob to the index (blob_index.rs:102-114);
+      flush (pack.rs:82-90): one final write_packfiles.
+    Returns the packfiles as lists of queue hashes in write order."""
+    from collections import deque
+    index, pending, out = set(bytes(h) for h in seeded), deque(), []
+
+    def write_packfiles():
+        while pending:
+            pf, written = [], 0
+            while pending:
+                h, n = pending.popleft()
+                if h in index:
+                    continue
+                pf.append(h)
+                written += n + BLOB_NONCE_SIZE
+                index.add(h)
+                if written >= PACKFILE_TARGET_SIZE or len(pf) >= PACKFILE_MAX_BLOBS:
+                    break
+            if pf:
+                out.append(pf)
+
+    size = cnt = 0  # the trigger's rescan, kept as a running sum (the index only grows in a drain)
+    for h, n in blobs:
+        h = bytes(h)
+        if h in index:
+            continue
+        pending.append((h, int(n)))
+        size, cnt = size + int(n), cnt + 1
+        if len(pending) <= 4096:  # the literal rescan of pack.rs:100-105 where it is affordable
+            assert size == sum(b[1] for b in pending if b[0] not in index)
+            assert cnt == sum(1 for b in pending if b[0] not in index)
+        if size >= PACKFILE_TARGET_SIZE or cnt >= PACKFILE_MAX_BLOBS:
+            write_packfiles()
+            size = cnt = 0
+    write_packfiles()
+    return out
+
+
 def seal_blob_payload(prk, h, nonce, payload):
     """compress_encrypt_blob's encryption (pack.rs:70-80) of an already compressed payload."""
     return oracle.seal_blob(prk, bytes(h), bytes(nonce), bytes(payload))

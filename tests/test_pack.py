@@ -394,3 +394,77 @@ def test_two_backups_through_index_files(ctx, po):
                 assert z.decompress(payload) == want
     finally:
         c2.close()
+
+
+# ------------------------------------------------------------------ the reference's write cadence
+
+def _session_case(seed, n, n_distinct, p_seeded, size_hi, flags_store=True):
+    rng = np.random.default_rng(seed)
+    pool = rng.integers(0, 256, (n_distinct, 32), dtype=np.uint8)
+    plen = rng.integers(0, size_hi, n_distinct).astype(np.uint64)
+    pick = rng.integers(0, n_distinct, n) if n_distinct < n else np.arange(n)
+    seeded = {bytes(pool[i]) for i in range(n_distinct) if rng.random() < p_seeded}
+    return pool, plen, pick, seeded
+
+
+@pytest.mark.parametrize("seed,n,nd,ps,hi,store", [
+    (1, 3000, 2000, 0.1, 300_000, True),     # many drains, pending duplicates, seeded blobs
+    (2, 500, 60, 0.0, 2 << 20, True),        # big blobs: nearly every add triggers a drain
+    (3, 4000, 4000, 0.2, 5000, True),        # small blobs: long drains, one remainder per drain
+    (4, 250_000, 250_000, 0.05, 1, False),   # caller frames of 0 B: the blob-count trigger fires
+])
+def test_session_cadence_matches_reference(po, seed, n, nd, ps, hi, store):
+    """bw_pack_plan_session vs a literal restatement of add_blob / trigger_write_if_desired /
+    write_packfiles / flush (oracle/pack_oracle.py session_packfiles), given the gate verdicts
+    the device produces (first occurrence in canonical order, seeded digests duplicates)."""
+    from backuwup_amd import Context
+    from backuwup_amd._lib import BW_PACK_ZSTD_STORE
+    pool, plen, pick, seeded = _session_case(seed, n, nd, ps, hi)
+    digests = pool[pick]
+    seen, is_dup = set(seeded), np.zeros(n, np.uint8)
+    for i, d in enumerate(digests):
+        k = d.tobytes()
+        is_dup[i] = k in seen
+        seen.add(k)
+    payload = plen[pick]
+    flags = BW_PACK_ZSTD_STORE if store else 0
+    sealed = [(po.zstd_store_size(int(x)) if store else int(x)) + 16 for x in payload]
+    want = po.session_packfiles([(digests[i].tobytes(), sealed[i]) for i in range(n)], seeded)
+    plan, total = Context.pack_plan_session(digests, is_dup, payload, flags)
+    uniq = [digests[i].tobytes() for i in range(n) if not is_dup[i]]
+    got = [uniq[int(p["first_blob"]):int(p["first_blob"] + p["n_blobs"])] for p in plan]
+    assert got == want
+    assert sum(len(g) for g in got) == len(uniq)
+    if not store:
+        assert any(len(g) == 100_000 for g in got)
+    # sizes/offsets are write_packfiles' (the same per-packfile layout as bw_pack_plan's)
+    assert total == sum(int(p["size"]) for p in plan)
+
+
+@pytest.mark.gpu
+def test_session_cadence_packfiles_on_gpu(ctx, po):
+    """A session's blobs gated on the GPU, packed with the reference's cadence: every packfile,
+    remainders included, is byte-identical to the format oracle's serialization of the group the
+    literal cadence restatement assigns."""
+    from backuwup_amd.synth import small_files
+    data, offs, lens = small_files(1200, seed=19, lo=1000, hi=400_000)
+    ctx.index_reset()
+    res = ctx.process_files(data, offs, lens)
+    plan, total = ctx.pack_plan_session(res["digest"], res["is_dup"], res["length"])
+    u = res[res["is_dup"] == 0]
+    want = po.session_packfiles([(bytes(r["digest"]), po.zstd_store_size(int(r["length"])) + 16) for r in res])
+    assert len(plan) == len(want) and any(int(p["n_blobs"]) < 10 for p in plan)  # remainders exist
+    rng = np.random.default_rng(5)
+    nonces = rng.integers(0, 256, (len(u), 12), dtype=np.uint8)
+    ids = rng.integers(0, 256, (len(plan), 12), dtype=np.uint8)
+    src_off = offs[u["file"].astype(np.int64)] + u["offset"]
+    out = ctx.pack_build(PRK, data, src_off, u["length"], u["digest"], np.zeros(len(u), np.uint8), nonces, plan,
+                         total, ids)
+    for k, p in enumerate(plan):
+        f, c = int(p["first_blob"]), int(p["n_blobs"])
+        assert [bytes(d) for d in u["digest"][f:f + c]] == want[k]
+        blobs = [(bytes(u["digest"][i]), 0, bytes(nonces[i]),
+                  po.seal_blob_payload(PRK, u["digest"][i], nonces[i],
+                                       po.zstd_store(data[int(src_off[i]):int(src_off[i] + u["length"][i])])))
+                 for i in range(f, f + c)]
+        assert out[int(p["offset"]):int(p["offset"] + p["size"])].tobytes() == po.serialize_packfile(PRK, bytes(ids[k]), blobs)
