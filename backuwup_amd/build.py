@@ -11,32 +11,38 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libbackuwup_amd.so")
+# BW_DEBUG build: the same sources with device bounds asserts (BW_ASSERT in csrc/bw_device.h); loaded
+# only when BW_LIB points at it (tools/debug_check.py), never by the product path
+LIB_DEBUG = os.path.join(HERE, "libbackuwup_amd_debug.so")
 SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_tree.hip", "bw_seal.hip", "bw_pack.hip"]
 ARCH = os.environ.get("BW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def _stale():
-    if not os.path.exists(LIB):
+def _stale(lib=LIB):
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
     deps.append(os.path.join(HERE, "..", "include", "backuwup_gpu.h"))
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
-        return LIB
+def build(force=False, verbose=False, debug=False):
+    lib = LIB_DEBUG if debug else LIB
+    if not force and not _stale(lib):
+        return lib
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-value", "-Wno-unused-result", "-o", LIB + ".tmp"]
+           "-Wno-unused-value", "-Wno-unused-result", "-o", lib + ".tmp"]
+    if debug:
+        cmd += ["-DBW_DEBUG", "-g"]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, debug="--debug" in sys.argv))

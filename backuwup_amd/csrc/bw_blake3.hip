@@ -101,8 +101,10 @@ __global__ __launch_bounds__(256, MINW) void k_b3_groups(const uint8_t* __restri
         else hi = mid;
     }
     const uint64_t blob = lo - 1;
+    BW_ASSERT(lo >= 1 && blob < b.cap);
     const uint64_t start = b.start[blob], len = b.len[blob], gi = g - b.goff[blob];
     const uint64_t bend = start + len;
+    BW_ASSERT(bend <= b.data_len && gi * 4 * B3_LEAF_BYTES <= (len ? len - 1 : 0));
     const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
     const uint64_t first = gi * 4;
     const uint32_t k = (uint32_t)(n - first < 4 ? n - first : 4);

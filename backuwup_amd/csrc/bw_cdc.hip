@@ -466,6 +466,7 @@ struct Walker {
     const uint64_t* lgear;  // plain 256-entry table in LDS
     Masks mk;
     uint64_t trunc;         // ctr[C_TRUNC]: candidates are complete only below this position
+    uint64_t data_len;      // bytes of the batch buffer (BW_DEBUG checks)
 };
 
 // First position p in [a, hi) whose windowed gear hash passes its region's mask (mask_s below
@@ -474,6 +475,7 @@ struct Walker {
 // 64-byte window is inside the hashed range) and a >= 64.
 __device__ uint64_t direct_scan(const Walker& W, uint64_t a, uint64_t hi, uint64_t c2a) {
     const int lane = bw_lane();
+    BW_ASSERT(a >= 64 && a <= hi && hi <= W.data_len);
     // h_{a-1} from the 64 bytes before a (only its low 48 bits matter)
     uint64_t carry = bw_shfl64(bw_gear_scan(W.lgear[W.data[a - 64 + lane]]), 63);
     for (uint64_t b = a; b < hi; b += 64) {
@@ -494,6 +496,7 @@ __device__ uint64_t direct_scan(const Walker& W, uint64_t a, uint64_t hi, uint64
 // `cptr` is the wave's running index into the sorted candidate array; it only moves forward.
 __device__ uint64_t walk_next(const Walker& W, uint64_t s, uint64_t fe, uint64_t& cptr) {
     const int lane = bw_lane();
+    BW_ASSERT(s < fe && fe <= W.data_len);
     const uint64_t rem = fe - s;
     if (rem <= W.mk.min) return fe;  // cut(): remaining <= min_size -> (0, remaining)
     uint64_t center = W.mk.avg, remaining = rem;
@@ -525,6 +528,7 @@ __device__ uint64_t walk_next(const Walker& W, uint64_t s, uint64_t fe, uint64_t
         if (mb) {
             const uint64_t cut = bw_shfl64(pos, __builtin_ctzll(mb));
             cptr += (uint64_t)__popcll(below);
+            BW_ASSERT(cut > s && cut < s + remaining && cptr <= W.ncand + 64);
             return cut;
         }
         if (__ballot(pos >= hc) != 0) {  // window exhausted (also covers the array end)
@@ -613,11 +617,11 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_extend(Walker W, const
     if (lane == 0) { chain_n[j] = n; merge[j] = m; }
 }
 
-void launch_chains(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+void launch_chains(hipStream_t st, const uint8_t* data, uint64_t data_len, const Masks& mk, const uint64_t* cand,
                    const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg, uint64_t* chains,
                    uint32_t* chain_n, uint64_t* chain_cptr, uint64_t* merge, int force_serial) {
     if (!nseg || force_serial) return;
-    Walker W{data, cand, 0, nullptr, mk};
+    Walker W{data, cand, 0, nullptr, mk, 0, data_len};
     const unsigned grid = (unsigned)((nseg + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL(k_chains, dim3(grid), dim3(64 * WAVES_PER_BLOCK), 0, st, W, tile_off, ctr, segs, nseg,
                        chains, chain_n, chain_cptr);
@@ -716,7 +720,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_BLOCK) void k_fallback(Walker W, con
     }
 }
 
-void launch_resolve(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+void launch_resolve(hipStream_t st, const uint8_t* data, uint64_t data_len, const Masks& mk, const uint64_t* cand,
                     const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg,
                     const CFileDesc* cfiles, uint64_t ncf, const uint64_t* chains, const uint32_t* chain_n,
                     const uint64_t* merge, uint64_t* seg_M, uint32_t* seg_cnt, uint32_t* cf_invalid,
@@ -725,7 +729,7 @@ void launch_resolve(hipStream_t st, const uint8_t* data, const Masks& mk, const 
     hipMemsetAsync(cf_invalid, 0, ncf * sizeof(uint32_t), st);
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(BLK), 0, st, segs, nseg, cfiles, chains, chain_n, merge, seg_M,
                        seg_cnt, cf_invalid, force_serial);
-    Walker W{data, cand, 0, nullptr, mk};
+    Walker W{data, cand, 0, nullptr, mk, 0, data_len};
     const unsigned grid = (unsigned)((ncf + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL(k_fallback, dim3(grid), dim3(64 * WAVES_PER_BLOCK), 0, st, W, tile_off, ctr, cfiles, ncf,
                        cf_invalid, fb_starts, fb_count);
@@ -748,8 +752,10 @@ __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDe
     ng = 0;
     auto emit = [&](uint64_t start, uint64_t end, uint32_t kind, uint64_t fend) {
         const uint64_t len = end - start;
+        BW_ASSERT(start <= end && end <= fend && fend <= b.data_len);
         if (WRITE) {
             const uint64_t k = bbase + nb;
+            BW_ASSERT(k < b.cap);
             b.start[k] = start;
             b.len[k] = len;
             b.goff[k] = gbase + ng;

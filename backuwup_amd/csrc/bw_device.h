@@ -12,6 +12,22 @@
 
 #define BW_WAVE 64
 
+// Device bounds checks of the BW_DEBUG build (python backuwup_amd/build.py --debug ->
+// libbackuwup_amd_debug.so): a failed check prints its location and traps the kernel.
+#ifdef BW_DEBUG
+#define BW_ASSERT(c)                                                              \
+    do {                                                                          \
+        if (!(c)) {                                                               \
+            printf("BW_ASSERT failed %s:%d: %s\n", __FILE__, __LINE__, #c);       \
+            __builtin_trap();                                                     \
+        }                                                                         \
+    } while (0)
+#else
+#define BW_ASSERT(c) \
+    do {             \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------- candidate records
 // A gear candidate is a global byte position with the normalized-chunking test results in the
 // two top bits: bit 63 = (g & mask_s) == 0, bit 62 = (g & mask_l) == 0.

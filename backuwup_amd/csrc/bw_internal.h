@@ -87,6 +87,8 @@ struct BlobArrays {
     uint32_t* kind;   // 0 = whole-file blob, 1 = CDC chunk
     uint64_t* fend;   // end of the owning file (for Chunk.hash of CDC chunks)
     uint64_t* ghash;  // Chunk.hash
+    uint64_t cap;       // entries the arrays hold (BW_DEBUG checks)
+    uint64_t data_len;  // bytes of the batch buffer (BW_DEBUG checks)
 };
 
 // ------------------------------------------------------------------ launchers (bw_cdc.hip)
@@ -98,11 +100,11 @@ void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint6
                     const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots,
                     uint64_t* tile_off, uint64_t* cand, uint64_t cand_cap, uint32_t* ovf_list,
                     uint64_t* ctr, uint64_t* scratch /* >= n_tiles / 1024 + 1 entries */);
-void launch_chains(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+void launch_chains(hipStream_t st, const uint8_t* data, uint64_t data_len, const Masks& mk, const uint64_t* cand,
                    const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg,
                    uint64_t* chains, uint32_t* chain_n, uint64_t* chain_cptr, uint64_t* merge,
                    int force_serial);
-void launch_resolve(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* cand,
+void launch_resolve(hipStream_t st, const uint8_t* data, uint64_t data_len, const Masks& mk, const uint64_t* cand,
                     const uint64_t* tile_off, uint64_t* ctr, const SegDesc* segs, uint64_t nseg,
                     const CFileDesc* cfiles, uint64_t ncf, const uint64_t* chains,
                     const uint32_t* chain_n, const uint64_t* merge, uint64_t* seg_M,
