@@ -19,6 +19,20 @@ ARCH = os.environ.get("BW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
+def source_digest():
+    """sha256 over the library's sources (csrc/* and the C ABI header): identifies the kernels a
+    profile was taken with (profiles/pmc_traffic.json), so bench.py can tell stale evidence."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(os.listdir(CSRC)) + ["../../include/backuwup_gpu.h"]
+    for f in files:
+        path = os.path.normpath(os.path.join(CSRC, f))
+        if os.path.isfile(path) and not f.endswith((".tmp", ".o")):
+            h.update(f.encode())
+            h.update(open(path, "rb").read())
+    return h.hexdigest()
+
+
 def _stale(lib=LIB):
     if not os.path.exists(lib):
         return True

@@ -12,11 +12,13 @@
 //     index operation waits for the index's previous operation (an event chain), so the batches of
 //     one backup session are gated in submission order whichever stream runs them.
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -123,6 +125,12 @@ struct bw_ctx {
     bw_index* own_idx = nullptr;
     bw_index* idx = nullptr;
     uint64_t idx_mark = 0;  // idx->enq_total right after this context's last append
+
+    // host-side time of submit's phases (diagnostic: BW_HOST_TIMING=1 at bw_create prints them at
+    // bw_destroy): metadata, device buffers, metadata upload, chunk/hash launches, gate, tail
+    bool host_timing = false;
+    double host_ms[6] = {};
+    uint64_t host_batches = 0;
 
     // stage timing: two event sets, alternated per batch so recording never waits on the GPU
     bool prof = false;
@@ -417,6 +425,7 @@ extern "C" int bw_create(int device, bw_ctx** out) {
         return BW_EHIP;
     }
     c->stream = c->own;
+    c->host_timing = getenv("BW_HOST_TIMING") != nullptr;
     c->own_idx = new bw_index();
     c->idx = c->own_idx;
     if (int rc = index_init(c->own_idx, device)) {
@@ -438,6 +447,11 @@ extern "C" int bw_create(int device, bw_ctx** out) {
 
 extern "C" void bw_destroy(bw_ctx* c) {
     if (!c) return;
+    if (c->host_timing && c->host_batches)
+        fprintf(stderr, "bw host ms/batch over %llu batches: meta %.3f bufs %.3f upload %.3f launch %.3f gate %.3f tail %.3f\n",
+                (unsigned long long)c->host_batches, c->host_ms[0] / c->host_batches, c->host_ms[1] / c->host_batches,
+                c->host_ms[2] / c->host_batches, c->host_ms[3] / c->host_batches, c->host_ms[4] / c->host_batches,
+                c->host_ms[5] / c->host_batches);
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->copy) hipStreamSynchronize(c->copy);
@@ -636,6 +650,14 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         return BW_EINVAL;
     }
     hipSetDevice(c->device);
+    auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t_mark = c->host_timing ? clk() : 0;
+    auto phase = [&](int k) {
+        if (!c->host_timing) return;
+        const double t = clk();
+        c->host_ms[k] += t - t_mark;
+        t_mark = t;
+    };
     const bool force_serial = (prm->flags & BW_F_SERIAL_RESOLVE) != 0;
     const bool do_hash = !(prm->flags & BW_F_NO_HASH);
     const bool do_dedup = do_hash && !(prm->flags & BW_F_NO_DEDUP);
@@ -704,6 +726,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     const uint64_t n_tiles = ncf ? (data_len + tile_bytes - 1) / tile_bytes : 0;
 
     // ---- device buffers
+    phase(0);
     int rc = 0;
     rc |= ensure(c, c->tile_count, n_tiles * 4);
     rc |= ensure(c, c->tile_slots, n_tiles * SCAN_CAP * 8);
@@ -752,6 +775,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     if (int r2 = ensure(c, c->cand, cand_cap * 8)) return r2;
 
     // ---- metadata upload through the slot's pinned staging
+    phase(1);
     const size_t meta_bytes = nseg * sizeof(SegDesc) + ncf * sizeof(CFileDesc) + nunits * sizeof(UnitDesc) + nf * 8;
     if (s.meta_pending) {
         hipEventSynchronize(s.meta_done);
@@ -774,6 +798,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     HIPCHK(c, hipEventRecord(s.meta_done, c->stream));
     s.meta_pending = true;
     HIPCHK(c, hipMemsetAsync(s.ctr.p, 0, C_COUNT * 8, c->stream));
+    phase(2);
 
     if (c->prof) {
         c->ev_set ^= 1;
@@ -826,11 +851,13 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         HIPCHK(c, hipMemsetAsync(s.digests.p, 0, max_blobs * 32, st));
     }
     HIPCHK(c, hipEventRecord(s.input_free, st));  // no kernel of this batch reads d_data after here
+    phase(3);
     prof_mark(c, BW_STAGE_DEDUP);
     if (do_dedup) {
         if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup)))
             return r4;
     }
+    phase(4);
     prof_mark(c, BW_STAGE_PACK);
     launch_pack(st, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
                 P<uint8_t>(s.packed), max_blobs);
@@ -839,6 +866,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     HIPCHK(c, hipGetLastError());
     s.max_blobs = max_blobs;
     s.dedup = do_dedup;
+    phase(5);
+    c->host_batches += c->host_timing;
     return BW_OK;
 }
 

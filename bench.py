@@ -294,8 +294,10 @@ def main():
     algo = processed if dom == "b3_leaf" else n
     achieved = algo / (per[dom] * 1e-3) / 1e9
     kernel = {"scan": "k_scan", "b3_leaf": "k_b3_groups"}[dom]
+    traffic, traffic_src = pmc_traffic(args, kernel)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, kernel), "kernel": kernel,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": kernel,
                 "algorithmic_bytes_per_launch": algo,
                 "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
     if kernel == "k_b3_groups":
@@ -339,6 +341,9 @@ def main():
         if pack:
             line["pack"] = pack
         print(json.dumps(line), flush=True)
+    for c in ctxs:
+        c.close()
+    index.close()
     if multi:
         dist.destroy_process_group()
 
@@ -527,18 +532,28 @@ def time_pack(ctx, data, res, file_off, reps):
 
 
 def pmc_traffic(args, kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of the same workload
-    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections), or None."""
+    """(HBM bytes per launch of `kernel`, provenance) from the committed PMC summary of the same
+    workload (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections).  The bytes
+    are reported only when the summary was measured on these kernel sources (its source digest
+    equals this tree's); otherwise None and the provenance says why."""
+    from backuwup_amd.build import source_digest
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if args.workload != "c2" or args.host_stream or not os.path.exists(path):
-        return None
+        return None, None
     try:
         pmc = json.load(open(path))
-        if pmc.get("gib") == args.gib and kernel in pmc.get("kernels", {}):
-            return pmc["kernels"][kernel]["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        pass
-    return None
+    except (OSError, ValueError):
+        return None, {"file": "profiles/pmc_traffic.json", "status": "unreadable"}
+    prov = {"file": "profiles/pmc_traffic.json", "commit": pmc.get("commit"),
+            "source_digest": pmc.get("source_digest")}
+    if pmc.get("source_digest") != source_digest():
+        prov["status"] = "stale: measured on other kernel sources"
+        return None, prov
+    if pmc.get("gib") != args.gib or kernel not in pmc.get("kernels", {}):
+        prov["status"] = "no entry for this workload/kernel"
+        return None, prov
+    prov["status"] = "measured on this tree's kernels"
+    return pmc["kernels"][kernel]["hbm_bytes_per_launch"], prov
 
 
 def parity_spot_check(workload, ctx, data, file_off, file_len, rank):

@@ -16,8 +16,9 @@ for step in "$@"; do
     c3) run bench_c3 900 python bench.py --workload c3 || exit 1 ;;
     c4) run bench_c4 900 python bench.py --workload c4 || exit 1 ;;
     c5) run bench_c5 900 python bench.py --workload c5 || exit 1 ;;
+    pmc) run pmc 900 bash tools/gpu_pmc.sh || exit 1 ;;
     debug) run debug_check 600 python tools/debug_check.py || exit 1 ;;
-    exchange) run bench_exchange 600 python bench.py --exchange --no-cpu-baseline || exit 1 ;;
+    exchange) BW_HOST_TIMING=1 run bench_exchange 600 python bench.py --exchange --no-cpu-baseline || exit 1 ;;
     prof) cd /tmp && export TMPDIR=/tmp
           run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline || exit 1
           cd "$GRAFT_REPO_ROOT" ;;

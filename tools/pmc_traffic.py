@@ -2,6 +2,9 @@
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes for the bw:: kernels.
 
 Usage: pmc_traffic.py <fetch_dir> <write_dir> <gib> <out.json>
+The summary is stamped with the digest of the library sources it was measured on
+(backuwup_amd.build.source_digest) and $BW_COMMIT when set; bench.py reports the traffic only
+when the digest matches its own tree.
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE is reported in KiB and on gfx950 counts
 exactly half of the bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE (KiB)
@@ -11,7 +14,10 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def per_kernel(d, counter):
@@ -43,7 +49,9 @@ def main():
              "hbm_write_bytes_per_launch": None if wr is None else int(wr * 1024)}
         e["hbm_bytes_per_launch"] = (e["hbm_read_bytes_per_launch"] or 0) + (e["hbm_write_bytes_per_launch"] or 0)
         kernels[name] = e
+    from backuwup_amd.build import source_digest
     json.dump({"gib": gib, "note": "FETCH_SIZE x2 (gfx950 half-count) + WRITE_SIZE, KiB->bytes, mean per launch",
+               "source_digest": source_digest(), "commit": os.environ.get("BW_COMMIT"),
                "kernels": kernels}, open(path, "w"), indent=1)
     for k, e in kernels.items():
         print(k, e)
