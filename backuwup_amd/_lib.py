@@ -12,7 +12,8 @@ LIB_PATH = os.environ.get("BW_LIB") or os.path.join(HERE, "libbackuwup_amd.so")
 BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -1, -2, -3, -4, -5, -6
 BW_ECRYPTO, BW_EFORMAT = -7, -8
 BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
-BW_OPT_DEPTH, BW_OPT_SCAN_SMALL_BYTES, BW_OPT_CAND_CAP, BW_OPT_STAGE_CHUNK = 1, 2, 3, 4
+BW_OPT_DEPTH, BW_OPT_SCAN_SMALL_BYTES, BW_OPT_CAND_CAP, BW_OPT_STAGE_CHUNK, BW_OPT_B3_LOADS = 1, 2, 3, 4, 5
+BW_OPT_SCAN_WAVES, BW_OPT_LATENCY_STREAM = 6, 7
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u64p = ctypes.POINTER(ctypes.c_uint64)

@@ -24,7 +24,7 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Chaining value of one leaf (<= 1024 bytes at global position `ls`), chunk counter `t`.
 // `bend` is the end of the blob: loads never touch bytes at or beyond it except through the
 // byte-exact tail path, so a blob at the very end of the caller's buffer is safe.
-__device__ uint32_t g_b3_dummy[20];  // target of clamped (never consumed) prefetches
+__device__ uint32_t g_b3_dummy[36];  // target of clamped (never consumed) prefetches
 
 __device__ __forceinline__ void load_words(const uint32_t* src, uint32_t w[17]) {
     const u32x4_a4* q = (const u32x4_a4*)src;
@@ -80,6 +80,78 @@ __device__ __forceinline__ void b3_leaf(const uint8_t* __restrict__ data, uint64
     }
 }
 
+// The same leaf with blocks taken in pairs: one 132-byte load (both 64-byte halves of the
+// 128-byte lines it covers, requested back to back) feeds two compressions.  The per-block loop
+// above requests the second half of a line one compression (~3k cycles) after the first, by
+// which time L2 has often evicted the line (k_b3_groups fetched 1.30x its bytes).  No prefetch:
+// at 5 waves per SIMD the other waves' ~1.5k VALU instructions per pair cover the load.  Pairs
+// within 132 bytes of the blob end (and an odd last block) take the per-block path.
+__device__ __forceinline__ void load_pair_words(const uint32_t* src, uint32_t w[33]) {
+    const u32x4_a4* q = (const u32x4_a4*)src;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const u32x4_a4 v = q[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+    w[32] = src[32];
+}
+
+__device__ __forceinline__ void b3_leaf_pairs(const uint8_t* __restrict__ data, uint64_t ls, uint32_t ll, uint64_t bend,
+                                              uint64_t t, uint32_t root, uint32_t cv[8]) {
+    b3_iv(cv);
+    const uint32_t nblk = ll == 0 ? 1 : (ll + 63) / 64;
+    const uint8_t* base = data + ls;
+    const uint32_t sh = (uint32_t)((uintptr_t)base & 3);
+    const uint32_t* wb = (const uint32_t*)(base - sh);
+    uint32_t blk = 0;
+#pragma unroll 1
+    for (; blk + 1 < nblk && ls + blk * 64 + 132 <= bend; blk += 2) {
+        uint32_t w[33];
+        load_pair_words(wb + blk * 16, w);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            uint32_t m[16];
+            if (h == 1) {
+                // keep the second block's message words unformed until the first compression is done
+                // (the scheduler would otherwise build both message sets up front: +20 VGPRs)
+#pragma unroll
+                for (int i = 16; i < 33; i++) asm volatile("" : "+v"(w[i]) : "v"(cv[0]));
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_alignbyte(w[16 * h + i + 1], w[16 * h + i], sh);
+            const uint32_t b = blk + h;
+            uint32_t flags = 0;
+            if (b == 0) flags |= B3_CHUNK_START;
+            if (b == nblk - 1) flags |= B3_CHUNK_END | root;
+            b3_compress(cv, m, 64, t, flags);
+        }
+    }
+    for (; blk < nblk; blk++) {  // the leaf's last one or two blocks near the blob end
+        uint32_t w[17], m[16];
+        const uint32_t left = ll - blk * 64;
+        const uint32_t blen = ll == 0 ? 0 : (left < 64 ? left : 64);
+        if (ls + blk * 64 + 68 <= bend) {
+            load_words(wb + blk * 16, w);
+#pragma unroll
+            for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+        } else {
+            const uint8_t* p = base + blk * 64;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if ((uint32_t)(4 * i + j) < blen) v |= (uint32_t)p[4 * i + j] << (8 * j);
+                m[i] = v;
+            }
+        }
+        uint32_t flags = 0;
+        if (blk == 0) flags |= B3_CHUNK_START;
+        if (blk == nblk - 1) flags |= B3_CHUNK_END | root;
+        b3_compress(cv, m, blen, t, flags);
+    }
+}
+
 __device__ __forceinline__ void store_digest(uint8_t* out, const uint32_t cv[8]) {
     uint32_t* o = (uint32_t*)out;
 #pragma unroll
@@ -87,7 +159,8 @@ __device__ __forceinline__ void store_digest(uint8_t* out, const uint32_t cv[8])
 }
 
 // PREFETCH: block b+1's words are loaded before block b is compressed (17 more VGPRs).
-template <bool PREFETCH, int MINW>
+// PAIRS: blocks are loaded two at a time instead (b3_leaf_pairs; PREFETCH is then unused).
+template <bool PREFETCH, int MINW, bool PAIRS>
 __global__ __launch_bounds__(256, MINW) void k_b3_groups(const uint8_t* __restrict__ data, const uint64_t* ctr,
                                                    BlobArrays b, uint32_t* __restrict__ cv_buf,
                                                    uint8_t* __restrict__ digests) {
@@ -117,7 +190,8 @@ __global__ __launch_bounds__(256, MINW) void k_b3_groups(const uint8_t* __restri
         const uint64_t li = first + t, ls = start + li * B3_LEAF_BYTES;
         const uint64_t rest = len - li * B3_LEAF_BYTES;
         const uint32_t ll = len == 0 ? 0 : (uint32_t)(rest < B3_LEAF_BYTES ? rest : B3_LEAF_BYTES);
-        b3_leaf<PREFETCH>(data, ls, ll, bend, li, n == 1 ? B3_ROOT : 0, cv);
+        if (PAIRS) b3_leaf_pairs(data, ls, ll, bend, li, n == 1 ? B3_ROOT : 0, cv);
+        else b3_leaf<PREFETCH>(data, ls, ll, bend, li, n == 1 ? B3_ROOT : 0, cv);
         if (t == 0 || t == 2) {
             uint32_t (*dst)[256] = t == 0 ? s_acc : s_sv;
 #pragma unroll
@@ -281,11 +355,17 @@ __global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays
 
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
                    uint64_t max_groups, uint32_t* cv_buf, uint32_t* cv_tmp, uint8_t* digests, int max_leaves,
-                   hipEvent_t between) {
+                   hipEvent_t between, int loads, hipStream_t upper) {
     if (!max_blobs) return;
-    hipLaunchKernelGGL((k_b3_groups<true, 1>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data,
-                       ctr, b, cv_buf, digests);
+    if (loads == B3_LOADS_PAIRS)
+        hipLaunchKernelGGL((k_b3_groups<false, 1, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
+                           data, ctr, b, cv_buf, digests);
+    else
+        hipLaunchKernelGGL((k_b3_groups<true, 1, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
+                           data, ctr, b, cv_buf, digests);
     if (between) hipEventRecord(between, st);
+    if (upper != st) hipStreamWaitEvent(upper, between, 0);
+    st = upper;
     if (max_leaves > 4)
         hipLaunchKernelGGL(k_b3_small, dim3((unsigned)((max_blobs + 255) / 256)), dim3(256), 0, st, ctr, b, cv_buf,
                            digests);

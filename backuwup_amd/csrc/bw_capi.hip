@@ -103,6 +103,14 @@ struct bw_ctx {
     // options (bw_set_option)
     uint64_t scan_small_bytes = SCAN_SMALL_BYTES;
     uint64_t cand_cap_forced = 0;
+    int b3_loads = B3_LOADS_PAIRS;
+    int scan_waves = 16;
+    // latency stream: the small kernels between the two big passes (compaction, boundary
+    // resolution, assembly, upper tree levels, gate, records) on a high-priority stream, so they
+    // get CUs ahead of another batch's big kernels (BW_OPT_LATENCY_STREAM)
+    bool lat_split = false;
+    hipStream_t hi = nullptr;
+    hipEvent_t e_scan = nullptr, e_lat = nullptr, e_b3 = nullptr, e_end = nullptr;
     uint64_t cand_override = 0;  // raised when a batch found more candidates than its array held
 
     // blob sealing (bw_seal.hip): item table staging + per-item key material + piece partials
@@ -243,8 +251,8 @@ static void prof_collect(bw_ctx* c, int set) {
     c->ev_pending[set] = false;
 }
 
-static void prof_mark(bw_ctx* c, int stage) {
-    if (c->prof) hipEventRecord(c->ev[c->ev_set][stage], c->stream);
+static void prof_mark(bw_ctx* c, int stage, hipStream_t st = nullptr) {
+    if (c->prof) hipEventRecord(c->ev[c->ev_set][stage], st ? st : c->stream);
 }
 
 // ------------------------------------------------------------------ the index object
@@ -275,19 +283,21 @@ static void index_release(bw_index* x) {
 struct IndexOp {
     bw_ctx* c;
     bw_index* x;
+    hipStream_t st;
     std::lock_guard<std::mutex> lk;
-    explicit IndexOp(bw_ctx* cc) : c(cc), x(cc->idx), lk(cc->idx->mu) {
-        if (x->tail_set) hipStreamWaitEvent(c->stream, x->tail, 0);
+    explicit IndexOp(bw_ctx* cc, hipStream_t s = nullptr)
+        : c(cc), x(cc->idx), st(s ? s : cc->stream), lk(cc->idx->mu) {
+        if (x->tail_set) hipStreamWaitEvent(st, x->tail, 0);
     }
     ~IndexOp() {
-        hipEventRecord(x->tail, c->stream);
+        hipEventRecord(x->tail, st);
         x->tail_set = true;
     }
 };
 
 // Room for `incoming` more log entries (lock held).  Growth waits for every earlier operation of
 // the index (its tail) before the old buffers are replaced; sessions pre-size with bw_index_reset.
-static int index_capacity(bw_ctx* c, uint64_t incoming) {
+static int index_capacity(bw_ctx* c, uint64_t incoming, hipStream_t st) {
     bw_index* x = c->idx;
     const uint64_t need_log = x->log_hi + incoming;
     if (need_log > x->log_cap) {
@@ -300,8 +310,8 @@ static int index_capacity(bw_ctx* c, uint64_t incoming) {
         }
         nb.cap = cap * 32;
         if (x->log.p) {
-            HIPCHK(c, hipMemcpyAsync(nb.p, x->log.p, x->log_cap * 32, hipMemcpyDeviceToDevice, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipMemcpyAsync(nb.p, x->log.p, x->log_cap * 32, hipMemcpyDeviceToDevice, st));
+            HIPCHK(c, hipStreamSynchronize(st));
             hipFree(x->log.p);
         }
         x->log = nb;
@@ -312,7 +322,7 @@ static int index_capacity(bw_ctx* c, uint64_t incoming) {
         uint64_t cap = x->table_cap ? x->table_cap : 1 << 16;
         while (cap < need_log * 2) cap *= 2;
         if (x->table.p) {
-            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipStreamSynchronize(st));
             hipFree(x->table.p);
             x->table.p = nullptr;
         }
@@ -323,32 +333,33 @@ static int index_capacity(bw_ctx* c, uint64_t incoming) {
         x->table.cap = cap * 16;
         const uint64_t old = x->table_cap;
         x->table_cap = cap;
-        launch_table_clear(c->stream, P<uint64_t>(x->table), cap);
-        if (old) launch_rehash(c->stream, P<uint64_t>(x->table), cap, P<uint8_t>(x->log), P<uint64_t>(x->dstate),
+        launch_table_clear(st, P<uint64_t>(x->table), cap);
+        if (old) launch_rehash(st, P<uint64_t>(x->table), cap, P<uint8_t>(x->log), P<uint64_t>(x->dstate),
                                x->log_hi);
     }
     return BW_OK;
 }
 
-static int index_reset_locked(bw_ctx* c, uint64_t hint) {
+static int index_reset_locked(bw_ctx* c, uint64_t hint, hipStream_t st) {
     bw_index* x = c->idx;
     x->log_hi = 0;
-    HIPCHK(c, hipMemsetAsync(x->dstate.p, 0, D_COUNT * 8, c->stream));
-    if (int rc = index_capacity(c, hint ? hint : 1024)) return rc;
-    launch_table_clear(c->stream, P<uint64_t>(x->table), x->table_cap);
+    HIPCHK(c, hipMemsetAsync(x->dstate.p, 0, D_COUNT * 8, st));
+    if (int rc = index_capacity(c, hint ? hint : 1024, st)) return rc;
+    launch_table_clear(st, P<uint64_t>(x->table), x->table_cap);
     HIPCHK(c, hipGetLastError());
     return BW_OK;
 }
 
 // Append + gate n digests (n read on the device from n_dev when given; max_n bounds it).
 static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
-                        uint8_t* d_is_dup) {
-    IndexOp op(c);
+                        uint8_t* d_is_dup, hipStream_t st = nullptr) {
+    IndexOp op(c, st);
+    st = op.st;
     bw_index* x = c->idx;
     if (!x->table_cap)
-        if (int rc = index_reset_locked(c, 0)) return rc;
-    if (int rc = index_capacity(c, max_n)) return rc;
-    launch_dedup(c->stream, P<uint64_t>(x->table), x->table_cap, P<uint8_t>(x->log), P<uint64_t>(x->dstate),
+        if (int rc = index_reset_locked(c, 0, st)) return rc;
+    if (int rc = index_capacity(c, max_n, st)) return rc;
+    launch_dedup(st, P<uint64_t>(x->table), x->table_cap, P<uint8_t>(x->log), P<uint64_t>(x->dstate),
                  d_digests, n_dev, n_host, max_n, d_is_dup);
     x->log_hi += max_n;
     x->enq_total += max_n;
@@ -487,6 +498,10 @@ extern "C" void bw_destroy(bw_ctx* c) {
             if (c->ev[k][i]) hipEventDestroy(c->ev[k][i]);
     if (c->idx != c->own_idx) index_release(c->idx);
     index_release(c->own_idx);
+    if (c->hi) hipStreamSynchronize(c->hi);
+    for (hipEvent_t e : {c->e_scan, c->e_lat, c->e_b3, c->e_end})
+        if (e) hipEventDestroy(e);
+    if (c->hi) hipStreamDestroy(c->hi);
     if (c->copy) hipStreamDestroy(c->copy);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
@@ -520,6 +535,25 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             return BW_OK;
         case BW_OPT_SCAN_SMALL_BYTES: c->scan_small_bytes = v; return BW_OK;
         case BW_OPT_CAND_CAP: c->cand_cap_forced = v; return BW_OK;
+        case BW_OPT_SCAN_WAVES:
+            if (v != 8 && v != 16) return BW_EINVAL;
+            c->scan_waves = (int)v;
+            return BW_OK;
+        case BW_OPT_LATENCY_STREAM:
+            if (v && !c->hi) {
+                hipSetDevice(c->device);
+                int least = 0, greatest = 0;
+                HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+                HIPCHK(c, hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest));
+                for (hipEvent_t* e : {&c->e_scan, &c->e_lat, &c->e_b3, &c->e_end})
+                    HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+            }
+            c->lat_split = v != 0;
+            return BW_OK;
+        case BW_OPT_B3_LOADS:
+            if (v > B3_LOADS_PAIRS) return BW_EINVAL;
+            c->b3_loads = (int)v;
+            return BW_OK;
         case BW_OPT_STAGE_CHUNK:
             if (v < 4096) return BW_EINVAL;
             hipSetDevice(c->device);
@@ -569,7 +603,7 @@ extern "C" int bw_index_reset(bw_ctx* c, uint64_t hint) {
     if (!c) return BW_EINVAL;
     hipSetDevice(c->device);
     IndexOp op(c);
-    return index_reset_locked(c, hint);
+    return index_reset_locked(c, hint, c->stream);
 }
 
 extern "C" int bw_index_seed(bw_ctx* c, const uint8_t* sorted, uint64_t n) {
@@ -810,58 +844,78 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     uint64_t* ctr = P<uint64_t>(s.ctr);
     hipStream_t st = c->stream;
 
-    // ---- chunking
+    // ---- chunking (the scan on the context stream, the latency-bound kernels after it on `lat`)
+    const bool split = c->lat_split;
+    hipStream_t lat = split ? c->hi : st;
     if (ncf) {
         if (!launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
-                         P<uint32_t>(c->ovf), ctr)) {
+                         P<uint32_t>(c->ovf), ctr, c->scan_waves)) {
             c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
             return BW_EINVAL;
         }
-        prof_mark(c, BW_STAGE_COMPACT);
-        launch_compact(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
+    }
+    if (split) {
+        HIPCHK(c, hipEventRecord(c->e_scan, st));
+        HIPCHK(c, hipStreamWaitEvent(lat, c->e_scan, 0));
+    }
+    prof_mark(c, BW_STAGE_COMPACT, lat);
+    if (ncf)
+        launch_compact(lat, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
                        P<uint64_t>(c->tile_off), P<uint64_t>(c->cand), cand_cap, P<uint32_t>(c->ovf), ctr,
                        P<uint64_t>(c->tile_btot));
-        prof_mark(c, BW_STAGE_RESOLVE);
-        launch_chains(st, d_data, data_len, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs), nseg,
-                      P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->chain_cptr),
+    prof_mark(c, BW_STAGE_RESOLVE, lat);
+    if (ncf) {
+        launch_chains(lat, d_data, data_len, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs),
+                      nseg, P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->chain_cptr),
                       P<uint64_t>(c->merge), force_serial);
-        launch_resolve(st, d_data, data_len, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs), nseg,
-                       P<CFileDesc>(c->cfiles), ncf, P<uint64_t>(c->chains), P<uint32_t>(c->chain_n),
-                       P<uint64_t>(c->merge), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
+        launch_resolve(lat, d_data, data_len, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr,
+                       P<SegDesc>(c->segs), nseg, P<CFileDesc>(c->cfiles), ncf, P<uint64_t>(c->chains),
+                       P<uint32_t>(c->chain_n), P<uint64_t>(c->merge), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
                        P<uint32_t>(c->cf_invalid), P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), force_serial);
-    } else {
-        prof_mark(c, BW_STAGE_COMPACT);
-        prof_mark(c, BW_STAGE_RESOLVE);
     }
-    prof_mark(c, BW_STAGE_ASSEMBLE);
-    launch_assemble(st, ctr, P<UnitDesc>(c->units), nunits, P<SegDesc>(c->segs), P<CFileDesc>(c->cfiles),
+    prof_mark(c, BW_STAGE_ASSEMBLE, lat);
+    launch_assemble(lat, ctr, P<UnitDesc>(c->units), nunits, P<SegDesc>(c->segs), P<CFileDesc>(c->cfiles),
                     P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->seg_M), P<uint32_t>(c->cf_invalid),
                     P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), b, P<uint64_t>(c->ucnt),
                     P<uint64_t>(c->ubtot));
-    if (ncf) launch_cut_hash(st, d_data, mk, ctr, b, max_blobs);
-    else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, st));
+    if (ncf) launch_cut_hash(lat, d_data, mk, ctr, b, max_blobs);
+    else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, lat));
+    if (split) {
+        HIPCHK(c, hipEventRecord(c->e_lat, lat));
+        HIPCHK(c, hipStreamWaitEvent(st, c->e_lat, 0));
+    }
 
-    // ---- hashing + dedup
-    prof_mark(c, BW_STAGE_B3LEAF);
+    // ---- hashing (the leaf pass on the context stream, the upper levels on lat) + dedup on lat
+    prof_mark(c, BW_STAGE_B3LEAF, st);
     if (do_hash) {
+        hipEvent_t between = c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : (split ? c->e_b3 : nullptr);
         launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint32_t>(c->cv2),
-                      P<uint8_t>(s.digests), max_leaves, c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : nullptr);
+                      P<uint8_t>(s.digests), max_leaves, between, c->b3_loads, lat);
     } else {
-        prof_mark(c, BW_STAGE_B3TREE);
-        HIPCHK(c, hipMemsetAsync(s.digests.p, 0, max_blobs * 32, st));
+        prof_mark(c, BW_STAGE_B3TREE, st);
+        if (split) {
+            HIPCHK(c, hipEventRecord(c->e_b3, st));
+            HIPCHK(c, hipStreamWaitEvent(lat, c->e_b3, 0));
+        }
+        HIPCHK(c, hipMemsetAsync(s.digests.p, 0, max_blobs * 32, lat));
     }
     HIPCHK(c, hipEventRecord(s.input_free, st));  // no kernel of this batch reads d_data after here
     phase(3);
-    prof_mark(c, BW_STAGE_DEDUP);
+    prof_mark(c, BW_STAGE_DEDUP, lat);
     if (do_dedup) {
-        if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup)))
+        if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup), lat))
             return r4;
     }
     phase(4);
-    prof_mark(c, BW_STAGE_PACK);
-    launch_pack(st, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
+    prof_mark(c, BW_STAGE_PACK, lat);
+    launch_pack(lat, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
                 P<uint8_t>(s.packed), max_blobs);
-    prof_mark(c, BW_N_STAGES);
+    if (split) {  // the batch ends on the context stream (the caller's order)
+        prof_mark(c, BW_N_STAGES, lat);
+        HIPCHK(c, hipEventRecord(c->e_end, lat));
+        HIPCHK(c, hipStreamWaitEvent(st, c->e_end, 0));
+    }
+    if (!split) prof_mark(c, BW_N_STAGES);
     if (c->prof) c->ev_pending[c->ev_set] = true;
     HIPCHK(c, hipGetLastError());
     s.max_blobs = max_blobs;

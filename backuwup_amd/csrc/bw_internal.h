@@ -95,7 +95,7 @@ struct BlobArrays {
 // returns false (nothing launched) when mk.tile_shift names no compiled tile size
 bool launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
                  const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf_list,
-                 uint64_t* ctr);
+                 uint64_t* ctr, int waves /* 16 or 8 per block */);
 void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles,
                     const Masks& mk, uint32_t* tile_count, uint64_t* tile_slots,
                     uint64_t* tile_off, uint64_t* cand, uint64_t cand_cap, uint32_t* ovf_list,
@@ -119,10 +119,13 @@ void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const
                      BlobArrays b, uint64_t max_blobs);
 
 // ------------------------------------------------------------------ launchers (bw_blake3.hip)
+// how k_b3_groups feeds its compressions: one 64-byte block ahead (prefetch) or block pairs
+enum { B3_LOADS_PREFETCH = 0, B3_LOADS_PAIRS = 1 };
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b,
                    uint64_t max_blobs, uint64_t max_groups, uint32_t* cv_buf,
                    uint32_t* cv_tmp /* like cv_buf */, uint8_t* digests, int max_leaves,
-                   hipEvent_t between /* may be null */);
+                   hipEvent_t between /* may be null */, int loads,
+                   hipStream_t upper /* stream of the upper tree levels; `between` must order it */);
 
 // ------------------------------------------------------------------ launchers (bw_dedup.hip)
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),

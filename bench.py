@@ -111,6 +111,10 @@ def main():
     ap.add_argument("--pack", action="store_true",
                     help="also time packing the last batch's unique blobs into packfiles: zstd store frames, "
                          "per-blob + header AES-256-GCM, packfile layout (§8f rows 2-4)")
+    ap.add_argument("--b3-loads", type=int, default=None, choices=[0, 1],
+                    help="k_b3_groups loads (BW_OPT_B3_LOADS): 0 = one block ahead, 1 = block pairs")
+    ap.add_argument("--scan-waves", type=int, default=None, choices=[8, 16], help="BW_OPT_SCAN_WAVES")
+    ap.add_argument("--latency-stream", type=int, default=None, choices=[0, 1], help="BW_OPT_LATENCY_STREAM")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
@@ -128,7 +132,8 @@ def main():
     import torch.distributed as dist
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
-    from backuwup_amd._lib import BW_F_NO_DEDUP, BW_OPT_DEPTH, STAGES
+    from backuwup_amd._lib import (BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM,
+                                   BW_OPT_SCAN_WAVES, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -164,6 +169,12 @@ def main():
         st = torch.cuda.Stream(dev)
         c.set_stream(st.cuda_stream)
         c.attach_index(index)
+        if args.b3_loads is not None:
+            c.set_option(BW_OPT_B3_LOADS, args.b3_loads)
+        if args.scan_waves is not None:
+            c.set_option(BW_OPT_SCAN_WAVES, args.scan_waves)
+        if args.latency_stream is not None:
+            c.set_option(BW_OPT_LATENCY_STREAM, args.latency_stream)
         if args.host_stream and nctx > 1:
             c.set_option(BW_OPT_DEPTH, 1)  # contexts alternate: one HBM input buffer each is enough
         ctxs.append(c)

@@ -336,3 +336,34 @@ def test_device_shard_ops_two_ranks_one_gpu(oracle):
             assert np.array_equal(dig, want["digest"]) and np.array_equal(dup, want["is_dup"]), (batch, r)
             n_checked += int(want["is_dup"].sum())
     assert n_checked > 0
+
+
+@pytest.mark.parametrize("scan_waves,latency,loads", [(8, 0, 1), (16, 1, 1), (8, 1, 0), (16, 0, 0)])
+def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads):
+    """The scheduling variants (8-wave scan blocks, the high-priority latency stream, both BLAKE3
+    load modes) change only where and when kernels run: results equal the oracle, including two
+    batches in flight on two contexts that share an index."""
+    import torch
+    from backuwup_amd._lib import BW_OPT_B3_LOADS, BW_OPT_LATENCY_STREAM, BW_OPT_SCAN_WAVES
+    data, offs, lens = tree_corpus(80 << 20, seed=21, max_file=20 << 20)
+    batches = _slices(data, offs, lens, [(0, len(lens) // 2), (len(lens) // 2, len(lens))]) * 2
+    want = oracle_session(oracle, batches)
+    devs = [torch.from_numpy(d).cuda() for d, _, _ in batches[:2]] * 2
+    torch.cuda.synchronize()
+    ix = Index(0)
+    cs = [Context(0), Context(0)]
+    try:
+        for c in cs:
+            c.set_stream(torch.cuda.Stream().cuda_stream)
+            c.attach_index(ix)
+            c.set_option(BW_OPT_SCAN_WAVES, scan_waves)
+            c.set_option(BW_OPT_LATENCY_STREAM, latency)
+            c.set_option(BW_OPT_B3_LOADS, loads)
+        cs[0].index_reset()
+        tickets = [cs[k % 2].submit_device(t.data_ptr(), d.size, o, l) for k, (t, (d, o, l)) in enumerate(zip(devs, batches))]
+        for k, t in enumerate(tickets):
+            blobs_equal(cs[k % 2].wait(t), want[k], k)
+    finally:
+        for c in cs:
+            c.close()
+        ix.close()
