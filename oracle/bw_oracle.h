@@ -88,6 +88,11 @@ void orc_seal_blob(const uint8_t prk[32], const uint8_t* info, size_t info_len, 
 int orc_open_blob(const uint8_t prk[32], const uint8_t* info, size_t info_len, const uint8_t nonce[12],
                   const uint8_t* sealed, size_t len_with_tag, uint8_t* out);
 
+/* ---- zstd level 3 (bw_oracle_zstd.c): pack.rs:58-64 ---- */
+void bwo_zstd3_params(size_t n, unsigned out[4]);  /* wlog, small-hash log, long-hash log, mls */
+size_t bwo_zstd3_bound(size_t n);
+size_t bwo_zstd3_compress(const uint8_t* src, size_t n, uint8_t* dst);
+
 #ifdef __cplusplus
 }
 #endif

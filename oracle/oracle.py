@@ -62,6 +62,11 @@ def lib():
                                         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                         ctypes.POINTER(OrcBlob), ctypes.c_size_t,
                                         ctypes.POINTER(ctypes.c_size_t)]
+        L.bwo_zstd3_params.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint)]
+        L.bwo_zstd3_bound.argtypes = [ctypes.c_size_t]
+        L.bwo_zstd3_bound.restype = ctypes.c_size_t
+        L.bwo_zstd3_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.bwo_zstd3_compress.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -270,3 +275,20 @@ def seal_blob(prk, info, nonce, payload):
 
 def open_blob(prk, info, nonce, sealed):
     return gcm_open(hkdf_expand32(prk, info), nonce, sealed)
+
+
+# ---- zstd level 3 (bw_oracle_zstd.c; pack.rs:58-64) ----
+def zstd3_params(n):
+    """(window log, small-hash log, long-hash log, min match) of level 3 for an n-byte blob."""
+    out = (ctypes.c_uint * 4)()
+    lib().bwo_zstd3_params(n, out)
+    return tuple(out)
+
+
+def zstd3_compress(data):
+    """The magicless level-3 frame the reference's Compressor writes for one blob."""
+    data = bytes(data)
+    L = lib()
+    out = ctypes.create_string_buffer(L.bwo_zstd3_bound(len(data)))
+    n = L.bwo_zstd3_compress(data, len(data), out)
+    return out.raw[:n]
