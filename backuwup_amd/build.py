@@ -14,7 +14,7 @@ LIB = os.path.join(HERE, "libbackuwup_amd.so")
 # BW_DEBUG build: the same sources with device bounds asserts (BW_ASSERT in csrc/bw_device.h); loaded
 # only when BW_LIB points at it (tools/debug_check.py), never by the product path
 LIB_DEBUG = os.path.join(HERE, "libbackuwup_amd_debug.so")
-SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_tree.hip", "bw_seal.hip", "bw_pack.hip"]
+SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_tree.hip", "bw_seal.hip", "bw_pack.hip", "bw_zstd.hip"]
 ARCH = os.environ.get("BW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

@@ -221,6 +221,38 @@ class Context:
         check(self._L.bw_seal_device(*args), self.h)
         return None
 
+    # -------------------------------------------------------------- zstd level 3 (§8f row 2)
+    def zstd_compress(self, blobs):
+        """Per-blob zstd level 3 as Manager::compress_encrypt_blob runs it (pack.rs:58-64): a
+        list of bytes-like blobs (each <= 3 MiB) -> the list of their magicless frames."""
+        lens = np.array([len(b) for b in blobs], dtype=np.uint64)
+        so = np.zeros(len(blobs), dtype=np.uint64)
+        if len(blobs) > 1:
+            so[1:] = np.cumsum(lens[:-1])
+        src = np.frombuffer(b"".join(bytes(b) for b in blobs) or b"\0", dtype=np.uint8)
+        cap = np.array([self._L.bw_zstd_store_size(int(x)) for x in lens], dtype=np.uint64)
+        do = np.zeros(len(blobs), dtype=np.uint64)
+        if len(blobs) > 1:
+            do[1:] = np.cumsum(cap[:-1])
+        out = np.zeros(max(int(cap.sum()), 1), dtype=np.uint8)
+        fl = np.zeros(len(blobs), dtype=np.uint64)
+        check(self._L.bw_zstd_compress(self.h, _ptr(src), so.ctypes.data_as(_lib.u64p), lens.ctypes.data_as(_lib.u64p),
+                                       len(blobs), _ptr(out), do.ctypes.data_as(_lib.u64p),
+                                       fl.ctypes.data_as(_lib.u64p)), self.h)
+        return [out[int(do[i]):int(do[i] + fl[i])].tobytes() for i in range(len(blobs))]
+
+    def zstd_compress_device(self, d_src, src_off, src_len, d_dst, dst_off):
+        """Device pointers (ints); frames at dst_off (each with room for bw_zstd_store_size);
+        returns the frame lengths (synchronous)."""
+        so = np.ascontiguousarray(src_off, dtype=np.uint64)
+        sl = np.ascontiguousarray(src_len, dtype=np.uint64)
+        do = np.ascontiguousarray(dst_off, dtype=np.uint64)
+        fl = np.zeros(so.size, dtype=np.uint64)
+        check(self._L.bw_zstd_compress_device(self.h, ctypes.c_void_p(d_src), so.ctypes.data_as(_lib.u64p),
+                                              sl.ctypes.data_as(_lib.u64p), so.size, ctypes.c_void_p(d_dst),
+                                              do.ctypes.data_as(_lib.u64p), fl.ctypes.data_as(_lib.u64p)), self.h)
+        return fl
+
     # -------------------------------------------------------------- index
     def index_reset(self, capacity_hint=0):
         check(self._L.bw_index_reset(self.h, capacity_hint), self.h)

@@ -129,6 +129,10 @@ struct bw_ctx {
     // many small messages (tree blobs): pinned staging of the serialized bytes
     PinBuf msg_stage;
 
+    // per-blob zstd level 3 (bw_zstd.hip): hash-table slots and scratch; zs_io = host-call staging
+    ZstdWork* zw = nullptr;
+    DevBuf zs_io;
+
     // dedup index: `idx` is `own` unless the context is attached to a shared one
     bw_index* own_idx = nullptr;
     bw_index* idx = nullptr;
@@ -472,8 +476,10 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->fstart,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
-                     &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v};
+                     &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io};
     for (DevBuf* b : all) free_dev(*b);
+    zstd_work_free(c->zw);
+    c->zw = nullptr;
     for (Slot& s : c->slots) {
         free_dev(s.ctr);
         free_dev(s.digests);
@@ -549,6 +555,16 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
                     HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
             }
             c->lat_split = v != 0;
+            return BW_OK;
+        case BW_OPT_ZSTD_SLOTS:
+            if (v < 1 || v > (1u << 20)) return BW_EINVAL;
+            hipSetDevice(c->device);
+            hipStreamSynchronize(c->stream);
+            zstd_work_limits(c->zw, v, 0);
+            return BW_OK;
+        case BW_OPT_ZSTD_BATCH_BYTES:
+            if (v < (1u << 20)) return BW_EINVAL;
+            zstd_work_limits(c->zw, 0, v);
             return BW_OK;
         case BW_OPT_B3_LOADS:
             if (v > B3_LOADS_PAIRS) return BW_EINVAL;
@@ -1396,6 +1412,40 @@ extern "C" int bw_open(bw_ctx* c, const uint8_t prk[32], const uint8_t* src, con
 // Manager::write_packfiles / serialize_packfile (pack.rs:115-227); kernels in bw_pack.hip.
 
 static uint32_t varint_len(uint64_t v) { return v < 251 ? 1 : (v < (1ull << 16) ? 3 : (v < (1ull << 32) ? 5 : 9)); }
+
+// ------------------------------------------------------------------ zstd level 3
+
+extern "C" int bw_zstd_compress_device(bw_ctx* c, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
+                                       uint64_t n, uint8_t* d_dst, const uint64_t* dst_off, uint64_t* frame_len) {
+    if (!c || (n && (!d_src || !src_off || !src_len || !d_dst || !dst_off || !frame_len))) return BW_EINVAL;
+    hipSetDevice(c->device);
+    return zstd_compress(c->stream, c->zw, d_src, src_off, src_len, n, d_dst, dst_off, frame_len, c->err);
+}
+
+extern "C" int bw_zstd_compress(bw_ctx* c, const uint8_t* src, const uint64_t* src_off, const uint64_t* src_len, uint64_t n,
+                                uint8_t* dst, const uint64_t* dst_off, uint64_t* frame_len) {
+    if (!c || (n && (!src || !src_off || !src_len || !dst || !dst_off || !frame_len))) return BW_EINVAL;
+    hipSetDevice(c->device);
+    // inputs packed back to back on the device, frames at their store-frame capacity
+    std::vector<uint64_t> so(n), fo(n);
+    uint64_t in = 0, out = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (src_len[i] > 3ull * 1024 * 1024) return BW_EINVAL;
+        so[i] = in;
+        in += (src_len[i] + 15) & ~15ull;
+        fo[i] = out;
+        out += bw_zstd_store_size(src_len[i]);
+    }
+    if (int rc = ensure(c, c->zs_io, in + out + 16)) return rc;
+    uint8_t* io = P<uint8_t>(c->zs_io);
+    for (uint64_t i = 0; i < n; i++)
+        if (src_len[i]) HIPCHK(c, hipMemcpyAsync(io + so[i], src + src_off[i], src_len[i], hipMemcpyHostToDevice, c->stream));
+    if (int rc = zstd_compress(c->stream, c->zw, io, so.data(), src_len, n, io + in, fo.data(), frame_len, c->err)) return rc;
+    for (uint64_t i = 0; i < n; i++)
+        HIPCHK(c, hipMemcpyAsync(dst + dst_off[i], io + in + fo[i], frame_len[i], hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BW_OK;
+}
 
 extern "C" uint64_t bw_zstd_store_size(uint64_t len) {
     const uint64_t nb = len ? (len + ZSTD_BLOCK - 1) / ZSTD_BLOCK : 1;

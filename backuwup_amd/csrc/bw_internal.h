@@ -1,6 +1,7 @@
 // bw_internal.h -- host-side declarations shared by the backuwup_amd translation units.
 #pragma once
 #include <algorithm>
+#include <string>
 #include <thread>
 #include <vector>
 #include <hip/hip_runtime.h>
@@ -244,5 +245,13 @@ void launch_index_parse(hipStream_t st, const uint8_t* pt, const uint64_t* pt_of
                         uint64_t n_files, uint64_t* parsed);
 void launch_index_gather(hipStream_t st, const uint8_t* pt, const uint64_t* file_rec0, const uint64_t* file_src,
                          uint64_t n_files, uint64_t n_rec, uint8_t* digests, uint8_t* records);
+
+// ------------------------------------------------------------------ zstd level 3 (bw_zstd.hip)
+struct ZstdWork;
+void zstd_work_free(ZstdWork* w);
+void zstd_work_limits(ZstdWork*& w, uint64_t max_slots, uint64_t max_bytes);
+// frames of n blobs (device buffers, host offset tables); synchronous on st; frame_len is host
+int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
+                  uint64_t n, uint8_t* d_dst, const uint64_t* dst_off, uint64_t* frame_len, std::string& err);
 
 }  // namespace bw

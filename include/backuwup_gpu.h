@@ -158,7 +158,9 @@ enum {
     BW_OPT_STAGE_CHUNK = 4,      /* pinned staging chunk for pageable bw_submit_host input (64 MiB)  */
     BW_OPT_B3_LOADS = 5,         /* k_b3_groups loads: 0 = one block ahead, 1 = block pairs (default) */
     BW_OPT_SCAN_WAVES = 6,       /* gear-scan workgroup: 16 waves (default) or 8 (leaves LDS for BLAKE3) */
-    BW_OPT_LATENCY_STREAM = 7    /* 1: the small kernels between the passes on a high-priority stream */
+    BW_OPT_LATENCY_STREAM = 7,   /* 1: the small kernels between the passes on a high-priority stream */
+    BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (768 KiB of hash tables each; 16384) */
+    BW_OPT_ZSTD_BATCH_BYTES = 9  /* bw_zstd_*: input bytes per internal batch (~4.2x in scratch; 8 GiB) */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 
@@ -340,6 +342,20 @@ typedef struct bw_packfile {
     uint64_t size;       /* 8 + header_len + blob section                            */
     uint64_t header_len; /* encrypted header bytes (the u64 LE prefix)                */
 } bw_packfile;
+
+/* ---- per-blob zstd level 3 ----
+ * Manager::compress_encrypt_blob's compression (pack.rs:58-64): for every blob, the frame
+ * zstd::bulk::Compressor::new(3) writes with include_checksum(false), include_contentsize(false),
+ * include_magicbytes(false) -- byte for byte the level-3 output of libzstd's dfast compressor
+ * (pinned against the system libzstd 1.4.8; the reference links 1.5.5).
+ * Blob i: src + src_off[i] (src_len[i] <= 3 MiB, else BW_EINVAL like add_blob's BlobTooLarge,
+ * pack.rs:32-34); its frame goes to dst + dst_off[i], which must hold bw_zstd_store_size(src_len[i])
+ * bytes (level 3 never writes more); frame_len[i] (host) = the frame's size.  Synchronous. */
+int bw_zstd_compress_device(bw_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
+                            uint64_t n, uint8_t* d_dst, const uint64_t* dst_off, uint64_t* frame_len);
+/* Same over host buffers (staged through the device). */
+int bw_zstd_compress(bw_ctx* ctx, const uint8_t* src, const uint64_t* src_off, const uint64_t* src_len, uint64_t n,
+                     uint8_t* dst, const uint64_t* dst_off, uint64_t* frame_len);
 
 /* Size of the zstd store frame of a len-byte blob. */
 uint64_t bw_zstd_store_size(uint64_t len);

@@ -68,3 +68,71 @@ def test_random_data_gives_the_store_frame(oracle):
     for n in (0, 1, 100, 131072, 131073, 1 << 20, 3 << 20):
         data = zstd_corpus.blob("random", n, n)
         assert oracle.zstd3_compress(data) == po.zstd_store(data)
+
+
+# ------------------------------------------------------------------ GPU (bw_zstd.hip) vs the oracle
+SIZES_GPU = [0, 1, 6, 7, 8, 63, 64, 65, 200, 255, 256, 1000, 1023, 1024, 4096, 16383, 16384, 16385, 70000,
+             131071, 131072, 131073, 262144, 262145, 700000, 2 * 1024 * 1024 + 4096, 3 * 1024 * 1024]
+
+
+def _check_frames(oracle, blobs, frames, z=None):
+    for i, (d, f) in enumerate(zip(blobs, frames)):
+        want = oracle.zstd3_compress(d)
+        assert f == want, (i, len(d), len(f), len(want))
+        if z is not None:
+            assert z.decompress(f) == bytes(d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", zstd_corpus.KINDS)
+def test_gpu_zstd_equals_oracle(ctx, oracle, kind):
+    blobs = [zstd_corpus.blob(kind, n, i) for i, n in enumerate(SIZES_GPU)]
+    frames = ctx.zstd_compress(blobs)
+    import zstd_ref
+    _check_frames(oracle, blobs, frames, zstd_ref if zstd_ref.available() else None)
+
+
+@pytest.mark.gpu
+def test_gpu_zstd_many_mixed_blobs_small_batches(oracle):
+    """Hundreds of blobs of every kind in one call, split into internal batches of at most 7 blobs
+    / 1 MiB (hash-table slots reused across batches through their index bases)."""
+    from backuwup_amd import Context, _lib
+    rng = np.random.default_rng(11)
+    blobs = []
+    for i in range(240):
+        kind = zstd_corpus.KINDS[int(rng.integers(len(zstd_corpus.KINDS)))]
+        n = int(rng.choice([rng.integers(0, 300), rng.integers(300, 20000), rng.integers(20000, 300000)]))
+        blobs.append(zstd_corpus.blob(kind, n, 1000 + i))
+    with Context(0) as c:
+        c.set_option(_lib.BW_OPT_ZSTD_SLOTS, 7)
+        c.set_option(_lib.BW_OPT_ZSTD_BATCH_BYTES, 1 << 20)
+        f1 = c.zstd_compress(blobs)
+        f2 = c.zstd_compress(blobs[::-1])  # the same slots again, at higher index bases
+    _check_frames(oracle, blobs, f1)
+    _check_frames(oracle, blobs[::-1], f2)
+
+
+@pytest.mark.gpu
+def test_gpu_zstd_device_buffers(ctx, oracle):
+    import torch
+    blobs = [zstd_corpus.blob(k, 3 * 1024 * 1024 - 5 * i, 77 + i) for i, k in enumerate(zstd_corpus.KINDS)]
+    lens = np.array([len(b) for b in blobs], dtype=np.uint64)
+    so = np.concatenate([[0], np.cumsum(lens + 16)[:-1]]).astype(np.uint64)
+    host = np.zeros(int(so[-1] + lens[-1]), dtype=np.uint8)
+    for o, b in zip(so, blobs):
+        host[int(o):int(o) + len(b)] = np.frombuffer(b, np.uint8)
+    d_src = torch.from_numpy(host).cuda()
+    cap = np.array([ctx._L.bw_zstd_store_size(int(x)) for x in lens], dtype=np.uint64)
+    do = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.uint64)
+    d_dst = torch.zeros(int(cap.sum()), dtype=torch.uint8, device="cuda")
+    fl = ctx.zstd_compress_device(d_src.data_ptr(), so, lens, d_dst.data_ptr(), do)
+    out = d_dst.cpu().numpy()
+    frames = [out[int(do[i]):int(do[i] + fl[i])].tobytes() for i in range(len(blobs))]
+    _check_frames(oracle, blobs, frames)
+
+
+@pytest.mark.gpu
+def test_gpu_zstd_rejects_blob_over_3mib(ctx):
+    from backuwup_amd._lib import BwError
+    with pytest.raises(BwError):
+        ctx.zstd_compress([bytes(3 * 1024 * 1024 + 1)])
