@@ -406,6 +406,10 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                                                  uint64_t* __restrict__ seqs, const uint32_t* __restrict__ active) {
     const uint32_t bi = active ? active[blockIdx.x] : blockIdx.x;
     const uint32_t lane = threadIdx.x;
+    constexpr uint32_t DUP_SLOTS = 512;
+    __shared__ unsigned long long s_mL[DUP_SLOTS], s_mS[DUP_SLOTS];
+    for (uint32_t i = lane; i < DUP_SLOTS; i += 64) { s_mL[i] = 0; s_mS[i] = 0; }
+    __builtin_amdgcn_wave_barrier();
     const ZBlob B = blobs[bi];
     const uint8_t* s = src + B.src;
     uint32_t* hl = tables + (uint64_t)B.slot * SLOT_WORDS;
@@ -436,6 +440,7 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 __threadfence_block();
                 // this lane's position in the skip sequence ip += ((ip - anchor) >> 8) + 1
                 uint32_t d = ip - anchor, j = lane;
+                if (d + 63 < 256) { d += j; j = 0; }  // step 1 for every lane: no divisions
                 while (j) {
                     const uint32_t q = d >> 8, st = q + 1;
                     const uint32_t stay = (((q + 1) << 8) - d + st - 1) / st;
@@ -460,9 +465,24 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 const uint64_t vmask = __ballot(valid);
                 const uint32_t nvalid = (uint32_t)__popcll(vmask);
                 // writes of earlier lanes to the same slots reach this lane's probes (the serial
-                // loop writes every visited position before it moves on)
+                // loop writes every visited position before it moves on).  Only lanes whose hash
+                // shares a bucket of a small LDS map with another lane can be involved: each lane
+                // ORs its bit into its two buckets, and the exact forwarding runs over the lanes
+                // of shared buckets only (~15 of 64; the map is cleared behind itself).
                 uint32_t nextL = 64, nextS = 64;
-                for (uint32_t jj = 0; jj < nvalid; jj++) {
+                uint64_t mL = 0, mS = 0;
+                if (valid) {
+                    atomicOr(&s_mL[h2 & (DUP_SLOTS - 1)], 1ull << lane);
+                    atomicOr(&s_mS[h & (DUP_SLOTS - 1)], 1ull << lane);
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (valid) { mL = s_mL[h2 & (DUP_SLOTS - 1)]; mS = s_mS[h & (DUP_SLOTS - 1)]; }
+                __builtin_amdgcn_wave_barrier();
+                if (valid) { s_mL[h2 & (DUP_SLOTS - 1)] = 0; s_mS[h & (DUP_SLOTS - 1)] = 0; }
+                __builtin_amdgcn_wave_barrier();
+                uint64_t shared = __ballot(valid && ((mL & (mL - 1)) | (mS & (mS - 1))) != 0);
+                for (; shared; shared &= shared - 1) {
+                    const uint32_t jj = (uint32_t)__builtin_ctzll(shared);
                     const uint32_t hj2 = rdlane(h2, jj), hj = rdlane(h, jj), cj = rdlane(curr, jj);
                     if (hj2 == h2) {
                         if (jj < lane) mil = cj;
@@ -523,7 +543,19 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                         }
                     }
                     offset = p - m;
-                    while (p > anchor && m > plo && s[p - 1] == s[m - 1]) { p--; m--; mLength++; }
+                    {   // catch up (extend the match backwards): 64 byte pairs per wave step
+                        const uint32_t lim = (p - anchor) < (m - plo) ? p - anchor : m - plo;
+                        uint32_t back = 0;
+                        while (back < lim) {
+                            const uint32_t kk = back + lane;
+                            const bool eq = kk < lim && s[p - 1 - kk] == s[m - 1 - kk];
+                            const uint64_t ne = __ballot(!eq);
+                            const uint32_t f = ne ? (uint32_t)__builtin_ctzll(ne) : 64u;
+                            back += f;
+                            if (f < 64) break;
+                        }
+                        p -= back; m -= back; mLength += back;
+                    }
                     o2 = o1;
                     o1 = offset;
                     if (lane == 0) sq[nseq] = seq_pack(p - anchor, mLength - 3, offset + 3);

@@ -200,3 +200,115 @@ def small_files_table(n_files, seed=3, lo=4096, hi=65536, dup_fraction=0.30):
     rng.shuffle(src)
     uniq_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
     return int(sizes.sum()), uniq_off[src], sizes[src].astype(np.uint64)
+
+
+def _text_piece(rng, nbytes, vocab, ws, wl1, pw):
+    """nbytes of words drawn from a Zipf-weighted vocabulary (vectorized gather)."""
+    nw = int(nbytes / float(wl1 @ pw) * 1.05) + 16
+    ids = np.minimum(np.searchsorted(np.cumsum(pw), rng.random(nw)), len(wl1) - 1)
+    lens = wl1[ids]
+    ends = np.cumsum(lens)
+    k = int(np.searchsorted(ends, nbytes)) + 1
+    ids, lens, ends = ids[:k], lens[:k], ends[:k]
+    gather = np.repeat(ws[ids] - (ends - lens), lens) + np.arange(int(ends[-1]))
+    return vocab[gather[:nbytes]]
+
+
+def compressible_corpus(nbytes, kind="text", seed=7, piece=64 << 20):
+    """Compressible synthetic bytes for the zstd level-3 measurements (§8f row 2; the benchmark
+    configurations themselves are incompressible splitmix64).  Test/benchmark data only.
+      text   words of 1-8 symbols from a skewed 48-letter alphabet, Zipf word frequencies
+             (Huffman-coded literals plus many short repeat matches: ratio ~3)
+      mixed  segments of 64 KiB - 4 MiB: half text, a quarter random (already-compressed media),
+             a quarter long byte runs with sparse noise (sparse VM-image regions)"""
+    rng = np.random.default_rng(seed)
+    p = rng.dirichlet(np.ones(48) * 0.35)
+    V = 4096
+    wl = rng.integers(1, 9, V)
+    wl1 = wl + 1
+    ws = np.concatenate([[0], np.cumsum(wl1)[:-1]])
+    vocab = np.full(int(wl1.sum()), 32, dtype=np.uint8)
+    letters = (rng.choice(48, size=int(wl.sum()), p=p) + 40).astype(np.uint8)
+    wstart = np.concatenate([[0], np.cumsum(wl)[:-1]])
+    vocab[np.repeat(ws, wl) + (np.arange(int(wl.sum())) - np.repeat(wstart, wl))] = letters
+    pw = 1.0 / (np.arange(V) + 2.0) ** 1.05
+    pw /= pw.sum()
+    out = np.empty(nbytes, dtype=np.uint8)
+    pos = 0
+    while pos < nbytes:
+        if kind == "text":
+            n = min(piece, nbytes - pos)
+            out[pos:pos + n] = _text_piece(rng, n, vocab, ws, wl1, pw)
+        else:
+            n = min(int(rng.integers(64 << 10, 4 << 20)), nbytes - pos)
+            r = rng.random()
+            if r < 0.5:
+                out[pos:pos + n] = _text_piece(rng, n, vocab, ws, wl1, pw)
+            elif r < 0.75:
+                out[pos:pos + n] = rng.integers(0, 256, n, dtype=np.uint8)
+            else:
+                seg = np.full(n, int(rng.integers(0, 3)), dtype=np.uint8)
+                k = max(1, n // 4096)
+                seg[rng.integers(0, n, k)] = rng.integers(0, 256, k, dtype=np.uint8)
+                out[pos:pos + n] = seg
+        pos += n
+    return out
+
+
+def compressible_corpus_torch(nbytes, device, kind="text", seed=7, piece=256 << 20):
+    """compressible_corpus's distributions generated on the GPU with torch (same recipe, its own
+    random stream): seconds for GiBs instead of a minute of numpy.  Checks read the bytes back
+    from the device, so nothing needs to regenerate them on the host."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    p = rng.dirichlet(np.ones(48) * 0.35)
+    V = 4096
+    wl = rng.integers(1, 9, V)
+    wl1 = wl + 1
+    ws = np.concatenate([[0], np.cumsum(wl1)[:-1]])
+    vocab = np.full(int(wl1.sum()), 32, dtype=np.uint8)
+    letters = (rng.choice(48, size=int(wl.sum()), p=p) + 40).astype(np.uint8)
+    wstart = np.concatenate([[0], np.cumsum(wl)[:-1]])
+    vocab[np.repeat(ws, wl) + (np.arange(int(wl.sum())) - np.repeat(wstart, wl))] = letters
+    pw = 1.0 / (np.arange(V) + 2.0) ** 1.05
+    pw /= pw.sum()
+    t_vocab = torch.from_numpy(vocab).to(device)
+    t_ws = torch.from_numpy(ws.astype(np.int64)).to(device)
+    t_wl1 = torch.from_numpy(wl1.astype(np.int64)).to(device)
+    t_cdf = torch.from_numpy(np.cumsum(pw)).to(device)
+    mean = float(wl1 @ pw)
+
+    def text(n):
+        nw = int(n / mean * 1.05) + 16
+        ids = torch.searchsorted(t_cdf, torch.rand(nw, generator=g, device=device, dtype=torch.float64))
+        ids.clamp_(max=V - 1)
+        lens = t_wl1[ids]
+        ends = torch.cumsum(lens, 0)
+        k = int(torch.searchsorted(ends, torch.tensor([n], device=device)).item()) + 1
+        ids, lens, ends = ids[:k], lens[:k], ends[:k]
+        base = torch.repeat_interleave(t_ws[ids] - (ends - lens), lens)
+        return t_vocab[base[:n] + torch.arange(n, device=device)]
+
+    out = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    pos = 0
+    while pos < nbytes:
+        if kind == "text":
+            n = min(piece, nbytes - pos)
+            out[pos:pos + n] = text(n)
+        else:
+            n = min(int(rng.integers(64 << 10, 4 << 20)), nbytes - pos)
+            r = rng.random()
+            if r < 0.5:
+                out[pos:pos + n] = text(n)
+            elif r < 0.75:
+                out[pos:pos + n] = torch.randint(0, 256, (n,), generator=g, device=device, dtype=torch.uint8)
+            else:
+                seg = torch.full((n,), int(rng.integers(0, 3)), dtype=torch.uint8, device=device)
+                k = max(1, n // 4096)
+                idx = torch.randint(0, n, (k,), generator=g, device=device)
+                seg[idx] = torch.randint(0, 256, (k,), generator=g, device=device, dtype=torch.uint8)
+                out[pos:pos + n] = seg
+        pos += n
+    return out
