@@ -406,8 +406,9 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                                                  uint64_t* __restrict__ seqs, const uint32_t* __restrict__ active) {
     const uint32_t bi = active ? active[blockIdx.x] : blockIdx.x;
     const uint32_t lane = threadIdx.x;
-    constexpr uint32_t DUP_SLOTS = 512;
+    constexpr uint32_t DUP_SLOTS = 128;  // 2 KiB of LDS: up to 8 waves per SIMD (one blob per wave)
     __shared__ unsigned long long s_mL[DUP_SLOTS], s_mS[DUP_SLOTS];
+    __shared__ uint32_t s_h2[64], s_h[64], s_cu[64];
     for (uint32_t i = lane; i < DUP_SLOTS; i += 64) { s_mL[i] = 0; s_mS[i] = 0; }
     __builtin_amdgcn_wave_barrier();
     const ZBlob B = blobs[bi];
@@ -417,6 +418,13 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
     const uint32_t ib = B.base + 1;  // index of s[0] (libzstd: dictLimit)
     const uint32_t hlog = B.hlog, clog = B.clog, mls = B.mls, maxD = 1u << B.wlog;
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+    // Probe window: a step tests the next W positions of the skip sequence (W <= 64 lanes).  Every
+    // probe is a random 4-byte read from a 768 KiB table (a cache line from HBM), and on
+    // compressible data the first match is usually a few positions ahead, so probing all 64
+    // positions fetched ~20x the lines the step consumes.  W follows the data: it doubles after a
+    // step without a match and shrinks to ~2x the matched lane after one.  Any W is exact (the
+    // lanes past the window are simply tested by a later step).
+    uint32_t W = 64;
     for (uint32_t k = 0; k < B.nblocks; k++) {
         ZBlock* blk = blocks + B.first_block + k;
         const uint32_t bs = blk->bs, off = (uint32_t)blk->off;
@@ -449,7 +457,7 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                     j -= t;
                 }
                 const uint32_t pos = anchor + d;
-                const bool valid = pos < ilimit;
+                const bool valid = pos < ilimit && lane < W;
                 uint64_t v8 = 0;
                 uint32_t h2 = 0xFFFFFFFFu, h = 0xFFFFFFFFu, mil = 0, mis = 0, v4n = 0, vrep = 1;
                 if (valid) {
@@ -469,30 +477,43 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 // shares a bucket of a small LDS map with another lane can be involved: each lane
                 // ORs its bit into its two buckets, and the exact forwarding runs over the lanes
                 // of shared buckets only (~15 of 64; the map is cleared behind itself).
+                // Each lane then walks only its own bucket-mates (usually none), nearest first, in
+                // LDS: the latest earlier lane with the same hash supplies the probe value, the
+                // nearest later one decides whether this lane's table write survives the step.
                 uint32_t nextL = 64, nextS = 64;
                 uint64_t mL = 0, mS = 0;
                 if (valid) {
                     atomicOr(&s_mL[h2 & (DUP_SLOTS - 1)], 1ull << lane);
                     atomicOr(&s_mS[h & (DUP_SLOTS - 1)], 1ull << lane);
+                    s_h2[lane] = h2;
+                    s_h[lane] = h;
+                    s_cu[lane] = curr;
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (valid) { mL = s_mL[h2 & (DUP_SLOTS - 1)]; mS = s_mS[h & (DUP_SLOTS - 1)]; }
                 __builtin_amdgcn_wave_barrier();
                 if (valid) { s_mL[h2 & (DUP_SLOTS - 1)] = 0; s_mS[h & (DUP_SLOTS - 1)] = 0; }
                 __builtin_amdgcn_wave_barrier();
-                uint64_t shared = __ballot(valid && ((mL & (mL - 1)) | (mS & (mS - 1))) != 0);
-                for (; shared; shared &= shared - 1) {
-                    const uint32_t jj = (uint32_t)__builtin_ctzll(shared);
-                    const uint32_t hj2 = rdlane(h2, jj), hj = rdlane(h, jj), cj = rdlane(curr, jj);
-                    if (hj2 == h2) {
-                        if (jj < lane) mil = cj;
-                        else if (jj > lane && nextL == 64) nextL = jj;
+                if (valid) {
+                    const uint64_t below = (1ull << lane) - 1, above = ~below & ~(1ull << lane);
+                    for (uint64_t c = mL & below; c; c &= ~(1ull << (63 - __builtin_clzll(c)))) {
+                        const uint32_t i = 63 - (uint32_t)__builtin_clzll(c);
+                        if (s_h2[i] == h2) { mil = s_cu[i]; break; }
                     }
-                    if (hj == h) {
-                        if (jj < lane) mis = cj;
-                        else if (jj > lane && nextS == 64) nextS = jj;
+                    for (uint64_t c = mL & above; c; c &= c - 1) {
+                        const uint32_t i = (uint32_t)__builtin_ctzll(c);
+                        if (s_h2[i] == h2) { nextL = i; break; }
+                    }
+                    for (uint64_t c = mS & below; c; c &= ~(1ull << (63 - __builtin_clzll(c)))) {
+                        const uint32_t i = 63 - (uint32_t)__builtin_clzll(c);
+                        if (s_h[i] == h) { mis = s_cu[i]; break; }
+                    }
+                    for (uint64_t c = mS & above; c; c &= c - 1) {
+                        const uint32_t i = (uint32_t)__builtin_ctzll(c);
+                        if (s_h[i] == h) { nextS = i; break; }
                     }
                 }
+                __builtin_amdgcn_wave_barrier();
                 bool evR = false, evL = false, evS = false;
                 if (valid) {
                     evR = o1 && vrep == v4n;
@@ -508,10 +529,12 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 if (!emask) {
                     const uint32_t pl = rdlane(pos, nvalid - 1);
                     ip = pl + ((pl - anchor) >> 8) + 1;
+                    W = W < 32 ? 2 * W : 64;
                     continue;
                 }
                 __threadfence_block();
                 const uint32_t e = lastw;
+                W = e < 4 ? 8 : (e < 8 ? 16 : (e < 16 ? 32 : 64));
                 uint32_t p = rdlane(pos, e);
                 const uint32_t cu = ib + p;
                 const bool eR = rdlane(evR, e), eL = rdlane(evL, e);
@@ -608,8 +631,17 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
 constexpr int ST_THREADS = 256;
 constexpr int ST_CHUNK = 1024;  // sequences staged in LDS per step of the backward FSE pass
 
+constexpr int ST_BITW = (ST_CHUNK * 80 + 63) / 32 + 2;  // LDS words of one chunk's bitstream (<= 80 bits a sequence)
+
 struct StatsLds {
-    uint32_t hist[4][4][256];      // [wave][segment][byte]
+    union {
+        uint32_t hist[4][4][256];  // [wave][segment][byte] (literal statistics)
+        struct {                   // then the sequences bitstream, one chunk at a time
+            uint32_t code[ST_CHUNK];      // ll code | of code << 8 | ml code << 16, in stream order
+            uint32_t sbits[3][ST_CHUNK];  // FSE state output of the OF / ML / LL chains: nbits << 16 | bits
+            uint32_t bitbuf[ST_BITW];
+        } bs;
+    };
     uint32_t cll[36], cof[32], cml[53];
     uint32_t scanA[ST_THREADS], scanB[ST_THREADS];
     uint32_t nlong;
@@ -798,59 +830,130 @@ __global__ __launch_bounds__(ST_THREADS) void k_zs_stats(const uint8_t* __restri
         s_lastNC = (uint32_t)lastNC;
     }
     __syncthreads();
-    // backward FSE pass: lane 0 encodes, the workgroup stages the sequences
-    BitW bw;
-    FseState sLL, sOF, sML;
-    const uint32_t cap = bs + 64;
+    // The backward sequences bitstream, in the order libzstd's bit writer produces it (sequence
+    // nseq - 1 first), one chunk of ST_CHUNK sequences at a time: every thread computes codes; lanes
+    // 0..2 of wave 0 run the three FSE state chains (OF, ML, LL) side by side over the chunk; every
+    // thread then places the six fields of its sequences at their bit offsets (a workgroup scan of
+    // the field lengths) in an LDS word buffer, which is stored as whole words.  The partially
+    // filled last word carries into the next chunk.  (One lane writing bytes serially took ~1/3 of
+    // the whole compressor's time.)
+    const uint32_t capB = bs + 64, capW = capB / 4;  // libzstd's limit: longer sections go raw
+    uint32_t* bo32 = (uint32_t*)bo;
     const uint32_t gLL = s_logs & 255, gOF = (s_logs >> 8) & 255, gML = s_logs >> 16;
-    uint32_t hi = nseq;
-    bool first = true;
-    while (hi > 0) {
-        const uint32_t lo_i = hi > (uint32_t)ST_CHUNK ? hi - ST_CHUNK : 0;
+    const uint16_t* stAll = L.stLL;  // stLL[512] | stOF[256] | stML[512]
+    const FseTT* ttAll = L.ttLL;     // ttLL[36] | ttOF[32] | ttML[53]
+    const uint32_t stb = t == 0 ? 512 : (t == 1 ? 768 : 0), ttb = t == 0 ? 36 : (t == 1 ? 68 : 0);
+    const uint32_t csh = t == 0 ? 8 : (t == 1 ? 16 : 0);
+    uint32_t fv = 0;  // the chain's FSE state (lanes 0..2)
+    uint64_t bitpos = 0;
+    uint32_t carry = 0;
+    for (uint32_t hi = nseq; hi > 0;) {
+        const uint32_t lo_i = hi > (uint32_t)ST_CHUNK ? hi - ST_CHUNK : 0, m = hi - lo_i;
         __syncthreads();
-        for (uint32_t i = lo_i + t; i < hi; i += ST_THREADS) L.chunk[i - lo_i] = sq[i];
+        for (uint32_t j = t; j < m; j += ST_THREADS) {
+            const uint64_t q = sq[hi - 1 - j];
+            L.chunk[j] = q;
+            L.bs.code[j] = ll_code(seq_ll(q)) | (hb32(seq_ov(q)) << 8) | (ml_code(seq_mb(q)) << 16);
+        }
+        const uint32_t nw = (m * 80 + 63) / 32 + 2;
+        for (uint32_t i = t; i < nw; i += ST_THREADS) L.bs.bitbuf[i] = 0;
         __syncthreads();
-        if (t == 0) {
-            uint32_t i = hi;
-            if (first) {
-                bw.init(bo, cap);
-                const uint64_t q = L.chunk[hi - 1 - lo_i];
-                const uint32_t ll = seq_ll(q), mb = seq_mb(q), ov = seq_ov(q);
-                const uint32_t cl = ll_code(ll), co = hb32(ov), cm = ml_code(mb);
-                sML.init2(L.stML, L.ttML, gML, cm);
-                sOF.init2(L.stOF, L.ttOF, gOF, co);
-                sLL.init2(L.stLL, L.ttLL, gLL, cl);
-                bw.add(ll, c_LL_bits[cl]);
-                bw.add(mb, c_ML_bits[cm]);
-                bw.add(ov, co);
-                i = hi - 1;
-                first = false;
-            }
-            while (i-- > lo_i) {
-                const uint64_t q = L.chunk[i - lo_i];
-                const uint32_t ll = seq_ll(q), mb = seq_mb(q), ov = seq_ov(q);
-                const uint32_t cl = ll_code(ll), co = hb32(ov), cm = ml_code(mb);
-                sOF.enc(bw, co);
-                sML.enc(bw, cm);
-                sLL.enc(bw, cl);
-                bw.add(ll, c_LL_bits[cl]);
-                bw.add(mb, c_ML_bits[cm]);
-                bw.add(ov, co);
+        if (t < 3) {
+            for (uint32_t j = 0; j < m; j++) {
+                const uint32_t sym = (L.bs.code[j] >> csh) & 255;
+                const FseTT x = ttAll[ttb + sym];
+                uint32_t out = 0;
+                if (hi == nseq && j == 0) {  // the last sequence initialises the states (no bits)
+                    const uint32_t nbOut = (x.dnb + (1u << 15)) >> 16;
+                    const uint32_t v0 = (nbOut << 16) - x.dnb;
+                    fv = stAll[stb + (v0 >> nbOut) + (uint32_t)x.dfs];
+                } else {
+                    const uint32_t nbOut = (fv + x.dnb) >> 16;
+                    out = (nbOut << 16) | (fv & ((1u << nbOut) - 1));
+                    fv = stAll[stb + (fv >> nbOut) + (uint32_t)x.dfs];
+                }
+                L.bs.sbits[t][j] = out;
             }
         }
+        __syncthreads();
+        // field lengths of this thread's run of sequences, then the workgroup scan
+        const uint32_t per = (m + ST_THREADS - 1) / ST_THREADS;
+        const uint32_t j0 = t * per < m ? t * per : m, j1 = j0 + per < m ? j0 + per : m;
+        uint32_t mine = 0;
+        for (uint32_t j = j0; j < j1; j++) {
+            const uint32_t cd = L.bs.code[j];
+            mine += (L.bs.sbits[0][j] >> 16) + (L.bs.sbits[1][j] >> 16) + (L.bs.sbits[2][j] >> 16) +
+                    c_LL_bits[cd & 255] + c_ML_bits[cd >> 16] + ((cd >> 8) & 255);
+        }
+        L.scanA[t] = mine;
+        __syncthreads();
+        for (uint32_t d = 1; d < ST_THREADS; d <<= 1) {
+            const uint32_t a = t >= d ? L.scanA[t - d] : 0;
+            __syncthreads();
+            L.scanA[t] += a;
+            __syncthreads();
+        }
+        const uint32_t chunkBits = L.scanA[ST_THREADS - 1];
+        const uint32_t r0 = (uint32_t)(bitpos & 31);
+        uint32_t r = r0 + L.scanA[t] - mine;  // this run's first bit, relative to word bitpos >> 5
+        auto put = [&](uint32_t v, uint32_t nb) {
+            if (!nb) return;
+            const uint64_t x = (uint64_t)(v & (0xFFFFFFFFu >> (32 - nb))) << (r & 31);
+            atomicOr(&L.bs.bitbuf[r >> 5], (uint32_t)x);
+            if (x >> 32) atomicOr(&L.bs.bitbuf[(r >> 5) + 1], (uint32_t)(x >> 32));
+            r += nb;
+        };
+        if (t == 0 && r0) atomicOr(&L.bs.bitbuf[0], carry);
+        for (uint32_t j = j0; j < j1; j++) {
+            const uint32_t cd = L.bs.code[j];
+            const uint64_t q = L.chunk[j];
+            const uint32_t cl = cd & 255, co = (cd >> 8) & 255, cm = cd >> 16;
+            put(L.bs.sbits[0][j] & 0xFFFF, L.bs.sbits[0][j] >> 16);
+            put(L.bs.sbits[1][j] & 0xFFFF, L.bs.sbits[1][j] >> 16);
+            put(L.bs.sbits[2][j] & 0xFFFF, L.bs.sbits[2][j] >> 16);
+            put(seq_ll(q), c_LL_bits[cl]);
+            put(seq_mb(q), c_ML_bits[cm]);
+            put(seq_ov(q), co);
+        }
+        __syncthreads();
+        const uint32_t endR = r0 + chunkBits, full = endR >> 5;
+        const uint64_t w0 = bitpos >> 5;
+        for (uint32_t i = t; i < full; i += ST_THREADS)
+            if (w0 + i < capW) bo32[w0 + i] = L.bs.bitbuf[i];
+        carry = L.bs.bitbuf[full];  // bits [0, endR & 31) of the next word
+        bitpos += chunkBits;
         hi = lo_i;
     }
+    // the state flushes (ML, OF, LL) and the end mark, by one lane
+    const uint32_t fOF = __shfl(fv, 0, 64), fML = __shfl(fv, 1, 64), fLL = __shfl(fv, 2, 64);
     if (t == 0) {
-        sML.flush(bw);
-        sOF.flush(bw);
-        sLL.flush(bw);
-        const uint32_t nb = bw.close();
+        uint64_t acc = carry;
+        uint32_t nb = (uint32_t)(bitpos & 31);
+        uint64_t wi = bitpos >> 5;
+        auto put1 = [&](uint32_t v, uint32_t bits) {
+            if (!bits) return;
+            acc |= (uint64_t)(v & (0xFFFFFFFFu >> (32 - bits))) << nb;
+            nb += bits;
+            while (nb >= 32) {
+                if (wi < capW) bo32[wi] = (uint32_t)acc;
+                wi++;
+                acc >>= 32;
+                nb -= 32;
+            }
+        };
+        put1(fML, gML);
+        put1(fOF, gOF);
+        put1(fLL, gLL);
+        put1(1, 1);
+        if (nb && wi < capW) bo32[wi] = (uint32_t)acc;
+        const uint64_t totalBits = bitpos + gML + gOF + gLL + 1;
+        const uint32_t nbytes = (uint32_t)((totalBits + 7) / 8);
         const uint32_t hdr = s_hdr;
-        uint32_t bad = nb > cap;
+        uint32_t bad = nbytes > capB;
         // zstd <= 1.3.4 decoders misread an NCount shorter than 4 bytes before the end
-        if (s_lastNC != 0xFFFFFFFFu && (hdr - s_lastNC) + nb < 4) bad = 1;
+        if (s_lastNC != 0xFFFFFFFFu && (hdr - s_lastNC) + nbytes < 4) bad = 1;
         blk->sec_hdr = hdr;
-        blk->sec_len = hdr + nb;
+        blk->sec_len = hdr + nbytes;
         blk->sec_bad = bad;
         blk->nlit = litTotal;
         blk->is_rle = L.flag ? 0 : 1;
@@ -1505,7 +1608,7 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
                 K.sec0 = secCap;
                 seqCap += K.bs / 4 + 2;
                 litCap += (K.bs + 15) & ~15u;
-                secCap += SEC_HDR + K.bs + 128;
+                secCap += (SEC_HDR + K.bs + 128 + 15) & ~15u;  // 16-byte aligned: the bitstream is stored in words
                 hk.push_back(K);
             }
         }
