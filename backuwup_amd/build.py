@@ -48,16 +48,19 @@ def _stale(lib=LIB):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False, debug=False, jobs=8):
+def build(force=False, verbose=False, debug=False, jobs=8, variant=None, defines=()):
     """One object per source, compiled in parallel under build/ (an unchanged source whose object
-    is newer than every header is not recompiled unless force), then one shared link."""
+    is newer than every header is not recompiled unless force), then one shared link.
+    variant="name" with defines=("-DX", ...) builds a diagnostic library libbackuwup_amd_<name>.so
+    (loaded only through BW_LIB by tools, never by the product path)."""
     from concurrent.futures import ThreadPoolExecutor
-    lib = LIB_DEBUG if debug else LIB
+    lib = LIB_DEBUG if debug else (os.path.join(HERE, "libbackuwup_amd_%s.so" % variant) if variant else LIB)
     if not force and not _stale(lib):
         return lib
-    odir = os.path.join(HERE, "..", "build", "debug" if debug else "release")
+    odir = os.path.join(HERE, "..", "build", "debug" if debug else (variant or "release"))
     os.makedirs(odir, exist_ok=True)
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wno-unused-value", "-Wno-unused-result"]
+    flags += list(defines)
     if debug:
         flags += ["-DBW_DEBUG", "-g"]
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
@@ -87,4 +90,7 @@ def build(force=False, verbose=False, debug=False, jobs=8):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, debug="--debug" in sys.argv))
+    if "--ztime" in sys.argv:  # zstd parse section timers (tools/zstd_bench.py --timing)
+        print(build(force="--force" in sys.argv, verbose=True, variant="ztime", defines=("-DBW_ZSTD_TIMING",)))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True, debug="--debug" in sys.argv))

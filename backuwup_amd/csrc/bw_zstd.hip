@@ -351,6 +351,9 @@ struct ZBlob {
     uint32_t raw_mask;          // blocks the parse treats as not compressed (repeat offsets kept)
     uint32_t flags;             // 1: the decisions contradicted raw_mask where it mattered (rerun)
     uint64_t frame_len;
+#ifdef BW_ZSTD_TIMING
+    uint64_t tm[8];             // parse section cycles: probe, length, catch-up, inserts; steps, sequences
+#endif
 };
 
 struct ZBlock {
@@ -401,6 +404,56 @@ __device__ uint32_t wave_count(const uint8_t* s, uint32_t a, uint32_t b, uint32_
     return (a + n > limit) ? limit - a : n;
 }
 
+// A match's forward length beyond a (vs b, up to limit) and its backward extension before pb (vs mb, up
+// to lim byte pairs), with the first 512 forward bytes and the first 64 backward pairs loaded in one
+// round (wave_count and the catch-up loop continue when those are all equal).
+__device__ void wave_extend(const uint8_t* s, uint32_t a, uint32_t b, uint32_t limit, uint32_t pb, uint32_t mb,
+                            uint32_t lim, uint32_t lane, uint32_t& fwd, uint32_t& back) {
+    const bool bin = lane < lim;
+    uint8_t bp = 0, bm = 1;
+    if (bin) {
+        bp = s[pb - 1 - lane];
+        bm = s[mb - 1 - lane];
+    }
+    uint32_t fd = 8;
+    const uint32_t o = a + 8 * lane, m = b + 8 * lane;
+    if (o + 8 <= limit) {
+        const uint64_t x = ld64(s + o) ^ ld64(s + m);
+        if (x) fd = (uint32_t)__builtin_ctzll(x) >> 3;
+    } else if (o < limit) {
+        const uint32_t rem = limit - o;
+        fd = rem;
+        for (uint32_t i = 0; i < rem; i++)
+            if (s[o + i] != s[m + i]) { fd = i; break; }
+    } else {
+        fd = 0;
+    }
+    const bool beq = bin && bp == bm;
+    const uint64_t mm = __ballot(fd < 8), ne = __ballot(!beq);
+    if (mm) {
+        const uint32_t L = (uint32_t)__builtin_ctzll(mm);
+        const uint32_t n = 8 * L + rdlane(fd, L);
+        fwd = (a + n > limit) ? limit - a : n;
+    } else {
+        fwd = 512 + wave_count(s, a + 512, b + 512, limit, lane);
+    }
+    back = ne ? (uint32_t)__builtin_ctzll(ne) : 64u;
+    if (back == 64) {
+        while (back < lim) {
+            const uint32_t kk = back + lane;
+            const bool eq = kk < lim && s[pb - 1 - kk] == s[mb - 1 - kk];
+            const uint64_t nn = __ballot(!eq);
+            const uint32_t f = nn ? (uint32_t)__builtin_ctzll(nn) : 64u;
+            back += f;
+            if (f < 64) break;
+        }
+    }
+}
+
+#ifndef BW_ZS_WMIN
+#define BW_ZS_WMIN 2  // probe window after a match at lane 0 (text: the mean first-match lane is 0.2-0.3)
+#endif
+
 __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src, ZBlob* __restrict__ blobs,
                                                  ZBlock* __restrict__ blocks, uint32_t* tables,
                                                  uint64_t* __restrict__ seqs, const uint32_t* __restrict__ active) {
@@ -425,6 +478,21 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
     // step without a match and shrinks to ~2x the matched lane after one.  Any W is exact (the
     // lanes past the window are simply tested by a later step).
     uint32_t W = 64;
+#ifdef BW_ZSTD_TIMING
+    uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0}, zlast = 0;
+#define ZT_START() (zlast = __builtin_amdgcn_s_memtime())
+#define ZT_LAP(i)                                              \
+    do {                                                       \
+        const uint64_t zn_ = __builtin_amdgcn_s_memtime();     \
+        tm[i] += zn_ - zlast;                                  \
+        zlast = zn_;                                           \
+    } while (0)
+#define ZT_COUNT(i) (tm[i]++)
+#else
+#define ZT_START() ((void)0)
+#define ZT_LAP(i) ((void)0)
+#define ZT_COUNT(i) ((void)0)
+#endif
     for (uint32_t k = 0; k < B.nblocks; k++) {
         ZBlock* blk = blocks + B.first_block + k;
         const uint32_t bs = blk->bs, off = (uint32_t)blk->off;
@@ -444,8 +512,15 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 if (o2 > maxRep) { saved = o2; o2 = 0; }
                 if (o1 > maxRep) { saved = o1; o1 = 0; }
             }
+            // the next step's probe data (pos = ip + lane), loaded in the same round as the previous
+            // match's insert keys and repeat check
+            bool pre = false;
+            uint64_t pv8 = 0, pv8n = 0;
+            uint32_t pvrep = 0;
             while (ip < ilimit) {
                 __threadfence_block();
+                ZT_START();
+                ZT_COUNT(4);
                 // this lane's position in the skip sequence ip += ((ip - anchor) >> 8) + 1
                 uint32_t d = ip - anchor, j = lane;
                 if (d + 63 < 256) { d += j; j = 0; }  // step 1 for every lane: no divisions
@@ -458,16 +533,27 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 }
                 const uint32_t pos = anchor + d;
                 const bool valid = pos < ilimit && lane < W;
-                uint64_t v8 = 0;
-                uint32_t h2 = 0xFFFFFFFFu, h = 0xFFFFFFFFu, mil = 0, mis = 0, v4n = 0, vrep = 1;
-                if (valid) {
+                // Loads are issued unconditionally (lanes without a use read a safe address) so that
+                // each round of a step is one trip to memory: a load under a divergent branch makes
+                // the compiler wait for it inside the branch.
+                uint64_t v8 = 0, v8n = 0;
+                uint32_t vrep = 0;
+                if (pre) {  // set only after a match: anchor == ip, so pos == ip + lane
+                    v8 = pv8; v8n = pv8n; vrep = pvrep;
+                } else if (valid) {
                     v8 = ld64(s + pos);
-                    h2 = hash_long(v8, hlog);
-                    h = hash_small(v8, clog, mls);
+                    v8n = ld64(s + pos + 1);
+                    vrep = ld32(s + pos + 1 - o1);
+                }
+                pre = false;
+                // Round of table probes: the long and short tables at pos, and -- speculatively, for the
+                // small-match path -- the long table at pos + 1 (libzstd's search_next_long)
+                const uint32_t h2 = hash_long(v8, hlog), h = hash_small(v8, clog, mls), h3 = hash_long(v8n, hlog);
+                uint32_t mil = 0, mis = 0, m3 = 0;
+                if (valid) {
                     mil = hl[h2];
                     mis = hs[h];
-                    v4n = ld32(s + pos + 1);
-                    if (o1) vrep = ld32(s + pos + 1 - o1);
+                    m3 = hl[h3];
                 }
                 const uint32_t curr = ib + pos;
                 const uint64_t vmask = __ballot(valid);
@@ -475,13 +561,12 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 // writes of earlier lanes to the same slots reach this lane's probes (the serial
                 // loop writes every visited position before it moves on).  Only lanes whose hash
                 // shares a bucket of a small LDS map with another lane can be involved: each lane
-                // ORs its bit into its two buckets, and the exact forwarding runs over the lanes
-                // of shared buckets only (~15 of 64; the map is cleared behind itself).
-                // Each lane then walks only its own bucket-mates (usually none), nearest first, in
-                // LDS: the latest earlier lane with the same hash supplies the probe value, the
-                // nearest later one decides whether this lane's table write survives the step.
+                // ORs its bit into its two buckets, then walks only its own bucket-mates (usually
+                // none), nearest first: the latest earlier lane with the same hash supplies the probe
+                // value, the nearest later one decides whether this lane's table write survives the
+                // step.  The pos + 1 probe sees the long-table writes up to and including its own lane.
                 uint32_t nextL = 64, nextS = 64;
-                uint64_t mL = 0, mS = 0;
+                uint64_t mL = 0, mS = 0, m3L = 0;
                 if (valid) {
                     atomicOr(&s_mL[h2 & (DUP_SLOTS - 1)], 1ull << lane);
                     atomicOr(&s_mS[h & (DUP_SLOTS - 1)], 1ull << lane);
@@ -490,7 +575,7 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                     s_cu[lane] = curr;
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (valid) { mL = s_mL[h2 & (DUP_SLOTS - 1)]; mS = s_mS[h & (DUP_SLOTS - 1)]; }
+                if (valid) { mL = s_mL[h2 & (DUP_SLOTS - 1)]; mS = s_mS[h & (DUP_SLOTS - 1)]; m3L = s_mL[h3 & (DUP_SLOTS - 1)]; }
                 __builtin_amdgcn_wave_barrier();
                 if (valid) { s_mL[h2 & (DUP_SLOTS - 1)] = 0; s_mS[h & (DUP_SLOTS - 1)] = 0; }
                 __builtin_amdgcn_wave_barrier();
@@ -512,15 +597,23 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                         const uint32_t i = (uint32_t)__builtin_ctzll(c);
                         if (s_h[i] == h) { nextS = i; break; }
                     }
+                    for (uint64_t c = m3L & (below | (1ull << lane)); c; c &= ~(1ull << (63 - __builtin_clzll(c)))) {
+                        const uint32_t i = 63 - (uint32_t)__builtin_clzll(c);
+                        if (s_h2[i] == h3) { m3 = s_cu[i]; break; }
+                    }
                 }
                 __builtin_amdgcn_wave_barrier();
-                bool evR = false, evL = false, evS = false;
-                if (valid) {
-                    evR = o1 && vrep == v4n;
-                    if (mil > pli) evL = ld64(s + (mil - ib)) == v8;
-                    if (mis > pli) evS = ld32(s + (mis - ib)) == (uint32_t)v8;
-                }
+                // round of candidate loads: the evidence of every path at once
+                const bool cL = mil > pli, cS = mis > pli, c3 = m3 > pli;  // (invalid lanes: 0, never > pli)
+                uint64_t xL = 0, x3 = 0;
+                uint32_t xS = 0;
+                if (cL) xL = ld64(s + (mil - ib));
+                if (c3) x3 = ld64(s + (m3 - ib));
+                if (cS) xS = ld32(s + (mis - ib));
+                const bool evR = valid && o1 && vrep == (uint32_t)v8n;
+                const bool evL = cL && xL == v8, evS = cS && xS == (uint32_t)v8, ev3 = c3 && x3 == v8n;
                 const uint64_t emask = __ballot(evR || evL || evS);
+                ZT_LAP(0);
                 const uint32_t lastw = emask ? (uint32_t)__builtin_ctzll(emask) : nvalid - 1;
                 if (valid && lane <= lastw) {
                     if (nextL > lastw) hl[h2] = curr;
@@ -534,68 +627,75 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 }
                 __threadfence_block();
                 const uint32_t e = lastw;
-                W = e < 4 ? 8 : (e < 8 ? 16 : (e < 16 ? 32 : 64));
+                W = e < BW_ZS_WMIN / 2 ? BW_ZS_WMIN : (e < 4 ? 8 : (e < 8 ? 16 : (e < 16 ? 32 : 64)));
                 uint32_t p = rdlane(pos, e);
                 const uint32_t cu = ib + p;
                 const bool eR = rdlane(evR, e), eL = rdlane(evL, e);
-                uint32_t mLength;
+                ZT_COUNT(5);
+#ifdef BW_ZSTD_TIMING
+                tm[2] += e;
+                if (!eR && !eL) tm[7]++;
+#endif
+                // the match: start p, candidate m (offsets in s), bytes already known equal, and the
+                // backward (catch-up) limit; then one round of loads extends it both ways
+                uint32_t m, known, lim = 0;
                 if (eR) {
-                    mLength = wave_count(s, p + 5, p + 5 - o1, iend, lane) + 4;
                     p++;
+                    m = p - o1;
+                    known = 4;
+                } else if (eL) {
+                    m = rdlane(mil, e) - ib;
+                    known = 8;
+                } else {
+                    if (lane == 0) hl[rdlane(h3, e)] = cu + 1;
+                    if (rdlane(ev3, e)) {
+                        m = rdlane(m3, e) - ib;
+                        p++;
+                        known = 8;
+                    } else {
+                        m = rdlane(mis, e) - ib;
+                        known = 4;
+                    }
+                }
+                if (!eR) lim = (p - anchor) < (m - plo) ? p - anchor : m - plo;
+                uint32_t fwd, back;
+                wave_extend(s, p + known, m + known, iend, p, m, lim, lane, fwd, back);
+                uint32_t mLength = fwd + known;
+                if (eR) {
                     if (lane == 0) sq[nseq] = seq_pack(p - anchor, mLength - 3, 1);
                     nseq++;
                 } else {
-                    uint32_t m, offset;
-                    if (eL) {
-                        m = rdlane(mil, e) - ib;
-                        mLength = wave_count(s, p + 8, m + 8, iend, lane) + 8;
-                    } else {
-                        const uint64_t v8n = ld64(s + p + 1);
-                        const uint32_t hl3 = hash_long(v8n, hlog);
-                        const uint32_t mL3 = hl[hl3];
-                        bool long3 = false;
-                        if (mL3 > pli) long3 = ld64(s + (mL3 - ib)) == v8n;
-                        if (lane == 0) hl[hl3] = cu + 1;
-                        if (long3) {
-                            m = mL3 - ib;
-                            mLength = wave_count(s, p + 9, m + 8, iend, lane) + 8;
-                            p++;
-                        } else {
-                            m = rdlane(mis, e) - ib;
-                            mLength = wave_count(s, p + 4, m + 4, iend, lane) + 4;
-                        }
-                    }
-                    offset = p - m;
-                    {   // catch up (extend the match backwards): 64 byte pairs per wave step
-                        const uint32_t lim = (p - anchor) < (m - plo) ? p - anchor : m - plo;
-                        uint32_t back = 0;
-                        while (back < lim) {
-                            const uint32_t kk = back + lane;
-                            const bool eq = kk < lim && s[p - 1 - kk] == s[m - 1 - kk];
-                            const uint64_t ne = __ballot(!eq);
-                            const uint32_t f = ne ? (uint32_t)__builtin_ctzll(ne) : 64u;
-                            back += f;
-                            if (f < 64) break;
-                        }
-                        p -= back; m -= back; mLength += back;
-                    }
+                    const uint32_t offset = p - m;
+                    p -= back;
+                    mLength += back;
                     o2 = o1;
                     o1 = offset;
                     if (lane == 0) sq[nseq] = seq_pack(p - anchor, mLength - 3, offset + 3);
                     nseq++;
                 }
+                ZT_LAP(1);
                 p += mLength;
                 anchor = p;
                 if (p <= ilimit) {
+                    // one round of loads: the four insert keys, the repeat check and the next step's data
                     const uint32_t iti = cu + 2, pti = iti - ib;
                     const uint64_t a8 = ld64(s + pti), b8 = ld64(s + p - 2), c8 = ld64(s + p - 1);
+                    uint32_t rA = ld32(s + p), rB = ld32(s + p - o2);
+                    // lanes past ilimit read at p - 1 (p <= ilimit: bytes up to iend, never past the block)
+                    if (p + lane < ilimit) {
+                        pv8 = ld64(s + p + lane);
+                        pv8n = ld64(s + p + lane + 1);
+                        pvrep = ld32(s + p + lane + 1 - o1);
+                    }
+                    if (!o2) rB = ~rA;
+                    pre = true;
                     if (lane == 0) {
                         hl[hash_long(a8, hlog)] = iti;
                         hl[hash_long(b8, hlog)] = ib + p - 2;
                         hs[hash_small(a8, clog, mls)] = iti;
                         hs[hash_small(c8, clog, mls)] = ib + p - 1;
                     }
-                    while (p <= ilimit && o2 > 0 && ld32(s + p) == ld32(s + p - o2)) {
+                    while (o2 > 0 && rA == rB) {
                         const uint32_t rL = wave_count(s, p + 4, p + 4 - o2, iend, lane) + 4;
                         const uint32_t t = o2;
                         o2 = o1;
@@ -609,8 +709,14 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                         nseq++;
                         p += rL;
                         anchor = p;
+                        pre = false;
+                        ZT_COUNT(6);
+                        if (p > ilimit) break;
+                        rA = ld32(s + p);
+                        rB = o2 ? ld32(s + p - o2) : ~rA;
                     }
                 }
+                ZT_LAP(3);
                 ip = p;
             }
             r0 = o1 ? o1 : saved;
@@ -625,6 +731,10 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
         if (!((B.raw_mask >> k) & 1)) { rep0 = r0; rep1 = r1; }
         __threadfence_block();
     }
+#ifdef BW_ZSTD_TIMING
+    if (lane == 0)
+        for (int i = 0; i < 8; i++) blobs[bi].tm[i] += tm[i];
+#endif
 }
 
 // ======================================================================= k_zs_stats
@@ -1680,6 +1790,17 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
             return BW_EHIP;
         }
         for (uint32_t j = 0; j < nb; j++) frame_len[i0 + j] = back[j].frame_len;
+#ifdef BW_ZSTD_TIMING
+        {
+            double sum[8] = {0};
+            for (uint32_t j = 0; j < nb; j++)
+                for (int i = 0; i < 8; i++) sum[i] += (double)back[j].tm[i];
+            fprintf(stderr, "zstd parse timing over %u blobs: cycles/blob probe %.4g length %.4g catchup %.4g insert+rep %.4g; "
+                    "steps/blob %.4g sequences/blob %.4g rep-loop/blob %.4g; mean first-match lane %.3f, small-path share %.3f\n", nb,
+                    sum[0] / nb, sum[1] / nb, 0.0, sum[3] / nb, sum[4] / nb, sum[5] / nb, sum[6] / nb,
+                    sum[2] / (sum[5] - sum[6] + 1e-9), sum[7] / (sum[5] - sum[6] + 1e-9));
+        }
+#endif
         i0 = i1;
     }
     return BW_OK;
