@@ -12,8 +12,9 @@
 //                parents, all lanes busy).  Blobs of <= 4 leaves finish here (ROOT in-lane);
 //                otherwise the lane stores the level-2 node, or for a blob's ragged last group
 //                the merged tail of the spine (bits 0..1 of n).
-//   k_b3_small   one lane per blob with 4 < n <= 64: the remaining levels on an in-place stack.
-//   k_b3_tree    32 lanes per blob with n > 64: level passes ping-ponging in global memory + the spine.
+//   k_b3_upper   the levels above the groups, one launch: one lane per blob with 4 < n <= 64 (an
+//                in-place stack), one wave per blob with n > 64 (global level passes down to 64
+//                nodes, then one compression pass per level from registers, spine folded alongside).
 #include "bw_device.h"
 #include "bw_internal.h"
 
@@ -235,9 +236,8 @@ __global__ __launch_bounds__(256, MINW) void k_b3_groups(const uint8_t* __restri
 // completes a power-of-two blob, or the last fold, carries ROOT.
 constexpr uint64_t B3_SMALL_LEAVES = 64;
 
-__global__ __launch_bounds__(256) void k_b3_small(const uint64_t* ctr, BlobArrays b, uint32_t* __restrict__ cv_buf,
-                                                  uint8_t* __restrict__ digests) {
-    const uint64_t blob = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr, const BlobArrays& b,
+                                              uint32_t* __restrict__ cv_buf, uint8_t* __restrict__ digests) {
     if (blob >= ctr[C_NBLOBS]) return;
     const uint64_t len = b.len[blob];
     const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
@@ -284,72 +284,128 @@ __global__ __launch_bounds__(256) void k_b3_small(const uint64_t* ctr, BlobArray
     store_digest(digests + blob * 32, acc);
 }
 
-// Upper levels of a larger blob (n > B3_SMALL_LEAVES leaves), TREE_LANES lanes per blob (two
-// blobs per wave).  Each level is one pass of parents over the group's lanes, ping-ponging
-// between cv_buf (level 2 from k_b3_groups) and cv_tmp at the blob's own group offsets; the
-// group's first lane folds the right spine as each level becomes available (it reads a level's
-// last node before the next-but-one level overwrites that buffer).  No LDS, so occupancy is set by
-// registers.  C2 (13.6k blobs of ~1.2 MiB): 0.29 ms with a wave per blob, 0.31 / 0.29 / 0.26 ms
-// with 8 / 16 / 32 lanes per blob.
-#ifndef BW_TREE_LANES
-#define BW_TREE_LANES 32
-#endif
-constexpr int TREE_LANES = BW_TREE_LANES;
+// Upper levels of a larger blob (n > B3_SMALL_LEAVES leaves), one wave per blob.  While a level
+// has more than 64 nodes, lanes 0..62 build the next level's parents in passes over global memory
+// (ping-ponging between cv_buf, which holds level 2 from k_b3_groups, and cv_tmp at the blob's own
+// group offsets) and lane 63 folds the right spine in the same pass (the last node of every level
+// whose bit is set in n, merged from the right); from 64 nodes down, node i lives in lane i's
+// registers and each level is one compression pass: lanes < cnt/2 build parents from their two
+// children (ds_bpermute), lane 63 takes the spine step.  A 3 MiB chunk (768 level-2 nodes) is 20
+// compression passes deep; 32 lanes per blob with every level in global memory took 29 plus a
+// separate spine compression per level.  C1 (939 blobs): upper levels 0.119 -> 0.051 ms per batch,
+// C2 unchanged (0.27 ms, throughput-bound).
+__device__ __forceinline__ void b3_shfl8(const uint32_t x[8], int src, uint32_t out[8]) {
+#pragma unroll
+    for (int w = 0; w < 8; w++) out[w] = __shfl(x[w], src, 64);
+}
 
-__global__ __launch_bounds__(256) void k_b3_tree(const uint64_t* ctr, BlobArrays b, uint32_t* __restrict__ cv_buf,
-                                                 uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests) {
-    const uint32_t sub = threadIdx.x % TREE_LANES;
-    const uint64_t nblobs = ctr[C_NBLOBS];
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x / TREE_LANES;
-    for (uint64_t blob = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / TREE_LANES; blob < nblobs;
-         blob += stride) {
-        const uint64_t len = b.len[blob];
-        const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
-        if (n <= B3_SMALL_LEAVES) continue;  // k_b3_groups / k_b3_small
-        uint32_t* src = cv_buf + b.goff[blob] * 8;
-        uint32_t* dst = cv_tmp + b.goff[blob] * 8;
-        uint64_t cnt = n / 4;
-        uint32_t acc[8];
-        bool have = false;
-        if (sub == 0 && (n & 3)) {
+__device__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
+                              uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t n = (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;  // > B3_SMALL_LEAVES
+    uint32_t* src = cv_buf + b.goff[blob] * 8;
+    uint32_t* dst = cv_tmp + b.goff[blob] * 8;
+    uint64_t cnt = n / 4;  // complete level-2 nodes; the ragged tail's merged node follows them
+    bool have = (n & 3) != 0;
+    uint32_t acc[8];
 #pragma unroll
-            for (int i = 0; i < 8; i++) acc[i] = src[cnt * 8 + i];
-            have = true;
-        }
-        for (int l = 2;; l++) {
-            if (sub == 0 && ((n >> l) & 1)) {
-                uint32_t T[8];
+    for (int w = 0; w < 8; w++) acc[w] = 0;
+    if (have && lane == 63) {
 #pragma unroll
-                for (int i = 0; i < 8; i++) T[i] = src[(cnt - 1) * 8 + i];
-                if (!have) {
+        for (int w = 0; w < 8; w++) acc[w] = src[cnt * 8 + w];
+    }
+    int l = 2;
+    while (cnt > 64) {  // never a root here: at least 65 nodes remain
+        const bool spine = cnt & 1;
+        const uint64_t next = cnt / 2;
+        for (uint64_t base = 0; base < next; base += 63) {
+            const uint64_t i = base + lane;
+            const bool pair = lane < 63 && i < next;
+            const bool fold = lane == 63 && base == 0 && spine && have;
+            if (pair || fold) {
+                uint32_t L[8], R[8], P[8];
+                const uint64_t li = pair ? 2 * i : cnt - 1;
 #pragma unroll
-                    for (int i = 0; i < 8; i++) acc[i] = T[i];
-                    have = true;
+                for (int w = 0; w < 8; w++) L[w] = src[li * 8 + w];
+#pragma unroll
+                for (int w = 0; w < 8; w++) R[w] = pair ? src[(li + 1) * 8 + w] : acc[w];
+                b3_parent(L, R, 0, P);
+                if (pair) {
+#pragma unroll
+                    for (int w = 0; w < 8; w++) dst[i * 8 + w] = P[w];
                 } else {
-                    b3_parent(T, acc, (n >> (l + 1)) == 0 ? B3_ROOT : 0, acc);
+#pragma unroll
+                    for (int w = 0; w < 8; w++) acc[w] = P[w];
                 }
             }
-            const uint64_t next = cnt / 2;
-            if (next == 0) break;
-            const uint32_t root = (n == (1ull << (l + 1))) ? B3_ROOT : 0;
-            for (uint64_t i = sub; i < next; i += TREE_LANES) {
-                uint32_t L[8], R[8], P[8];
-#pragma unroll
-                for (int w = 0; w < 8; w++) { L[w] = src[(2 * i) * 8 + w]; R[w] = src[(2 * i + 1) * 8 + w]; }
-                b3_parent(L, R, root, P);
-#pragma unroll
-                for (int w = 0; w < 8; w++) dst[i * 8 + w] = P[w];
-            }
-            // the group's lanes read each other's nodes next level: same wave, same CU
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            uint32_t* t = src;
-            src = dst;
-            dst = t;
-            cnt = next;
         }
-        if (sub == 0) store_digest(digests + blob * 32, acc);
+        if (spine && !have && lane == 63) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) acc[w] = src[(cnt - 1) * 8 + w];
+        }
+        have |= spine;
+        // the wave reads the level it just wrote (same wave, same CU)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        uint32_t* t = src;
+        src = dst;
+        dst = t;
+        cnt = next;
+        l++;
+    }
+    uint32_t x[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) x[w] = lane < cnt ? src[lane * 8 + w] : 0;
+    for (;;) {
+        const bool spine = cnt & 1;
+        const uint32_t next = (uint32_t)(cnt / 2);
+        uint32_t L[8], R[8], T[8], P[8];
+        b3_shfl8(x, (int)(2 * lane) & 63, L);
+        b3_shfl8(x, (int)(2 * lane + 1) & 63, R);
+        b3_shfl8(x, (int)(cnt - 1), T);
+        const bool pair = lane < next;
+        const bool fold = lane == 63 && spine && have;
+        if (pair || fold) {
+            const uint32_t root = pair ? (n == (2ull << l) ? B3_ROOT : 0) : ((n >> (l + 1)) == 0 ? B3_ROOT : 0);
+            uint32_t A[8], B[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) { A[w] = pair ? L[w] : T[w]; B[w] = pair ? R[w] : acc[w]; }
+            b3_parent(A, B, root, P);
+        }
+        if (lane == 63 && spine) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) acc[w] = have ? P[w] : T[w];
+        }
+        have |= spine;
+        if (next == 0) break;
+        if (pair) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) x[w] = P[w];
+        }
+        cnt = next;
+        l++;
+    }
+    if (lane == 63) store_digest(digests + blob * 32, acc);
+}
+
+// The upper levels of every blob with more than 4 leaves in one launch: blocks [0, small_blocks)
+// run k_b3_small's lane-per-blob stacks, the rest run b3_upper_wave over the blobs with more than
+// B3_SMALL_LEAVES leaves, so the two latency-bound passes overlap instead of running back to back.
+__global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArrays b, uint32_t* __restrict__ cv_buf,
+                                                  uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests,
+                                                  uint32_t small_blocks) {
+    if (blockIdx.x < small_blocks) {
+        b3_small_blob((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ctr, b, cv_buf, digests);
+        return;
+    }
+    const uint64_t nblobs = ctr[C_NBLOBS];
+    const uint64_t waves = (uint64_t)(gridDim.x - small_blocks) * (blockDim.x / 64);
+    for (uint64_t blob = (uint64_t)(blockIdx.x - small_blocks) * (blockDim.x / 64) + threadIdx.x / 64; blob < nblobs;
+         blob += waves) {
+        const uint64_t len = b.len[blob];
+        if (len <= (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) continue;  // k_b3_groups / the small path
+        b3_upper_wave(blob, len, b, cv_buf, cv_tmp, digests);
     }
 }
 
@@ -357,8 +413,11 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
                    uint64_t max_groups, uint32_t* cv_buf, uint32_t* cv_tmp, uint8_t* digests, int max_leaves,
                    hipEvent_t between, int loads, hipStream_t upper) {
     if (!max_blobs) return;
+#ifndef BW_B3_DYN_LDS
+#define BW_B3_DYN_LDS 0  // A/B: extra LDS per block caps the blocks per CU (occupancy experiments)
+#endif
     if (loads == B3_LOADS_PAIRS)
-        hipLaunchKernelGGL((k_b3_groups<false, 1, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL((k_b3_groups<false, 1, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), BW_B3_DYN_LDS, st,
                            data, ctr, b, cv_buf, digests);
     else
         hipLaunchKernelGGL((k_b3_groups<true, 1, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
@@ -366,13 +425,12 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     if (between) hipEventRecord(between, st);
     if (upper != st) hipStreamWaitEvent(upper, between, 0);
     st = upper;
-    if (max_leaves > 4)
-        hipLaunchKernelGGL(k_b3_small, dim3((unsigned)((max_blobs + 255) / 256)), dim3(256), 0, st, ctr, b, cv_buf,
-                           digests);
-    if (max_leaves > (int)B3_SMALL_LEAVES) {
-        uint64_t grid = (max_blobs * TREE_LANES + 255) / 256;
-        if (grid > 16384) grid = 16384;
-        hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)grid), dim3(256), 0, st, ctr, b, cv_buf, cv_tmp, digests);
+    if (max_leaves > 4) {
+        const uint64_t small = (max_blobs + 255) / 256;
+        uint64_t big = max_leaves > (int)B3_SMALL_LEAVES ? (max_blobs + 3) / 4 : 0;  // 4 waves per block
+        if (big > 4096) big = 4096;
+        hipLaunchKernelGGL(k_b3_upper, dim3((unsigned)(small + big)), dim3(256), 0, st, ctr, b, cv_buf, cv_tmp, digests,
+                           (uint32_t)small);
     }
 }
 

@@ -149,6 +149,7 @@ __device__ __forceinline__ void refine_block(const uint8_t* __restrict__ data, u
     record_hit(b + lane, h >> mk.pre_shift, mk, cnt, slots);
 }
 
+
 template <int BLOCK, int STRIP>
 __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ data, uint64_t n_bytes,
                                                        uint64_t n_tiles, Masks mk,
@@ -273,7 +274,10 @@ template <int BLOCK, int STRIP>
 static void launch_scan_t(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                           uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf, uint64_t* ctr) {
     uint64_t grid = (n_tiles + BLOCK / 64 - 1) / (BLOCK / 64);
-    if (grid > 512) grid = 512;  // persistent: every CU holds one block (LDS), two rounds
+#ifndef BW_SCAN_GRID
+#define BW_SCAN_GRID 512
+#endif
+    if (grid > BW_SCAN_GRID) grid = BW_SCAN_GRID;  // persistent: every CU holds one block (LDS), two rounds
     hipLaunchKernelGGL((k_scan<BLOCK, STRIP>), dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes,
                        n_tiles, mk, tile_count, tile_slots, ovf, ctr);
 }

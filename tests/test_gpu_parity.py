@@ -60,6 +60,21 @@ def test_blake3_tree_shapes_batched(ctx, oracle):
         assert bytes(got[i]) == oracle.blake3(data[o:o + l]), l
 
 
+def test_blake3_upper_tree_levels(ctx, oracle):
+    # wave-per-blob upper tree: leaf counts around its global passes (more than 64 level-2 nodes,
+    # i.e. > 259 leaves) and the register levels below them, every spine-bit pattern near powers
+    # of two, next to lane-per-blob blobs in the same launch
+    leaves = [65, 66, 67, 68, 127, 128, 129, 255, 256, 257, 258, 259, 260, 261, 263, 264, 511, 512, 513, 515,
+              516, 517, 1000, 1023, 1024, 1025, 2047, 2048, 2049, 3071, 3072, 4095, 4096, 4097, 5000, 8191, 8193]
+    lens = [k * 1024 + d for k in leaves for d in (-1, 0, 1)] + [5 * 1024, 64 * 1024 + 7, 9000]
+    data = splitmix_bytes(23, sum(lens) + 64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) + 1
+    got = ctx.blake3_many(data, offs, lens)
+    for i, l in enumerate(lens):
+        o = int(offs[i])
+        assert bytes(got[i]) == oracle.blake3(data[o:o + l]), l
+
+
 def test_blake3_many_unaligned(ctx, oracle):
     rng = np.random.default_rng(7)
     data = splitmix_bytes(11, 6 << 20)
