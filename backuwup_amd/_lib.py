@@ -131,6 +131,9 @@ SIGNATURES = [
                                             ctypes.POINTER(BwPackfile), ctypes.c_uint64, vp, vp]),
     ("bw_pack_build", ctypes.c_int, [vp, vp, vp, u64p, u64p, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint32,
                                      ctypes.POINTER(BwPackfile), ctypes.c_uint64, vp, vp]),
+    ("bw_pack_compress_device", ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint64, u64p]),
+    ("bw_pack_build_compressed", ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.POINTER(BwPackfile), ctypes.c_uint64,
+                                                vp, vp]),
     ("bw_index_files_build", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64,
                                             ctypes.POINTER(BwIndexFile), ctypes.c_uint64, u64p, u64p]),
     ("bw_index_load_files", ctypes.c_int, [vp, vp, vp, ctypes.POINTER(BwIndexFile), ctypes.c_uint64, vp,

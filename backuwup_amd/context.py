@@ -453,6 +453,32 @@ class Context:
         check(self._L.bw_pack_build_device(self.h, *a, flags, *b, ctypes.c_void_p(d_out)), self.h)
         self._pack_keep = keep
 
+    def pack_compress_device(self, d_src, src_off, src_len):
+        """Level-3 frames of the queue's blobs (device pointer d_src) staged in the context for
+        pack_build_compressed; returns the frame lengths (synchronous)."""
+        so = np.ascontiguousarray(src_off, dtype=np.uint64)
+        sl = np.ascontiguousarray(src_len, dtype=np.uint64)
+        assert so.size == sl.size
+        fl = np.zeros(so.size, dtype=np.uint64)
+        check(self._L.bw_pack_compress_device(self.h, ctypes.c_void_p(d_src), so.ctypes.data_as(_lib.u64p),
+                                              sl.ctypes.data_as(_lib.u64p), so.size, fl.ctypes.data_as(_lib.u64p)),
+              self.h)
+        return fl
+
+    def pack_build_compressed(self, prk, hashes, kinds, nonces, plan, packfile_ids, d_out):
+        """Seal and lay out the staged frames into the planned packfiles at d_out (asynchronous)."""
+        h = np.ascontiguousarray(np.asarray(hashes, dtype=np.uint8).reshape(-1, 32))
+        kd = np.ascontiguousarray(kinds, dtype=np.uint8)
+        no = np.ascontiguousarray(np.asarray(nonces, dtype=np.uint8).reshape(-1, 12))
+        pl = np.ascontiguousarray(plan, dtype=PACKFILE_DTYPE)
+        ids = np.ascontiguousarray(np.asarray(packfile_ids, dtype=np.uint8).reshape(-1, 12))
+        assert h.shape[0] == kd.size == no.shape[0] and ids.shape[0] >= pl.size
+        k = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(prk))
+        check(self._L.bw_pack_build_compressed(self.h, k, _ptr(h), _ptr(kd), _ptr(no),
+                                               pl.ctypes.data_as(ctypes.POINTER(_lib.BwPackfile)), pl.size,
+                                               _ptr(ids), ctypes.c_void_p(d_out)), self.h)
+        self._pack_keep = (h, kd, no, pl, ids, k)
+
     def index_files_build(self, prk, entries, last_file_num=0):
         """BlobIndex::push + flush over n (hash, packfile id) entries (n x 44 bytes):
         [(file_num, bytes)] as the reference writes them to index/{file_num:0>10}."""

@@ -132,6 +132,9 @@ struct bw_ctx {
     // per-blob zstd level 3 (bw_zstd.hip): hash-table slots and scratch; zs_io = host-call staging
     ZstdWork* zw = nullptr;
     DevBuf zs_io;
+    // bw_pack_compress_device: level-3 frames staged for bw_pack_build_compressed
+    DevBuf pk_stage;
+    std::vector<uint64_t> pk_stage_off, pk_stage_len;
 
     // dedup index: `idx` is `own` unless the context is attached to a shared one
     bw_index* own_idx = nullptr;
@@ -476,7 +479,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->fstart,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
-                     &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io};
+                     &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage};
     for (DevBuf* b : all) free_dev(*b);
     zstd_work_free(c->zw);
     c->zw = nullptr;
@@ -1704,6 +1707,46 @@ extern "C" int bw_pack_build_device(bw_ctx* c, const uint8_t prk[32], const uint
                                     const uint8_t* nonces, uint32_t flags, const bw_packfile* plan, uint64_t npf,
                                     const uint8_t* ids, uint8_t* d_out) {
     return pack_submit(c, prk, d_src, src_off, src_len, n, hashes, kinds, nonces, flags, plan, npf, ids, d_out);
+}
+
+// compress_encrypt_blob + write_packfiles end to end on the device (pack.rs:58-80, 115-227):
+// level-3 frames of the queue's blobs into the context's staging area, then -- after the host's
+// plan over the frame lengths -- sealing and packfile layout straight from that staging.
+extern "C" int bw_pack_compress_device(bw_ctx* c, const uint8_t* d_src, const uint64_t* src_off,
+                                       const uint64_t* src_len, uint64_t n, uint64_t* frame_len) {
+    if (!c || (n && (!d_src || !src_off || !src_len || !frame_len))) return BW_EINVAL;
+    hipSetDevice(c->device);
+    c->pk_stage_off.assign(n, 0);
+    c->pk_stage_len.assign(n, 0);
+    uint64_t out = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (src_len[i] > BW_BLOB_MAX_UNCOMPRESSED_SIZE) return BW_EINVAL;  // BlobTooLarge, pack.rs:32-34
+        c->pk_stage_off[i] = out;
+        out += (bw_zstd_store_size(src_len[i]) + 15) & ~15ull;
+    }
+    if (int rc = ensure(c, c->pk_stage, out + 16)) return rc;
+    if (int rc = zstd_compress(c->stream, c->zw, d_src, src_off, src_len, n, P<uint8_t>(c->pk_stage),
+                               c->pk_stage_off.data(), frame_len, c->err)) {
+        c->pk_stage_off.clear();
+        c->pk_stage_len.clear();
+        return rc;
+    }
+    for (uint64_t i = 0; i < n; i++) c->pk_stage_len[i] = frame_len[i];
+    return BW_OK;
+}
+
+extern "C" int bw_pack_build_compressed(bw_ctx* c, const uint8_t prk[32], const uint8_t* hashes, const uint8_t* kinds,
+                                        const uint8_t* nonces, const bw_packfile* plan, uint64_t npf,
+                                        const uint8_t* ids, uint8_t* d_out) {
+    if (!c) return BW_EINVAL;
+    hipSetDevice(c->device);
+    const uint64_t n = c->pk_stage_len.size();
+    if (npf && plan[npf - 1].first_blob + plan[npf - 1].n_blobs != n) {
+        c->err = "the plan does not cover the staged blobs";
+        return BW_EINVAL;
+    }
+    return pack_submit(c, prk, P<uint8_t>(c->pk_stage), c->pk_stage_off.data(), c->pk_stage_len.data(), n, hashes,
+                       kinds, nonces, 0, plan, npf, ids, d_out);
 }
 
 extern "C" int bw_pack_build(bw_ctx* c, const uint8_t prk[32], const uint8_t* src, const uint64_t* src_off,

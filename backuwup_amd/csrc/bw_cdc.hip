@@ -274,10 +274,12 @@ template <int BLOCK, int STRIP>
 static void launch_scan_t(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t n_tiles, const Masks& mk,
                           uint32_t* tile_count, uint64_t* tile_slots, uint32_t* ovf, uint64_t* ctr) {
     uint64_t grid = (n_tiles + BLOCK / 64 - 1) / (BLOCK / 64);
-#ifndef BW_SCAN_GRID
-#define BW_SCAN_GRID 512
-#endif
-    if (grid > BW_SCAN_GRID) grid = BW_SCAN_GRID;  // persistent: every CU holds one block (LDS), two rounds
+    // Every CU holds one block (LDS).  Large batches: 512 persistent blocks (two rounds, each wave
+    // streams many tiles).  Small batches (half-size tiles): 1024 blocks, four rounds of about one
+    // tile per wave -- C1's scan 0.32 -> 0.27 ms; 512 or an uncapped grid (one tile per wave, a
+    // ragged fifth round) measured 0.32 / 0.43 ms, and 1024 on C2 changed nothing (profiles/r02/s15_grid).
+    const uint64_t cap = STRIP == SCAN_STRIP ? 512 : 1024;
+    if (grid > cap) grid = cap;
     hipLaunchKernelGGL((k_scan<BLOCK, STRIP>), dim3((unsigned)grid), dim3(BLOCK), 0, st, data, n_bytes,
                        n_tiles, mk, tile_count, tile_slots, ovf, ctr);
 }

@@ -111,6 +111,9 @@ def main():
     ap.add_argument("--pack", action="store_true",
                     help="also time packing the last batch's unique blobs into packfiles: zstd store frames, "
                          "per-blob + header AES-256-GCM, packfile layout (§8f rows 2-4)")
+    ap.add_argument("--pack-l3", action="store_true",
+                    help="also time the full chain on the last batch's unique blobs: level-3 zstd on the GPU, "
+                         "the packfile grouping over the frame sizes, sealing + layout (§8f rows 2-4)")
     ap.add_argument("--b3-loads", type=int, default=None, choices=[0, 1],
                     help="k_b3_groups loads (BW_OPT_B3_LOADS): 0 = one block ahead, 1 = block pairs")
     ap.add_argument("--scan-waves", type=int, default=None, choices=[8, 16], help="BW_OPT_SCAN_WAVES")
@@ -329,6 +332,7 @@ def main():
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None
     seal = time_seal(ctx, data, res, file_off, args.steps) if args.seal else None
     pack = time_pack(ctx, data, res, file_off, args.steps) if args.pack else None
+    pack_l3 = time_pack_l3(ctx, data, res, file_off, min(args.steps, 10)) if args.pack_l3 else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -351,6 +355,8 @@ def main():
             line["seal"] = seal
         if pack:
             line["pack"] = pack
+        if pack_l3:
+            line["pack_l3"] = pack_l3
         print(json.dumps(line), flush=True)
     for c in ctxs:
         c.close()
@@ -462,6 +468,16 @@ def time_file_trees(ctx, res, file_len, reps):
             "bit_exact_sample": bool(ok)}
 
 
+def unique_queue(res):
+    """The blobs the packer would queue for the batch as the first of a session: the first
+    occurrence of every digest, in canonical order.  (The bench's session index has seen the
+    batch's data in earlier steps, so its own verdicts mark everything a duplicate.)"""
+    import numpy as np
+    d = np.ascontiguousarray(res["digest"]).view(np.dtype((np.void, 32))).ravel()
+    _, first = np.unique(d, return_index=True)
+    return res[np.sort(first)]
+
+
 def time_seal(ctx, data, res, file_off, reps):
     """Seal every unique blob of the last batch in HBM (derive_backup_key(hash) + AES-256-GCM,
     pack.rs:70-80), as the packer would after compression; the blob bytes stand in for the zstd
@@ -470,7 +486,7 @@ def time_seal(ctx, data, res, file_off, reps):
     import numpy as np
     import torch
     from oracle import oracle
-    u = res[res["is_dup"] == 0]
+    u = unique_queue(res)
     fo = np.asarray(file_off, dtype=np.uint64)
     src_off = fo[u["file"].astype(np.int64)] + u["offset"]
     lens = u["length"].astype(np.uint64)
@@ -508,7 +524,7 @@ def time_pack(ctx, data, res, file_off, reps):
     import numpy as np
     import torch
     from oracle import pack_oracle as po
-    u = res[res["is_dup"] == 0]
+    u = unique_queue(res)
     fo = np.asarray(file_off, dtype=np.uint64)
     src_off = fo[u["file"].astype(np.int64)] + u["offset"]
     lens = u["length"].astype(np.uint64)
@@ -540,6 +556,58 @@ def time_pack(ctx, data, res, file_off, reps):
     return {"blobs": int(len(u)), "packfiles": int(len(plan)), "payload_bytes": payload,
             "packfile_bytes": int(total), "ms": round(ms, 3), "GBps": round(payload / (ms * 1e-3) / 1e9, 1),
             "bit_exact_packfile_sample": bool(ok)}
+
+
+def time_pack_l3(ctx, data, res, file_off, reps):
+    """The whole downstream chain of add_blob over every unique blob of the last batch, from HBM
+    to HBM (pack.rs:58-80, 115-227): level-3 zstd on the GPU (bw_pack_compress_device, the real
+    compressor's decisions, not store frames), write_packfiles' grouping over the frame sizes on
+    the host, sealing + packfile layout (bw_pack_build_compressed).  One packfile is checked byte
+    for byte against the oracle chain (zstd restatement -> seal -> serialize)."""
+    import numpy as np
+    import torch
+    from oracle import oracle as orc
+    from oracle import pack_oracle as po
+    u = unique_queue(res)
+    fo = np.asarray(file_off, dtype=np.uint64)
+    src_off = fo[u["file"].astype(np.int64)] + u["offset"]
+    lens = u["length"].astype(np.uint64)
+    rng = np.random.default_rng(5)
+    nonces = rng.integers(0, 256, (len(u), 12), dtype=np.uint8)
+    kinds = np.zeros(len(u), dtype=np.uint8)
+    prk = bytes(range(32))
+    out = None
+
+    def once():
+        nonlocal out
+        fl = ctx.pack_compress_device(data.data_ptr(), src_off, lens)
+        plan, total = ctx.pack_plan(fl, flags=0)
+        ids = np.random.default_rng(6).integers(0, 256, (len(plan), 12), dtype=np.uint8)
+        if out is None or out.numel() < total:
+            out = torch.empty(total, dtype=torch.uint8, device=data.device)
+        ctx.pack_build_compressed(prk, u["digest"], kinds, nonces, plan, ids, out.data_ptr())
+        return fl, plan, total, ids
+
+    once()  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(max(1, reps)):
+        fl, plan, total, ids = once()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / max(1, reps)
+    k = int(rng.integers(0, len(plan)))
+    p = plan[k]
+    blobs = []
+    for i in range(int(p["first_blob"]), int(p["first_blob"] + p["n_blobs"])):
+        pt = data[int(src_off[i]):int(src_off[i] + lens[i])].cpu().numpy().tobytes()
+        blobs.append((bytes(u["digest"][i]), 0, bytes(nonces[i]),
+                      po.seal_blob_payload(prk, u["digest"][i], nonces[i], orc.zstd3_compress(pt))))
+    got = out[int(p["offset"]):int(p["offset"] + p["size"])].cpu().numpy().tobytes()
+    ok = got == po.serialize_packfile(prk, bytes(ids[k]), blobs)
+    payload = int(np.sum(lens))
+    return {"blobs": int(len(u)), "packfiles": int(len(plan)), "payload_bytes": payload,
+            "frame_bytes": int(np.sum(fl)), "packfile_bytes": int(total), "ms": round(ms, 3),
+            "GBps": round(payload / (ms * 1e-3) / 1e9, 1), "bit_exact_packfile_sample": bool(ok)}
 
 
 def pmc_traffic(args, kernel):

@@ -357,6 +357,21 @@ int bw_zstd_compress_device(bw_ctx* ctx, const uint8_t* d_src, const uint64_t* s
 int bw_zstd_compress(bw_ctx* ctx, const uint8_t* src, const uint64_t* src_off, const uint64_t* src_len, uint64_t n,
                      uint8_t* dst, const uint64_t* dst_off, uint64_t* frame_len);
 
+/* compress_encrypt_blob + write_packfiles end to end (pack.rs:58-80, 115-227) for a queue of
+ * unique blobs in device memory, in two calls around the caller's plan:
+ *   1. bw_pack_compress_device: zstd level 3 of blob i (d_src + src_off[i], src_len[i] <= 3 MiB,
+ *      else BW_EINVAL) into a staging area the context owns; frame_len[i] (host) = its frame's
+ *      size (synchronous);
+ *   2. the caller plans over those sizes -- bw_pack_plan(frame_len, n, 0, ...) or
+ *      bw_pack_plan_session(..., frame_len, ..., 0, ...) -- and draws one id per packfile;
+ *   3. bw_pack_build_compressed: the staged frames sealed (derive_backup_key(hashes[i]), nonces[i])
+ *      and laid out as bw_pack_build_device does with flags 0 (asynchronous on the context stream).
+ * The staged frames stay valid until the next bw_pack_compress_device on the same context. */
+int bw_pack_compress_device(bw_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
+                            uint64_t n, uint64_t* frame_len);
+int bw_pack_build_compressed(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* hashes, const uint8_t* kinds,
+                             const uint8_t* nonces, const bw_packfile* plan, uint64_t npf, const uint8_t* ids,
+                             uint8_t* d_out);
 /* Size of the zstd store frame of a len-byte blob. */
 uint64_t bw_zstd_store_size(uint64_t len);
 /* Grouping and sizes (host only).  out may be NULL with cap 0 to query *n_out; BW_ENOSPC when

@@ -262,6 +262,47 @@ def test_pack_build_device_precompressed(ctx, po):
 
 
 @pytest.mark.gpu
+def test_pack_compressed_chain_matches_oracle(ctx, po, oracle):
+    """compress_encrypt_blob + write_packfiles end to end on the device (pack.rs:58-80, 115-227):
+    level-3 frames of a queue of mixed blobs (text, repeats, runs, random, tiny) staged by
+    bw_pack_compress_device, the reference's grouping over the frame sizes, and the sealed
+    packfiles from bw_pack_build_compressed -- equal byte for byte to the oracle chain (the zstd
+    restatement, pinned to libzstd level 3, then seal + serialize) and read back through get_blob
+    + libzstd.  The queue sits at ragged device offsets and spans several packfiles."""
+    import torch
+    import zstd_corpus
+    z = _zstd()
+    rng = np.random.default_rng(31)
+    kinds_c = ["text", "repeats", "runs", "random", "tokens", "mixed"]
+    raw = [zstd_corpus.blob(kinds_c[i % 6], int(n), i) for i, n in
+           enumerate(list(rng.integers(0, 3 << 20, 18)) + [0, 1, 5, 3 << 20, 131072, 131073])]
+    src, offs, lens = _concat(raw, align=3)
+    _, hashes, kinds, nonces = _blob_set([len(d) for d in raw], 41)
+    d_src = torch.from_numpy(src).cuda()
+    fl = ctx.pack_compress_device(d_src.data_ptr(), offs, lens)
+    frames = [oracle.zstd3_compress(d) for d in raw]
+    assert [int(x) for x in fl] == [len(f) for f in frames]
+    plan, total = ctx.pack_plan(fl, flags=0)
+    assert len(plan) > 2
+    ids = rng.integers(0, 256, (len(plan), 12), dtype=np.uint8)
+    d_out = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    ctx.pack_build_compressed(PRK, hashes, kinds, nonces, plan, ids, d_out.data_ptr())
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().tobytes()
+    want = b"".join(b for _, b in _oracle_packs(po, frames, hashes, kinds, nonces, ids, store=False))
+    assert got == want
+    for i, d in enumerate(raw):
+        k = int(np.searchsorted(plan["first_blob"], i, side="right") - 1)
+        p = plan[k]
+        buf = got[int(p["offset"]):int(p["offset"] + p["size"])]
+        assert z.decompress(po.get_blob(PRK, bytes(ids[k]), buf, bytes(hashes[i]))[1]) == d
+    # a plan that does not cover the staged queue is refused
+    from backuwup_amd._lib import BwError
+    with pytest.raises(BwError):
+        ctx.pack_build_compressed(PRK, hashes, kinds, nonces, plan[:1], ids, d_out.data_ptr())
+
+
+@pytest.mark.gpu
 def test_pack_build_blob_count_limit(ctx, po):
     """100 003 tiny caller payloads: the first packfile closes at PACKFILE_MAX_BLOBS (a 5-byte Vec
     length).  Store frames never get there (>= 33 bytes per blob reach 3 MiB first)."""
