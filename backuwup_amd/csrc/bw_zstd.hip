@@ -522,14 +522,21 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 ZT_START();
                 ZT_COUNT(4);
                 // this lane's position in the skip sequence ip += ((ip - anchor) >> 8) + 1
-                uint32_t d = ip - anchor, j = lane;
-                if (d + 63 < 256) { d += j; j = 0; }  // step 1 for every lane: no divisions
-                while (j) {
-                    const uint32_t q = d >> 8, st = q + 1;
-                    const uint32_t stay = (((q + 1) << 8) - d + st - 1) / st;
-                    const uint32_t t = j < stay ? j : stay;
-                    d += t * st;
-                    j -= t;
+                uint32_t d = ip - anchor;
+                if (d + 63 < 256) {
+                    d += lane;  // step 1 for every lane
+                } else {
+                    // the skip sequence is uniform: walk it once in scalar registers and hand
+                    // position i to lane i (per-lane walks with a division per step change cost
+                    // ~2k VALU instructions a step on incompressible data, where the step grows
+                    // every position)
+                    uint32_t dd = __builtin_amdgcn_readfirstlane(d), pd = 0;
+                    const uint32_t w = __builtin_amdgcn_readfirstlane(W);
+                    for (uint32_t i = 0; i < w; i++) {
+                        pd = lane == i ? dd : pd;
+                        dd += (dd >> 8) + 1;
+                    }
+                    d = pd;
                 }
                 const uint32_t pos = anchor + d;
                 const bool valid = pos < ilimit && lane < W;
@@ -837,7 +844,9 @@ __global__ __launch_bounds__(ST_THREADS) void k_zs_stats(const uint8_t* __restri
     }
     const uint32_t litTotal = L.scanA[ST_THREADS - 1] + lastLL;
     const uint32_t srcTotal = L.scanB[ST_THREADS - 1];
-    const uint32_t seg = (litTotal + 3) / 4;
+    const uint32_t seg = (litTotal + 3) / 4, seg2 = 2 * seg, seg3 = 3 * seg;
+    // Huffman segment of literal i (i < litTotal <= 4 * seg): compares, not a division per byte
+    auto seg_of = [&](uint32_t i) -> uint32_t { return (uint32_t)(i >= seg) + (i >= seg2) + (i >= seg3); };
     uint8_t* lo = lits + blk->lit0;
     // literal gather + segment histograms + code histograms
     {
@@ -852,13 +861,13 @@ __global__ __launch_bounds__(ST_THREADS) void k_zs_stats(const uint8_t* __restri
                     for (uint32_t x = 0; x < ll; x++) {
                         const uint8_t c = s[si + x];
                         lo[li + x] = c;
-                        atomicAdd(&L.hist[wave][(li + x) / seg][c], 1u);
+                        atomicAdd(&L.hist[wave][seg_of(li + x)][c], 1u);
                     }
             } else {
                 for (uint32_t x = 0; x < ll; x++) {
                     const uint8_t c = s[si + x];
                     lo[li + x] = c;
-                    atomicAdd(&L.hist[wave][(li + x) / seg][c], 1u);
+                    atomicAdd(&L.hist[wave][seg_of(li + x)][c], 1u);
                 }
             }
             atomicAdd(&L.cll[ll_code(ll)], 1u);
@@ -870,11 +879,18 @@ __global__ __launch_bounds__(ST_THREADS) void k_zs_stats(const uint8_t* __restri
     }
     // the last literals
     {
-        const uint32_t li0 = litTotal - lastLL, si0 = srcTotal;
-        for (uint32_t x = t; x < lastLL; x += ST_THREADS) {
+        // four bytes per thread and step (a random block is one 128 KiB run of last literals)
+        const uint32_t li0 = litTotal - lastLL, si0 = srcTotal, n4 = lastLL & ~3u;
+        for (uint32_t x = 4 * t; x < n4; x += 4 * ST_THREADS) {
+            const uint32_t w = ld32(s + si0 + x);
+            *(u32u*)(lo + li0 + x) = w;
+#pragma unroll
+            for (int j = 0; j < 4; j++) atomicAdd(&L.hist[wave][seg_of(li0 + x + j)][(w >> (8 * j)) & 255u], 1u);
+        }
+        for (uint32_t x = n4 + t; x < lastLL; x += ST_THREADS) {
             const uint8_t c = s[si0 + x];
             lo[li0 + x] = c;
-            atomicAdd(&L.hist[wave][(li0 + x) / seg][c], 1u);
+            atomicAdd(&L.hist[wave][seg_of(li0 + x)][c], 1u);
         }
     }
     __syncthreads();
@@ -885,7 +901,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_zs_stats(const uint8_t* __restri
             for (uint32_t x = t; x < ll; x += ST_THREADS) {
                 const uint8_t c = s[si + x];
                 lo[li + x] = c;
-                atomicAdd(&L.hist[wave][(li + x) / seg][c], 1u);
+                atomicAdd(&L.hist[wave][seg_of(li + x)][c], 1u);
             }
         }
     }
