@@ -14,6 +14,7 @@ BW_ECRYPTO, BW_EFORMAT = -7, -8
 BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
 BW_OPT_DEPTH, BW_OPT_SCAN_SMALL_BYTES, BW_OPT_CAND_CAP, BW_OPT_STAGE_CHUNK, BW_OPT_B3_LOADS = 1, 2, 3, 4, 5
 BW_OPT_SCAN_WAVES, BW_OPT_LATENCY_STREAM, BW_OPT_ZSTD_SLOTS, BW_OPT_ZSTD_BATCH_BYTES = 6, 7, 8, 9
+BW_OPT_ORDER_HASH = 10
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -134,6 +135,9 @@ SIGNATURES = [
     ("bw_pack_compress_device", ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint64, u64p]),
     ("bw_pack_build_compressed", ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.POINTER(BwPackfile), ctypes.c_uint64,
                                                 vp, vp]),
+    ("bw_pack_compress", ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint64, u64p]),
+    ("bw_pack_build_compressed_host", ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.POINTER(BwPackfile),
+                                                     ctypes.c_uint64, vp, vp]),
     ("bw_index_files_build", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64,
                                             ctypes.POINTER(BwIndexFile), ctypes.c_uint64, u64p, u64p]),
     ("bw_index_load_files", ctypes.c_int, [vp, vp, vp, ctypes.POINTER(BwIndexFile), ctypes.c_uint64, vp,

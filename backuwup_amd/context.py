@@ -479,6 +479,32 @@ class Context:
                                                _ptr(ids), ctypes.c_void_p(d_out)), self.h)
         self._pack_keep = (h, kd, no, pl, ids, k)
 
+    def pack_compress(self, blobs):
+        """Host form of pack_compress_device over a list of bytes-like blobs; frame lengths."""
+        lens = np.array([len(b) for b in blobs], dtype=np.uint64)
+        so = np.zeros(len(blobs), dtype=np.uint64)
+        if len(blobs) > 1:
+            so[1:] = np.cumsum(lens[:-1])
+        src = np.frombuffer(b"".join(bytes(b) for b in blobs) or b"\0", dtype=np.uint8)
+        fl = np.zeros(len(blobs), dtype=np.uint64)
+        check(self._L.bw_pack_compress(self.h, _ptr(src), so.ctypes.data_as(_lib.u64p), lens.ctypes.data_as(_lib.u64p),
+                                       len(blobs), fl.ctypes.data_as(_lib.u64p)), self.h)
+        return fl
+
+    def pack_build_compressed_host(self, prk, hashes, kinds, nonces, plan, total, packfile_ids):
+        """Host form of pack_build_compressed: the planned packfiles back to back (numpy u8)."""
+        h = np.ascontiguousarray(np.asarray(hashes, dtype=np.uint8).reshape(-1, 32))
+        kd = np.ascontiguousarray(kinds, dtype=np.uint8)
+        no = np.ascontiguousarray(np.asarray(nonces, dtype=np.uint8).reshape(-1, 12))
+        pl = np.ascontiguousarray(plan, dtype=PACKFILE_DTYPE)
+        ids = np.ascontiguousarray(np.asarray(packfile_ids, dtype=np.uint8).reshape(-1, 12))
+        k = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(prk))
+        out = np.zeros(max(int(total), 1), dtype=np.uint8)
+        check(self._L.bw_pack_build_compressed_host(self.h, k, _ptr(h), _ptr(kd), _ptr(no),
+                                                    pl.ctypes.data_as(ctypes.POINTER(_lib.BwPackfile)), pl.size,
+                                                    _ptr(ids), _ptr(out)), self.h)
+        return out[:int(total)]
+
     def index_files_build(self, prk, entries, last_file_num=0):
         """BlobIndex::push + flush over n (hash, packfile id) entries (n x 44 bytes):
         [(file_num, bytes)] as the reference writes them to index/{file_num:0>10}."""

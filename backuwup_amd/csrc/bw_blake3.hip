@@ -411,8 +411,11 @@ __global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArray
 
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
                    uint64_t max_groups, uint32_t* cv_buf, uint32_t* cv_tmp, uint8_t* digests, int max_leaves,
-                   hipEvent_t between, int loads, hipStream_t upper) {
-    if (!max_blobs) return;
+                   hipEvent_t between, int loads, hipStream_t upper, hipEvent_t leaf_done) {
+    if (!max_blobs) {
+        if (leaf_done) hipEventRecord(leaf_done, st);
+        return;
+    }
 #ifndef BW_B3_DYN_LDS
 #define BW_B3_DYN_LDS 0  // A/B: extra LDS per block caps the blocks per CU (occupancy experiments)
 #endif
@@ -422,6 +425,7 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     else
         hipLaunchKernelGGL((k_b3_groups<true, 1, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
                            data, ctr, b, cv_buf, digests);
+    if (leaf_done) hipEventRecord(leaf_done, st);
     if (between) hipEventRecord(between, st);
     if (upper != st) hipStreamWaitEvent(upper, between, 0);
     st = upper;

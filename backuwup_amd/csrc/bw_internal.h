@@ -126,7 +126,8 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
                    uint64_t max_blobs, uint64_t max_groups, uint32_t* cv_buf,
                    uint32_t* cv_tmp /* like cv_buf */, uint8_t* digests, int max_leaves,
                    hipEvent_t between /* may be null */, int loads,
-                   hipStream_t upper /* stream of the upper tree levels; `between` must order it */);
+                   hipStream_t upper /* stream of the upper tree levels; `between` must order it */,
+                   hipEvent_t leaf_done = nullptr /* recorded on st right after the leaf pass */);
 
 // ------------------------------------------------------------------ launchers (bw_dedup.hip)
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),

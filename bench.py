@@ -100,8 +100,10 @@ def main():
                          "on 16 cores for the other workloads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="batches in flight: consecutive steps alternate between this many contexts/streams")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="batches in flight: consecutive steps alternate between this many contexts/streams "
+                         "(default 3 for C1's 1 GiB batches, whose fixed per-batch latency a third batch hides "
+                         "(1.42 -> 1.60 TB/s), 2 otherwise: a third gains nothing on large batches)")
     ap.add_argument("--host-stream", action="store_true",
                     help="batches start in pinned host memory (H2D copies overlapped with processing)")
     ap.add_argument("--trees", action="store_true",
@@ -118,6 +120,7 @@ def main():
                     help="k_b3_groups loads (BW_OPT_B3_LOADS): 0 = one block ahead, 1 = block pairs")
     ap.add_argument("--scan-waves", type=int, default=None, choices=[8, 16], help="BW_OPT_SCAN_WAVES")
     ap.add_argument("--latency-stream", type=int, default=None, choices=[0, 1], help="BW_OPT_LATENCY_STREAM")
+    ap.add_argument("--order-hash", type=int, default=None, choices=[0, 1], help="BW_OPT_ORDER_HASH")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
@@ -135,7 +138,7 @@ def main():
     import torch.distributed as dist
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
-    from backuwup_amd._lib import (BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM,
+    from backuwup_amd._lib import (BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
                                    BW_OPT_SCAN_WAVES, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
@@ -158,12 +161,14 @@ def main():
     log("rank %d: %s -- generated in %.1f s" % (rank, desc, time.time() - t0))
 
     # One backup session: every batch is gated by ONE index (bw_index) shared by the contexts.
-    # Device-resident: consecutive batches alternate between two contexts on two streams (one
+    # Device-resident: consecutive batches alternate between two (C1: three) contexts on their streams (one
     # batch's HBM-bound scan beside the other's VALU-bound BLAKE3), the index event chain keeps
     # their dedup in submission order, and batch k's results are read after batch k+1 is queued.
     # Host-streamed: one context; its copy stream brings batch k+1 from pinned host memory while
     # batch k computes (bw_submit_host).  N > 1: the local pass skips the index; each batch's
     # digests go through the RCCL exchange to their owner's index while the next batch computes.
+    if args.streams is None:
+        args.streams = 3 if args.workload == "c1" else 2
     nctx = 1 if args.host_stream and not multi else (2 if multi else max(1, args.streams))
     index = Index(local)
     ctxs, streams = [], []
@@ -178,6 +183,8 @@ def main():
             c.set_option(BW_OPT_SCAN_WAVES, args.scan_waves)
         if args.latency_stream is not None:
             c.set_option(BW_OPT_LATENCY_STREAM, args.latency_stream)
+        if args.order_hash is not None:
+            c.set_option(BW_OPT_ORDER_HASH, args.order_hash)
         if args.host_stream and nctx > 1:
             c.set_option(BW_OPT_DEPTH, 1)  # contexts alternate: one HBM input buffer each is enough
         ctxs.append(c)
@@ -245,7 +252,7 @@ def main():
             exchange(k, t)
         else:
             inflight.append((c, t))
-            if len(inflight) > 1:  # two batches in flight: read batch k-1 while batch k runs
+            if len(inflight) >= len(ctxs):  # one batch per context in flight: read the oldest while the rest run
                 c0, t0 = inflight.pop(0)
                 c0.wait(t0, out=out_buf)
 
@@ -323,7 +330,7 @@ def main():
     if iso is not None:
         # live durations above include the overlap with the other batch in flight
         a_iso = algo / (iso["b3_leaf" if kernel == "k_b3_groups" else "scan"] * 1e-3) / 1e9
-        roofline["live_shares_gpu_with"] = "the other batch in flight (%d contexts)" % len(ctxs)
+        roofline["live_shares_gpu_with"] = "the other batches in flight (%d contexts)" % len(ctxs)
         roofline["isolated"] = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
                                 "valu_issue_frac": (round(a_iso / B3_VALU_CEILING_GBS, 4)
                                                     if kernel == "k_b3_groups" else None),
@@ -346,7 +353,7 @@ def main():
                            "bytes_per_gpu": processed, "blobs_per_gpu": int(len(res)),
                            "files_per_gpu": len(file_len),
                            "parallelism": "dp%d (files sharded, index by digest prefix)" % world,
-                           "batches_in_flight": 2 if (len(ctxs) > 1 or host is not None) else 1,
+                           "batches_in_flight": len(ctxs) if len(ctxs) > 1 else (2 if host is not None else 1),
                            "index": "one shared index for every batch (a single backup session)"},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": check}
         if trees:

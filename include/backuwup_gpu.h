@@ -160,7 +160,11 @@ enum {
     BW_OPT_SCAN_WAVES = 6,       /* gear-scan workgroup: 16 waves (default) or 8 (leaves LDS for BLAKE3) */
     BW_OPT_LATENCY_STREAM = 7,   /* 1: the small kernels between the passes on a high-priority stream */
     BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (768 KiB of hash tables each; 16384) */
-    BW_OPT_ZSTD_BATCH_BYTES = 9  /* bw_zstd_*: input bytes per internal batch (~4.2x in scratch; 8 GiB) */
+    BW_OPT_ZSTD_BATCH_BYTES = 9, /* bw_zstd_*: input bytes per internal batch (~4.2x in scratch; 8 GiB) */
+    BW_OPT_ORDER_HASH = 10       /* 1: the scans and the BLAKE3 leaf passes of the contexts sharing an
+                                    index run one at a time each, in submission order (a batch's scan
+                                    then overlaps the previous batch's hashing); 0 (default): as soon
+                                    as their inputs are ready */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 
@@ -372,6 +376,13 @@ int bw_pack_compress_device(bw_ctx* ctx, const uint8_t* d_src, const uint64_t* s
 int bw_pack_build_compressed(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* hashes, const uint8_t* kinds,
                              const uint8_t* nonces, const bw_packfile* plan, uint64_t npf, const uint8_t* ids,
                              uint8_t* d_out);
+/* Host-buffer forms (synchronous): the blobs are staged through the device; the packfiles land
+ * in out (plan[npf-1].offset + plan[npf-1].size bytes). */
+int bw_pack_compress(bw_ctx* ctx, const uint8_t* src, const uint64_t* src_off, const uint64_t* src_len, uint64_t n,
+                     uint64_t* frame_len);
+int bw_pack_build_compressed_host(bw_ctx* ctx, const uint8_t prk[32], const uint8_t* hashes, const uint8_t* kinds,
+                                  const uint8_t* nonces, const bw_packfile* plan, uint64_t npf, const uint8_t* ids,
+                                  uint8_t* out);
 /* Size of the zstd store frame of a len-byte blob. */
 uint64_t bw_zstd_store_size(uint64_t len);
 /* Grouping and sizes (host only).  out may be NULL with cap 0 to query *n_out; BW_ENOSPC when

@@ -71,10 +71,13 @@ def test_tickets_ring(oracle):
             c.wait(tickets[3] + 1)
 
 
-def test_shared_index_two_contexts_six_batches(oracle):
-    """One session, two contexts on two streams, one index: six batches of C1 (tree corpus) and C4
-    (small files) data with duplicates across batches and contexts, submitted back to back (batch
-    k+1 queued before batch k is read); verdicts equal the oracle over the concatenated batches."""
+@pytest.mark.parametrize("nctx,order", [(2, 0), (3, 1)])
+def test_shared_index_two_contexts_six_batches(oracle, nctx, order):
+    """One session, two (three) contexts on their own streams, one index: six batches of C1 (tree
+    corpus) and C4 (small files) data with duplicates across batches and contexts, submitted back
+    to back (one batch per context in flight); verdicts equal the oracle over the concatenated
+    batches.  order = BW_OPT_ORDER_HASH (scans and leaf passes serialized across the contexts)."""
+    from backuwup_amd._lib import BW_OPT_ORDER_HASH
     import torch
     t_data, t_offs, t_lens = tree_corpus(48 << 20, seed=77, max_file=6 << 20)
     s_data, s_offs, s_lens = small_files(3000, seed=78)
@@ -87,20 +90,21 @@ def test_shared_index_two_contexts_six_batches(oracle):
     devs = [torch.from_numpy(d).cuda() for d, _, _ in batches]
     torch.cuda.synchronize()
     ix = Index(0)
-    ca, cb = Context(0), Context(0)
-    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    cs = [Context(0) for _ in range(nctx)]
+    ss = [torch.cuda.Stream() for _ in range(nctx)]
+    ca, cb = cs[0], cs[1]
     try:
-        ca.set_stream(sa.cuda_stream)
-        cb.set_stream(sb.cuda_stream)
-        ca.attach_index(ix)
-        cb.attach_index(ix)
+        for c, st in zip(cs, ss):
+            c.set_stream(st.cuda_stream)
+            c.attach_index(ix)
+            c.set_option(BW_OPT_ORDER_HASH, order)
         ca.index_reset(1 << 16)
         cb.index_seed(np.frombuffer(seed, dtype=np.uint8).reshape(-1, 32))
         got, pending = [None] * len(batches), []
         for k, (t, (d, o, l)) in enumerate(zip(devs, batches)):
-            c = (ca, cb)[k % 2]
+            c = cs[k % nctx]
             pending.append((k, c, c.submit_device(t.data_ptr(), d.size, o, l)))
-            if len(pending) > 1:
+            if len(pending) >= nctx:
                 j, cj, tj = pending.pop(0)
                 got[j] = cj.wait(tj)
         for j, cj, tj in pending:
@@ -112,8 +116,8 @@ def test_shared_index_two_contexts_six_batches(oracle):
         assert ca.index_size() == cb.index_size() == len(uniq)
         ca.index_check()
     finally:
-        ca.close()
-        cb.close()
+        for c in cs:
+            c.close()
         ix.close()
 
 

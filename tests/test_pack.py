@@ -296,6 +296,10 @@ def test_pack_compressed_chain_matches_oracle(ctx, po, oracle):
         p = plan[k]
         buf = got[int(p["offset"]):int(p["offset"] + p["size"])]
         assert z.decompress(po.get_blob(PRK, bytes(ids[k]), buf, bytes(hashes[i]))[1]) == d
+    # the host forms give the same packfiles
+    fl2 = ctx.pack_compress(raw)
+    assert np.array_equal(fl2, fl)
+    assert ctx.pack_build_compressed_host(PRK, hashes, kinds, nonces, plan, total, ids).tobytes() == want
     # a plan that does not cover the staged queue is refused
     from backuwup_amd._lib import BwError
     with pytest.raises(BwError):
