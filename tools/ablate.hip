@@ -2,7 +2,8 @@
 // (diagnostic only; not part of the product).  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17
 // -I backuwup_amd/csrc tools/ablate.hip -o build_ab/ablate ; run on an MI355X.
 //
-// For a 4 GiB random buffer it times:
+// `ablate scan|b3|both [seconds]` instead repeats one workload for that long (power sampling,
+// tools/gpu_ablate_power.sh).  For a 4 GiB random buffer it times:
 //   copy_strided   every lane reads its own 2 KiB strip in 128 B lines (the scan's pattern)
 //   copy_coalesced every lane reads 16 B at consecutive addresses (the HBM ceiling)
 //   scan_full      bw::k_scan exactly as shipped
@@ -12,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+
+#include <string>
 
 #include "bw_cdc.hip"
 #include "bw_blake3.hip"
@@ -117,16 +120,41 @@ static float timeit(F f, int reps = 5) {
     return ms / reps;
 }
 
-int main() {
+// Repeats f for `seconds` (power sampling: tools/gpu_ablate_power.sh runs amd-smi beside it).
+template <class F>
+static void hold(F f, double seconds, const char* name, double gb_per_call) {
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    CHECK(hipEventRecord(a, 0));
+    int calls = 0;
+    float ms = 0;
+    while (ms < seconds * 1e3) {
+        for (int i = 0; i < 20; i++) f();
+        calls += 20;
+        CHECK(hipEventRecord(b, 0));
+        CHECK(hipEventSynchronize(b));
+        CHECK(hipEventElapsedTime(&ms, a, b));
+    }
+    printf("hold %-8s %d calls in %.3f s: %.3f ms/call, %.1f GB/s\n", name, calls, ms / 1e3, ms / calls,
+           gb_per_call * calls / (ms / 1e3));
+    fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    const char* hold_what = argc > 1 ? argv[1] : nullptr;  // "scan", "b3" or "both": power mode
+    const double hold_s = argc > 2 ? atof(argv[2]) : 8.0;
     const uint64_t n = 4ull << 30;
     uint8_t* d;
-    uint32_t *out, *tc;
-    uint64_t* ts;
+    uint32_t *out, *tc, *ovf;
+    uint64_t *ts, *sctr;
     CHECK(hipMalloc(&d, n));
     CHECK(hipMalloc(&out, 64));
     const uint64_t tiles = n / SCAN_TILE;
     CHECK(hipMalloc(&tc, tiles * 4));
     CHECK(hipMalloc(&ts, tiles * SCAN_CAP * 8));
+    CHECK(hipMalloc(&ovf, tiles * 4));
+    CHECK(hipMalloc(&sctr, 16 * 8));
     {
         uint32_t* h = (uint32_t*)malloc(1 << 26);
         for (int i = 0; i < (1 << 24); i++) h[i] = (uint32_t)rand() * 2654435761u ^ (uint32_t)rand();
@@ -144,14 +172,20 @@ int main() {
     printf("copy_strided   %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { hipLaunchKernelGGL(copy_coalesced, dim3(4096), dim3(512), 0, 0, d, n, out); });
     printf("copy_coalesced %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
-    t = timeit([&] { launch_scan(0, d, n, tiles, mk, tc, ts, (uint32_t*)ts, (uint64_t*)out); });
+    auto scan_all = [&](hipStream_t st) {
+        CHECK(hipMemsetAsync(sctr, 0, 16 * 8, st));
+        launch_scan(st, d, n, tiles, mk, tc, ts, ovf, sctr, 16);
+    };
+    if (!hold_what) {
+    t = timeit([&] { scan_all(0); });
     printf("scan_full      %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
-    t = timeit([&] { launch_scan_t<512>(0, d, n, tiles, mk, tc, ts); });
+    t = timeit([&] { launch_scan(0, d, n, tiles, mk, tc, ts, ovf, sctr, 8); });
     printf("scan_b512      %8.3f ms %8.1f GB/s (8-wave blocks: leaves LDS for a co-resident kernel)\n", t, gb / t * 1e3);
     t = timeit([&] { hipLaunchKernelGGL(scan_noload<true>, dim3(512), dim3(512), 0, 0, n, mk, out); });
     printf("scan_noload    %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { hipLaunchKernelGGL(scan_noload<false>, dim3(512), dim3(512), 0, 0, n, mk, out); });
     printf("scan_nolds     %8.3f ms %8.1f GB/s (no LDS, no HBM)\n", t, gb / t * 1e3);
+    }
     {  // the shipped BLAKE3 kernels on 4096 blobs of 1 MiB (one unaligned start per blob)
         const uint64_t nb = 4096, blen = (1ull << 20) - 64;
         uint64_t *ctr, *bs, *bl, *bg, *fe, *gh;
@@ -171,28 +205,48 @@ int main() {
         CHECK(hipMemcpy(bl, tmp + nb, nb * 8, hipMemcpyHostToDevice));
         CHECK(hipMemcpy(bg, tmp + 2 * nb, nb * 8, hipMemcpyHostToDevice));
         free(tmp);
-        BlobArrays b{bs, bl, bg, bf, bk, fe, gh};
-        t = timeit([&] { launch_blake3(0, d, ctr, b, nb, nb * groups_per, cv, dig, (int)(blen / 1024 + 1), nullptr); });
-        printf("b3_full        %8.3f ms %8.1f GB/s (k_b3_groups + k_b3_tree, 4096 x 1 MiB blobs)\n", t,
+        uint32_t* cv2;
+        CHECK(hipMalloc(&cv2, nb * groups_per * 32));
+        BlobArrays b{bs, bl, bg, bf, bk, fe, gh, nb, n};
+        auto b3_all = [&](hipStream_t st) {
+            launch_blake3(st, d, ctr, b, nb, nb * groups_per, cv, cv2, dig, (int)(blen / 1024 + 1), nullptr,
+                          B3_LOADS_PAIRS, st);
+        };
+        if (hold_what) {
+            hipStream_t s1, s2;
+            CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+            CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+            const std::string w = hold_what;
+            if (w == "scan") hold([&] { scan_all(0); }, hold_s, "scan", gb);
+            else if (w == "b3") hold([&] { b3_all(0); }, hold_s, "b3", nb * blen / 1e9);
+            else hold([&] {
+                scan_all(s1);
+                b3_all(s2);
+                CHECK(hipStreamSynchronize(s1));
+                CHECK(hipStreamSynchronize(s2));
+            }, hold_s, "both", gb + nb * blen / 1e9);
+            return 0;
+        }
+        t = timeit([&] { b3_all(0); });
+        printf("b3_full        %8.3f ms %8.1f GB/s (k_b3_groups + k_b3_upper, 4096 x 1 MiB blobs)\n", t,
                nb * blen / 1e9 / t * 1e3);
         const unsigned g = (unsigned)((nb * groups_per + 255) / 256);
 #define B3V(P, W, name)                                                                                   \
-        t = timeit([&] { hipLaunchKernelGGL((k_b3_groups<P, W>), dim3(g), dim3(256), 0, 0, d, ctr, b, cv, dig); }); \
+        t = timeit([&] { hipLaunchKernelGGL((k_b3_groups<P, W, false>), dim3(g), dim3(256), 0, 0, d, ctr, b, cv, dig); }); \
         printf("%-14s %8.3f ms %8.1f GB/s (k_b3_groups only)\n", name, t, nb * blen / 1e9 / t * 1e3);
         B3V(true, 1, "b3g_pf")
         B3V(false, 1, "b3g_nopf")
-        B3V(false, 6, "b3g_nopf_w6")
-        B3V(false, 7, "b3g_nopf_w7")
-        B3V(true, 6, "b3g_pf_w6")
+        t = timeit([&] { hipLaunchKernelGGL((k_b3_groups<false, 1, true>), dim3(g), dim3(256), 0, 0, d, ctr, b, cv, dig); });
+        printf("%-14s %8.3f ms %8.1f GB/s (k_b3_groups only)\n", "b3g_pairs", t, nb * blen / 1e9 / t * 1e3);
 #undef B3V
         hipStream_t s1, s2;
         CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
         CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
         for (int blk : {1024, 512}) {
             t = timeit([&] {
-                if (blk == 1024) launch_scan_t<1024>(s1, d, n, tiles, mk, tc, ts);
-                else launch_scan_t<512>(s1, d, n, tiles, mk, tc, ts);
-                launch_blake3(s2, d, ctr, b, nb, nb * groups_per, cv, dig, (int)(blen / 1024 + 1), nullptr);
+                CHECK(hipMemsetAsync(sctr, 0, 16 * 8, s1));
+                launch_scan(s1, d, n, tiles, mk, tc, ts, ovf, sctr, blk == 1024 ? 16 : 8);
+                b3_all(s2);
                 CHECK(hipStreamSynchronize(s1));
                 CHECK(hipStreamSynchronize(s2));
             });
