@@ -2,7 +2,7 @@
 // (diagnostic only; not part of the product).  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17
 // -I backuwup_amd/csrc tools/ablate.hip -o build_ab/ablate ; run on an MI355X.
 //
-// `ablate scan|b3|both [seconds]` instead repeats one workload for that long (power sampling,
+// `ablate scan|b3|both|noload|nolds|copy|b3reg [seconds]` instead repeats one workload for that long (power sampling,
 // tools/gpu_ablate_power.sh).  For a 4 GiB random buffer it times:
 //   copy_strided   every lane reads its own 2 KiB strip in 128 B lines (the scan's pattern)
 //   copy_coalesced every lane reads 16 B at consecutive addresses (the HBM ceiling)
@@ -176,6 +176,39 @@ int main(int argc, char** argv) {
         CHECK(hipMemsetAsync(sctr, 0, 16 * 8, st));
         launch_scan(st, d, n, tiles, mk, tc, ts, ovf, sctr, 16);
     };
+    if (hold_what && std::string(hold_what) == "noload") {
+        hold([&] { hipLaunchKernelGGL(scan_noload<true>, dim3(512), dim3(512), 0, 0, n, mk, out); }, hold_s, "noload", gb);
+        return 0;
+    }
+    if (hold_what && std::string(hold_what) == "nolds") {
+        hold([&] { hipLaunchKernelGGL(scan_noload<false>, dim3(512), dim3(512), 0, 0, n, mk, out); }, hold_s, "nolds", gb);
+        return 0;
+    }
+    if (hold_what && std::string(hold_what) == "copy") {
+        hold([&] { hipLaunchKernelGGL(copy_strided, dim3(1024), dim3(512), 0, 0, d, n, out); }, hold_s, "copy", gb);
+        return 0;
+    }
+    if (hold_what && std::string(hold_what) == "copyhbm") {
+        hold([&] { hipLaunchKernelGGL(copy_coalesced, dim3(4096), dim3(512), 0, 0, d, n, out); }, hold_s, "copyhbm", gb);
+        return 0;
+    }
+    if (hold_what && std::string(hold_what) == "copymall") {  // 128 MiB, re-read: Infinity Cache resident
+        const uint64_t m = 128ull << 20;
+        hold([&] { for (int r = 0; r < 8; r++) hipLaunchKernelGGL(copy_coalesced, dim3(2048), dim3(512), 0, 0, d, m, out); },
+             hold_s, "copymall", 8 * m / 1e9);
+        return 0;
+    }
+    if (hold_what && std::string(hold_what) == "copyl2") {  // 16 MiB, re-read: L2 resident (4 MiB per XCD)
+        const uint64_t m = 16ull << 20;
+        hold([&] { for (int r = 0; r < 64; r++) hipLaunchKernelGGL(copy_coalesced, dim3(2048), dim3(512), 0, 0, d, m, out); },
+             hold_s, "copyl2", 64 * m / 1e9);
+        return 0;
+    }
+    if (hold_what && std::string(hold_what) == "b3reg") {
+        const uint64_t lanes = 256ull * 4096, bpl = n / 64 / lanes;
+        hold([&] { hipLaunchKernelGGL(b3_noload, dim3(4096), dim3(256), 0, 0, bpl, out); }, hold_s, "b3reg", gb);
+        return 0;
+    }
     if (!hold_what) {
     t = timeit([&] { scan_all(0); });
     printf("scan_full      %8.3f ms %8.1f GB/s\n", t, gb / t * 1e3);
