@@ -252,6 +252,21 @@ int main(int argc, char** argv) {
             const std::string w = hold_what;
             if (w == "scan") hold([&] { scan_all(0); }, hold_s, "scan", gb);
             else if (w == "b3") hold([&] { b3_all(0); }, hold_s, "b3", nb * blen / 1e9);
+            else if (w == "b3mall") {  // the same kernels over the first 128 blobs (128 MiB, cache-resident)
+                const uint64_t nm = 128;
+                uint64_t hc2[16] = {0};
+                hc2[C_NBLOBS] = nm;
+                hc2[C_NGROUPS] = nm * groups_per;
+                uint64_t* ctr2;
+                CHECK(hipMalloc(&ctr2, 16 * 8));
+                CHECK(hipMemcpy(ctr2, hc2, sizeof hc2, hipMemcpyHostToDevice));
+                BlobArrays b2{bs, bl, bg, bf, bk, fe, gh, nm, n};
+                hold([&] {
+                    for (int r = 0; r < 16; r++)
+                        launch_blake3(0, d, ctr2, b2, nm, nm * groups_per, cv, cv2, dig, (int)(blen / 1024 + 1), nullptr,
+                                      B3_LOADS_PAIRS, 0);
+                }, hold_s, "b3mall", 16 * nm * blen / 1e9);
+            }
             else hold([&] {
                 scan_all(s1);
                 b3_all(s2);
