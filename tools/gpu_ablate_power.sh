@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
 HOLD=${HOLD:-8}
-for w in scan b3 both; do
+for w in ${WHAT:-scan b3 both}; do
   ( for i in $(seq 1 200); do echo "T $(date +%s.%N)"; timeout -k 2 5 amd-smi metric -p -c 2>&1; sleep 0.1; done ) > "$OUT/power_$w.log" 2>&1 &
   P=$!
   sleep 1
@@ -18,4 +18,4 @@ for w in scan b3 both; do
   wait $P 2>/dev/null
   [ $RC -eq 0 ] || exit $RC
 done
-timeout -k 10 300 ./build_ab/ablate > "$OUT/ablate_times.log" 2>&1
+[ -n "${WHAT:-}" ] || timeout -k 10 300 ./build_ab/ablate > "$OUT/ablate_times.log" 2>&1
