@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--cpu-sample-mib", type=int, default=128)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--check", type=int, default=8, help="frames checked against the oracle")
+    ap.add_argument("--slots", type=int, default=None, help="BW_OPT_ZSTD_SLOTS (blobs parsed at once)")
     args = ap.parse_args()
 
     import numpy as np
@@ -48,6 +49,9 @@ def main():
     print("corpus %s %.2f GiB generated in %.1f s" % (args.kind, n / 2**30, time.time() - t0), file=sys.stderr)
 
     ctx = Context(0)
+    if args.slots:
+        from backuwup_amd._lib import BW_OPT_ZSTD_SLOTS
+        ctx.set_option(BW_OPT_ZSTD_SLOTS, args.slots)
     t = ctx.submit_device(data.data_ptr(), n, np.array([0], np.uint64), np.array([n], np.uint64), make_params())
     blobs = ctx.wait(t)
     src_off = blobs["offset"].astype(np.uint64)
