@@ -99,6 +99,7 @@ def main():
                     help="CPU baseline sample (default: 8 GiB of C2 on one core, ~10 s; up to 16 GiB of files "
                          "on 16 cores for the other workloads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-power", action="store_true", help="do not sample socket power during the timed steps")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--streams", type=int, default=None,
                     help="batches in flight: consecutive steps alternate between this many contexts/streams "
@@ -275,6 +276,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     host_ms[0] = 0.0
+    sampler = PowerSampler(local) if (rank == 0 and not args.no_power) else None
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -283,6 +285,7 @@ def main():
     if multi:
         dist.barrier()
     el = time.perf_counter() - t0
+    power = sampler.stop() if sampler else None
     if multi:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -327,6 +330,12 @@ def main():
                                   "frac": round(achieved / B3_VALU_CEILING_GBS, 4)}
     if host is not None:
         roofline.update({"host_stream_pcie_frac": round(value / PCIE_PEAK_GBS, 4)})
+    if power is not None:
+        # the limit the whole pipeline meets: the socket power cap; energy per byte
+        # of this GPU's share of the work = its power / its throughput
+        if power.get("samples"):
+            power["pj_per_byte"] = round(power["socket_w_median"] / (value / world * 1e9) * 1e12, 1)
+        roofline["power"] = power
     if iso is not None:
         # live durations above include the overlap with the other batch in flight
         a_iso = algo / (iso["b3_leaf" if kernel == "k_b3_groups" else "scan"] * 1e-3) / 1e9
@@ -370,6 +379,62 @@ def main():
     index.close()
     if multi:
         dist.destroy_process_group()
+
+
+class PowerSampler:
+    """Socket power and GFX clock of GPU `dev` sampled by `amd-smi metric -p -c` (read-only) in a
+    background thread while the timed steps run: the path holds the chip at its power cap
+    (DESIGN.md §5), so energy per byte = power / throughput is the figure that bounds it.  Absent
+    amd-smi, or any parse failure, yields no samples (the line then says so)."""
+
+    def __init__(self, dev):
+        import shutil
+        import subprocess
+        import threading
+        self.samples, self._stop = [], threading.Event()
+        self.exe = shutil.which("amd-smi")
+        self._sp = subprocess
+        self.dev = dev
+        self.t = threading.Thread(target=self._run, daemon=True)
+        if self.exe:
+            self.t.start()
+
+    def _run(self):
+        import re
+        args = [self.exe, "metric", "-p", "-c", "-g", str(self.dev)]
+        while not self._stop.is_set():
+            try:
+                out = self._sp.run(args, capture_output=True, text=True, timeout=5).stdout
+                if "SOCKET_POWER" not in out and "-g" in args:  # no GPU selector: the first GPU listed
+                    args = args[:4]
+                    out = self._sp.run(args, capture_output=True, text=True, timeout=5).stdout
+                    out = out.split("GPU: 1")[0]
+            except Exception:
+                return
+            m = re.search(r"SOCKET_POWER: (\d+) W", out)
+            gfx, clks = False, []
+            for line in out.splitlines():
+                if re.match(r"\s+GFX_\d+:", line):
+                    gfx = True
+                elif re.match(r"\s+(MEM|VCLK|DCLK|SOC|FCLK)", line):
+                    gfx = False
+                c = re.match(r"\s+CLK: (\d+) MHz", line)
+                if c and gfx:
+                    clks.append(int(c.group(1)))
+            if m and not self._stop.is_set():
+                self.samples.append((int(m.group(1)), sum(clks) / len(clks) if clks else None))
+            self._stop.wait(0.1)
+
+    def stop(self):
+        self._stop.set()
+        if self.exe:
+            self.t.join(timeout=10)
+        if not self.samples:
+            return {"samples": 0, "note": "amd-smi unavailable or unparsed"}
+        ps = sorted(p for p, _ in self.samples)
+        cs = [c for _, c in self.samples if c]
+        return {"samples": len(ps), "socket_w_median": ps[len(ps) // 2], "socket_w_max": ps[-1],
+                "gfx_mhz_mean": round(sum(cs) / len(cs)) if cs else None, "source": "amd-smi metric -p -c"}
 
 
 def cpu_model():
