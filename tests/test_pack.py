@@ -300,7 +300,15 @@ def test_pack_compressed_chain_matches_oracle(ctx, po, oracle):
     fl2 = ctx.pack_compress(raw)
     assert np.array_equal(fl2, fl)
     assert ctx.pack_build_compressed_host(PRK, hashes, kinds, nonces, plan, total, ids).tobytes() == want
+    # an empty queue stages nothing and builds nothing
+    assert ctx.pack_compress_device(d_src.data_ptr(), [], []).size == 0
+    plan0, total0 = ctx.pack_plan(np.zeros(0, np.uint64), flags=0)
+    assert len(plan0) == 0 and total0 == 0
+    ctx.pack_build_compressed(PRK, np.zeros((0, 32), np.uint8), [], np.zeros((0, 12), np.uint8), plan0,
+                              np.zeros((0, 12), np.uint8), d_out.data_ptr())
+    torch.cuda.synchronize()
     # a plan that does not cover the staged queue is refused
+    fl = ctx.pack_compress_device(d_src.data_ptr(), offs, lens)
     from backuwup_amd._lib import BwError
     with pytest.raises(BwError):
         ctx.pack_build_compressed(PRK, hashes, kinds, nonces, plan[:1], ids, d_out.data_ptr())
