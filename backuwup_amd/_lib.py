@@ -148,7 +148,7 @@ SIGNATURES = [
 
 STAGES = ["scan", "compact", "resolve", "assemble", "b3_leaf", "b3_tree", "dedup", "pack"]
 # the kernel each stage's events bracket (names as rocprofv3 reports them)
-STAGE_KERNELS = {"scan": "k_scan", "b3_leaf": "k_b3_groups", "b3_tree": "k_b3_tree"}
+STAGE_KERNELS = {"scan": "k_scan", "b3_leaf": "k_b3_groups", "b3_tree": "k_b3_upper"}
 
 _lib = None
 
