@@ -3,17 +3,38 @@
     let hash = blake3::hash(data).into();     // dir_packer.rs:286 (also :320, :353)
 
 `hash(data)` returns the 32-byte BlobHash computed on the GPU; `hash_many` hashes a batch of
-independent messages in one launch sequence (the batched form the GPU wants).
+independent messages in one launch sequence (the batched form the GPU wants: one call per file
+is a synchronous round trip).
 """
+import numpy as np
+
 from .context import default_context
 
 OUT_LEN = 32
 
 
+def _as_bytes_view(data):
+    if isinstance(data, np.ndarray):
+        if data.dtype != np.uint8:
+            raise TypeError("blake3: expected a uint8 array, got %s" % data.dtype)
+        return data.ravel()
+    return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+
+
 def hash(data, ctx=None):  # noqa: A001 - mirrors blake3::hash
-    return (ctx or default_context()).blake3(data)
+    """blake3::hash(data) -> 32 bytes (the crate's Hash converted with .into())."""
+    buf = _as_bytes_view(data)
+    return (ctx or default_context()).blake3(buf)
 
 
 def hash_many(data, offsets, lengths, ctx=None):
-    """digests (n x 32 uint8) of data[offsets[i] : offsets[i] + lengths[i]]."""
-    return (ctx or default_context()).blake3_many(data, offsets, lengths)
+    """Digests (n x 32 uint8) of data[offsets[i] : offsets[i] + lengths[i]] for every i, in one
+    batch.  Ranges may overlap; each must lie inside `data` (ValueError otherwise)."""
+    buf = _as_bytes_view(data)
+    offs = np.asarray(offsets, dtype=np.uint64).ravel()
+    lens = np.asarray(lengths, dtype=np.uint64).ravel()
+    if offs.shape != lens.shape:
+        raise ValueError("blake3.hash_many: %d offsets but %d lengths" % (offs.size, lens.size))
+    if offs.size and int((offs + lens).max()) > buf.size:
+        raise ValueError("blake3.hash_many: a message runs past the end of the data")
+    return (ctx or default_context()).blake3_many(buf, offs, lens)

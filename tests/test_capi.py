@@ -83,3 +83,17 @@ def test_missing_library_fails_loudly(monkeypatch):
         _lib.load()
     monkeypatch.undo()
     importlib.reload(_lib)
+
+
+def test_blake3_module_validates_before_any_device_call():
+    """backuwup_amd.blake3 (the blake3::hash mirror) rejects malformed batches on the host."""
+    import numpy as np
+    import pytest
+    from backuwup_amd import blake3
+    data = np.zeros(100, dtype=np.uint8)
+    with pytest.raises(ValueError):
+        blake3.hash_many(data, [0, 10], [5])
+    with pytest.raises(ValueError):
+        blake3.hash_many(data, [90], [11])
+    with pytest.raises(TypeError):
+        blake3.hash(np.zeros(4, dtype=np.uint32))
