@@ -733,9 +733,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     const bool do_hash = !(prm->flags & BW_F_NO_HASH);
     const bool do_dedup = do_hash && !(prm->flags & BW_F_NO_DEDUP);
 
-    // ---- the gear scan first: it needs only the batch buffer and the tile size, so it is enqueued
-    // before the host builds the batch's metadata (a batch then starts on the GPU ~0.1 ms earlier
-    // when nothing else is in flight, e.g. C1 with one batch in flight)
+    // ---- the scan's tiles and buffers
     uint64_t ncf_pre = 0;
     for (uint64_t f = 0; f < nf; f++) ncf_pre += flen[f] > prm->small_file_threshold && flen[f] > 0;
     // small batches scan half-size tiles: with one 128 KiB tile per wave the per-tile start
@@ -752,32 +750,6 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         rc0 |= ensure(c, s.ctr, C_COUNT * 8);
         if (rc0) return BW_ENOMEM;
     }
-    HIPCHK(c, hipMemsetAsync(s.ctr.p, 0, C_COUNT * 8, c->stream));
-    if (c->prof) {
-        c->ev_set ^= 1;
-        prof_collect(c, c->ev_set);  // the set about to be reused belongs to batch k-2
-    }
-    prof_mark(c, BW_STAGE_SCAN);
-    uint64_t* ctr = P<uint64_t>(s.ctr);
-    hipStream_t st = c->stream;
-    if (ncf_pre) {
-        bw_index* x = c->idx;
-        std::unique_lock<std::mutex> lk(x->mu, std::defer_lock);
-        if (c->order_hash) {
-            lk.lock();
-            if (x->scan_tail_set) HIPCHK(c, hipStreamWaitEvent(st, x->scan_tail, 0));
-        }
-        if (!launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
-                         P<uint32_t>(c->ovf), ctr, c->scan_waves)) {
-            c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
-            return BW_EINVAL;
-        }
-        if (c->order_hash) {
-            HIPCHK(c, hipEventRecord(x->scan_tail, st));
-            x->scan_tail_set = true;
-        }
-    }
-
     // ---- host metadata: CDC files, segments, canonical units
     const uint64_t L = seg_len_for(mk);
     // every chunk but a file's last is >= min(2*(min/2), max) bytes (max < min is legal in the crate)
@@ -947,11 +919,39 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     s.meta_pending = true;
     phase(2);
 
+    // The gear scan is enqueued after the metadata upload, not before the host builds the tables:
+    // enqueued first, it made C3's two contexts fall into a slower phase in one run of two (1,647
+    // vs 1,871 GB/s; 1,859-1,864 this way) for no measurable gain elsewhere (profiles/r02/s31_reorder).
+    HIPCHK(c, hipMemsetAsync(s.ctr.p, 0, C_COUNT * 8, c->stream));
+    if (c->prof) {
+        c->ev_set ^= 1;
+        prof_collect(c, c->ev_set);  // the set about to be reused belongs to batch k-2
+    }
+    prof_mark(c, BW_STAGE_SCAN);
+    uint64_t* ctr = P<uint64_t>(s.ctr);
+    hipStream_t st = c->stream;
+    if (ncf_pre) {
+        bw_index* x = c->idx;
+        std::unique_lock<std::mutex> lk(x->mu, std::defer_lock);
+        if (c->order_hash) {
+            lk.lock();
+            if (x->scan_tail_set) HIPCHK(c, hipStreamWaitEvent(st, x->scan_tail, 0));
+        }
+        if (!launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
+                         P<uint32_t>(c->ovf), ctr, c->scan_waves)) {
+            c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
+            return BW_EINVAL;
+        }
+        if (c->order_hash) {
+            HIPCHK(c, hipEventRecord(x->scan_tail, st));
+            x->scan_tail_set = true;
+        }
+    }
+
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len};
 
-    // ---- chunking (the scan, already enqueued on the context stream; the latency-bound kernels
-    // after it and the metadata upload on `lat`)
+    // ---- chunking (the scan on the context stream, the latency-bound kernels after it on `lat`)
     const bool split = c->lat_split;
     hipStream_t lat = split ? c->hi : st;
     if (split) {
