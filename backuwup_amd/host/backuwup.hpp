@@ -12,6 +12,7 @@
 //   dir_packer::process_file           dir_packer.rs:231-282 (batched over many files)
 //   Tree / split_serialize_tree / add_tree_to_blobs   filesystem/mod.rs:63-77, dir_packer.rs:314-390
 //   Manager::write_packfiles / serialize_packfile      packfile/pack.rs:115-227
+//   compress_encrypt_blob (zstd level 3) + write_packfiles   packfile/pack.rs:58-80
 //   BlobIndex::flush / load (index files)              packfile/blob_index.rs:151-240
 #pragma once
 
@@ -273,6 +274,42 @@ inline std::vector<std::pair<PackfileId, std::vector<uint8_t>>> write_packfiles(
     for (size_t k = 0; k < np; k++) idb.insert(idb.end(), ids[k].begin(), ids[k].end());
     check(bw_pack_build(ctx.get(), prk.data(), data.data(), offs.data(), lens.data(), lens.size(), hashes.data(),
                         kinds.data(), nb.data(), BW_PACK_ZSTD_STORE, plan.data(), np, idb.data(), out.data()),
+          ctx.get());
+    std::vector<std::pair<PackfileId, std::vector<uint8_t>>> res;
+    for (size_t k = 0; k < np; k++)
+        res.emplace_back(ids[k], std::vector<uint8_t>(out.begin() + plan[k].offset,
+                                                      out.begin() + plan[k].offset + plan[k].size));
+    return res;
+}
+
+// compress_encrypt_blob + write_packfiles with the reference's level-3 zstd (pack.rs:58-80,
+// 115-227): the frames are made and staged on the GPU, the grouping runs over their sizes, and the
+// packfiles are sealed from the staging.  ids must hold at least the resulting packfile count
+// (8 per blob is always enough).  Returns (id, bytes) per packfile.
+inline std::vector<std::pair<PackfileId, std::vector<uint8_t>>> write_packfiles_zstd(
+    Context& ctx, const std::array<uint8_t, 32>& prk, const std::vector<Blob>& blobs,
+    const std::vector<BlobNonce>& nonces, const std::vector<PackfileId>& ids) {
+    std::vector<uint64_t> lens, offs, frame(blobs.size());
+    std::vector<uint8_t> data, hashes, kinds, nb;
+    for (size_t i = 0; i < blobs.size(); i++) {
+        offs.push_back(data.size());
+        lens.push_back(blobs[i].data.size());
+        data.insert(data.end(), blobs[i].data.begin(), blobs[i].data.end());
+        hashes.insert(hashes.end(), blobs[i].hash.begin(), blobs[i].hash.end());
+        kinds.push_back((uint8_t)blobs[i].kind);
+        nb.insert(nb.end(), nonces.at(i).begin(), nonces.at(i).end());
+    }
+    check(bw_pack_compress(ctx.get(), data.data(), offs.data(), lens.data(), lens.size(), frame.data()), ctx.get());
+    uint64_t np = 0, total = 0;
+    const int rc = bw_pack_plan(frame.data(), frame.size(), 0, nullptr, 0, &np, &total);
+    if (rc != BW_ENOSPC && rc != BW_OK) check(rc);
+    std::vector<bw_packfile> plan(np);
+    check(bw_pack_plan(frame.data(), frame.size(), 0, plan.data(), plan.size(), &np, &total));
+    if (ids.size() < np) throw Error(BW_EINVAL, "not enough packfile ids");
+    std::vector<uint8_t> idb, out(total);
+    for (size_t k = 0; k < np; k++) idb.insert(idb.end(), ids[k].begin(), ids[k].end());
+    check(bw_pack_build_compressed_host(ctx.get(), prk.data(), hashes.data(), kinds.data(), nb.data(), plan.data(), np,
+                                        idb.data(), out.data()),
           ctx.get());
     std::vector<std::pair<PackfileId, std::vector<uint8_t>>> res;
     for (size_t k = 0; k < np; k++)

@@ -99,5 +99,28 @@ int main() {
     }
     auto items = index_load(ctx, prk, files);
     printf("index-load %zu %d\n", items.size(), (int)std::is_sorted(items.begin(), items.end()));
+    // the level-3 chain over compressible blobs (tests/test_cpp_host.py rebuilds the same bytes)
+    std::vector<Blob> zb;
+    std::vector<BlobNonce> zn;
+    const size_t zsizes[4] = {0, 5000, 200000, (1u << 20) + 17};
+    for (size_t j = 0; j < 4; j++) {
+        Blob bl;
+        bl.data.resize(zsizes[j]);
+        for (size_t i = 0; i < zsizes[j]; i++) bl.data[i] = (uint8_t)('a' + ((i * (j + 3)) / 7) % 26);
+        bl.hash = blake3::hash(ctx, bl.data.data(), bl.data.size());
+        bl.kind = BlobKind::FileChunk;
+        zb.push_back(bl);
+        BlobNonce nn;
+        for (int k = 0; k < 12; k++) nn[k] = (uint8_t)(3 * j + k + 1);
+        zn.push_back(nn);
+    }
+    std::vector<PackfileId> zids(8);
+    for (size_t p = 0; p < zids.size(); p++)
+        for (int k = 0; k < 12; k++) zids[p][k] = (uint8_t)(0x30 + 16 * p + k);
+    for (const auto& pk : write_packfiles_zstd(ctx, prk, zb, zn, zids)) {
+        printf("packfile-zstd %zu ", pk.second.size());
+        for (auto x : pk.second) printf("%02x", x);
+        printf("\n");
+    }
     return 0;
 }

@@ -65,3 +65,16 @@ def test_cpp_mirror_parity(tmp_path, oracle):
     files = [(int(l.split()[1]), bytes.fromhex(l.split()[2])) for l in out if l.startswith("index ")]
     assert files == po.push_and_flush(prk, 9, ents)
     assert "index-load 4 1" in out
+    # the level-3 chain (write_packfiles_zstd) against the oracle chain: zstd restatement (pinned
+    # to libzstd level 3) -> seal -> packfile layout
+    zb = []
+    for j, n in enumerate([0, 5000, 200000, (1 << 20) + 17]):
+        d = bytes(ord("a") + ((i * (j + 3)) // 7) % 26 for i in range(n))
+        h = oracle.blake3(d)
+        nonce = bytes(3 * j + k + 1 for k in range(12))
+        zb.append((h, 0, nonce, po.seal_blob_payload(prk, h, nonce, oracle.zstd3_compress(d))))
+    zgroups = po.plan_packfiles([len(b[3]) for b in zb])
+    zids = [bytes(0x30 + 16 * p + k for k in range(12)) for p in range(len(zgroups))]
+    zwant = po.write_packfiles(prk, zb, zids)
+    zgot = [bytes.fromhex(l.split()[2]) for l in out if l.startswith("packfile-zstd ")]
+    assert zgot == [b for _, b in zwant] and len(zgot) >= 1
