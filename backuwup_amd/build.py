@@ -14,14 +14,16 @@ LIB = os.path.join(HERE, "libbackuwup_amd.so")
 # BW_DEBUG build: the same sources with device bounds asserts (BW_ASSERT in csrc/bw_device.h); loaded
 # only when BW_LIB points at it (tools/debug_check.py), never by the product path
 LIB_DEBUG = os.path.join(HERE, "libbackuwup_amd_debug.so")
-SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_tree.hip", "bw_seal.hip", "bw_pack.hip", "bw_zstd.hip"]
+SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_comm.hip", "bw_tree.hip", "bw_seal.hip",
+           "bw_pack.hip", "bw_zstd.hip"]
+ROCM_LIB = "/opt/rocm/lib"
 ARCH = os.environ.get("BW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
 # sources that are not on the chunk -> hash -> dedup path the bench profiles (their kernels never
 # run in the C2 command), so editing them does not make the committed PMC traffic stale
-OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip")
+OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip", "bw_comm.hip")
 
 
 def source_digest():
@@ -81,7 +83,10 @@ def build(force=False, verbose=False, debug=False, jobs=8, variant=None, defines
 
     with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(SOURCES)))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
+    # RCCL for the digest exchange (bw_comm.hip); under torch the process's already-loaded librccl.so.1
+    # (same soname) is the one bound, so a process holds one RCCL
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + \
+        ["-L" + ROCM_LIB, "-lrccl", "-Wl,-rpath," + ROCM_LIB]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd, cwd=CSRC)

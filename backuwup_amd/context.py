@@ -569,6 +569,14 @@ class Context:
                                      ctypes.byref(mx)), self.h)
         return n.value, d.value, dup.value, mx.value
 
+    def exchange_dedup(self, comm, ticket=0):
+        """Batch `ticket` (submitted with BW_F_NO_DEDUP) through the digest-prefix exchange of
+        `comm` (a backuwup_amd.comm.Comm): its verdicts land in the batch's results."""
+        rc = self._L.bw_exchange_dedup(self.h, comm.h, int(ticket))
+        if rc == _lib.BW_ECOMM:
+            raise _lib.BwError(rc, comm.last_error() or self._L.bw_last_error(self.h).decode())
+        check(rc, self.h)
+
     def partition_buckets(self, d_digests, d_n, max_n, cap, n_owners, d_buckets, d_perm, d_counts):
         check(self._L.bw_partition_buckets(self.h, ctypes.c_void_p(d_digests), ctypes.c_void_p(d_n), max_n, cap,
                                            n_owners, ctypes.c_void_p(d_buckets), ctypes.c_void_p(d_perm),

@@ -95,11 +95,18 @@ struct bw_ctx {
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
     DevBuf cv, cv2, fstart, data, scratch, ucnt, ubtot;
     DevBuf bk_blk, bk_pack, bk_v;  // multi-GPU exchange buckets (bw_partition_buckets, ...)
+    // bw_exchange_dedup: my buckets and the ones received, their source positions, the counts
+    // (mine, received, and scratch for the capacity agreement), verdicts out and back
+    DevBuf ex_bk, ex_rbk, ex_perm, ex_cnt, ex_v, ex_rv;
 
     // batches in flight: ring of result slots addressed by ticket
     Slot slots[MAX_DEPTH];
     int depth = 2;
     uint64_t next_ticket = 1, last_ticket = 0;
+    // the synchronous helpers (bw_process_files, bw_fastcdc_chunks, bw_blake3_hash(_many), tree
+    // blobs) run in a slot of their own outside the ring: they never drop a batch the caller still
+    // holds a ticket for, and leave last_ticket (bw_results, bw_batch_views) unchanged
+    Slot sync_slot;
 
     // pageable host input: ring of pinned staging chunks on the copy stream
     PinBuf ring[STAGE_RING];
@@ -320,6 +327,18 @@ struct IndexOp {
 // the index (its tail) before the old buffers are replaced; sessions pre-size with bw_index_reset.
 static int index_capacity(bw_ctx* c, uint64_t incoming, hipStream_t st) {
     bw_index* x = c->idx;
+    if (x->table_cap && ((x->log_hi + incoming) > x->log_cap || (x->log_hi + incoming) * 2 > x->table_cap)) {
+        // Before growing, replace the host's bound by the real log length.  The bound adds every
+        // gate's max_n (a batch's len/min + 2 blobs, an exchange gate's n_src x cap slots) and only
+        // a result read tightens it, so without this a session whose batches are never read back
+        // (the multi-GPU exchange) would grow the table by its bounds, not its digests.  `st`
+        // already waits for the index tail and the lock is held, so once it drains the length is
+        // exact; growing synchronizes anyway.
+        uint64_t len = 0;
+        HIPCHK(c, hipMemcpyAsync(&len, P<uint64_t>(x->dstate) + D_LOGLEN, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        x->log_hi = std::min(x->log_hi, len);
+    }
     const uint64_t need_log = x->log_hi + incoming;
     if (need_log > x->log_cap) {
         uint64_t cap = x->log_cap ? x->log_cap : 1 << 16;
@@ -464,8 +483,8 @@ extern "C" int bw_create(int device, bw_ctx** out) {
         bw_destroy(c);
         return rc;
     }
-    for (int s = 0; s < MAX_DEPTH; s++) {
-        Slot& sl = c->slots[s];
+    for (int s = 0; s <= MAX_DEPTH; s++) {
+        Slot& sl = s < MAX_DEPTH ? c->slots[s] : c->sync_slot;
         if (hipEventCreateWithFlags(&sl.meta_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&sl.input_free, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) != hipSuccess) {
@@ -493,11 +512,13 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->fstart,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
-                     &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage};
+                     &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage,
+                     &c->ex_bk, &c->ex_rbk, &c->ex_perm, &c->ex_cnt, &c->ex_v, &c->ex_rv};
     for (DevBuf* b : all) free_dev(*b);
     zstd_work_free(c->zw);
     c->zw = nullptr;
-    for (Slot& s : c->slots) {
+    for (int k = 0; k <= MAX_DEPTH; k++) {
+        Slot& s = k < MAX_DEPTH ? c->slots[k] : c->sync_slot;
         free_dev(s.ctr);
         free_dev(s.digests);
         free_dev(s.is_dup);
@@ -1193,14 +1214,25 @@ static int upload_data(bw_ctx* c, const uint8_t* data, uint64_t len) {
     return BW_OK;
 }
 
+// A synchronous helper's batch: bytes already in c->data, enqueued into the context's own slot
+// (outside the ticket ring).
+static int submit_sync(bw_ctx* c, uint64_t data_len, const uint64_t* foff, const uint64_t* flen, uint64_t nf,
+                       const bw_params* prm) {
+    Slot& s = c->sync_slot;
+    s.ticket = 0;
+    return submit(c, s, P<uint8_t>(c->data), data_len, foff, flen, nf, prm);
+}
+
 extern "C" int bw_process_files(bw_ctx* c, const uint8_t* data, uint64_t data_len, const uint64_t* foff,
                                 const uint64_t* flen, uint64_t nf, const bw_params* prm, bw_blob* out, uint64_t cap,
                                 uint64_t* n_out) {
     if (!c || !n_out || (data_len && !data)) return BW_EINVAL;
     hipSetDevice(c->device);
+    bw_params def;
+    prm = params_or_default(prm, &def);
     if (int rc = upload_data(c, data, data_len)) return rc;
-    if (int rc = bw_process_files_device(c, P<uint8_t>(c->data), data_len, foff, flen, nf, prm)) return rc;
-    return bw_results(c, out, cap, n_out);
+    if (int rc = submit_sync(c, data_len, foff, flen, nf, prm)) return rc;
+    return slot_results(c, c->sync_slot, out, cap, n_out);
 }
 
 extern "C" int bw_fastcdc_chunks(bw_ctx* c, const uint8_t* src, uint64_t len, uint32_t mn, uint32_t av, uint32_t mx,
@@ -1264,11 +1296,8 @@ int bw::hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const ui
     bw_params_default(&p);
     p.flags = dedup ? 0 : BW_F_NO_DEDUP;
     p.small_file_threshold = ~0ull;  // every message is one whole blob, in the order given
-    Slot& s = claim_slot(c, nullptr);
-    if (int rc = submit(c, s, P<uint8_t>(c->data), total, offs, lens, n, &p)) {
-        s.ticket = 0;
-        return rc;
-    }
+    if (int rc = submit_sync(c, total, offs, lens, n, &p)) return rc;
+    Slot& s = c->sync_slot;
     HIPCHK(c, hipMemcpyAsync(hashes, s.digests.p, n * 32, hipMemcpyDeviceToHost, c->stream));
     if (dedup) HIPCHK(c, hipMemcpyAsync(dup, s.is_dup.p, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1355,6 +1384,55 @@ extern "C" int bw_scatter_verdicts(bw_ctx* c, const uint8_t* d_verdict, const ui
     hipSetDevice(c->device);
     launch_scatter(c->stream, d_verdict, d_perm, n, d_is_dup);
     HIPCHK(c, hipGetLastError());
+    return BW_OK;
+}
+
+// One batch through the digest-prefix exchange (include/backuwup_gpu.h): the steps of
+// backuwup_amd/sharded.py's exchange_dedup, behind one C call, enqueued on the context stream.
+extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
+    if (!c || !comm) return BW_EINVAL;
+    if (comm_device(comm) != c->device) {
+        c->err = "communicator and context live on different devices";
+        return BW_EINVAL;
+    }
+    Slot* s = slot_of(c, ticket ? ticket : c->last_ticket);
+    if (!s) {
+        c->err = "ticket " + std::to_string(ticket) + " is not (or no longer) held by the context";
+        return BW_ESTATE;
+    }
+    if (s->dedup) {
+        c->err = "the batch was gated by the local index already (submit it with BW_F_NO_DEDUP)";
+        return BW_ESTATE;
+    }
+    hipSetDevice(c->device);
+    const uint32_t W = (uint32_t)comm_world(comm);
+    hipStream_t st = c->stream;
+    if (int rc = ensure(c, c->ex_cnt, 4 * W * 8)) return rc;
+    uint64_t* cnt = P<uint64_t>(c->ex_cnt);  // [0, W): my counts, [W, 2W): received, [2W, 4W): scratch
+    uint64_t& cap = comm_cap(comm);
+    if (!cap)  // the session's bucket capacity: the largest per-batch bound over the ranks, once
+        if (int rc = comm_max(comm, s->max_blobs, &cap, cnt + 2 * W, st, c->err)) return rc;
+    const uint64_t slots = (uint64_t)W * cap;
+    int rc = 0;
+    rc |= ensure(c, c->ex_bk, slots * 32);
+    rc |= ensure(c, c->ex_rbk, slots * 32);
+    rc |= ensure(c, c->ex_perm, slots * 8);
+    rc |= ensure(c, c->ex_v, slots);
+    rc |= ensure(c, c->ex_rv, slots);
+    if (rc) return BW_ENOMEM;
+    const uint64_t* d_n = P<uint64_t>(s->ctr) + C_NBLOBS;
+    if (int r = bw_partition_buckets(c, P<uint8_t>(s->digests), d_n, s->max_blobs, cap, W, P<uint8_t>(c->ex_bk),
+                                     P<uint64_t>(c->ex_perm), cnt))
+        return r;
+    if (int r = comm_all_to_all(comm, cnt, cnt + W, 8, st, c->err)) return r;
+    if (int r = comm_all_to_all(comm, c->ex_bk.p, c->ex_rbk.p, cap * 32, st, c->err)) return r;
+    if (int r = bw_index_check_insert_buckets(c, P<uint8_t>(c->ex_rbk), cnt + W, W, cap, P<uint8_t>(c->ex_v)))
+        return r;
+    if (int r = comm_all_to_all(comm, c->ex_v.p, c->ex_rv.p, cap, st, c->err)) return r;
+    launch_bucket_scatter(st, P<uint8_t>(c->ex_rv), P<uint64_t>(c->ex_perm), cnt, W, cap, P<uint8_t>(s->is_dup),
+                          P<uint8_t>(s->packed));
+    HIPCHK(c, hipGetLastError());
+    s->dedup = true;  // bw_wait now reports the index's sticky errors for this batch
     return BW_OK;
 }
 
@@ -1805,22 +1883,27 @@ extern "C" int bw_pack_compress_device(bw_ctx* c, const uint8_t* d_src, const ui
                                        const uint64_t* src_len, uint64_t n, uint64_t* frame_len) {
     if (!c || (n && (!d_src || !src_off || !src_len || !frame_len))) return BW_EINVAL;
     hipSetDevice(c->device);
-    c->pk_stage_off.assign(n, 0);
-    c->pk_stage_len.assign(n, 0);
+    // whatever was staged before is gone; a call that fails leaves nothing staged, so a later
+    // bw_pack_build_compressed cannot seal stale staging bytes under a plan of empty frames
+    c->pk_stage_off.clear();
+    c->pk_stage_len.clear();
+    for (uint64_t i = 0; i < n; i++)
+        if (src_len[i] > BW_BLOB_MAX_UNCOMPRESSED_SIZE) {  // BlobTooLarge, pack.rs:32-34
+            c->err = "blob " + std::to_string(i) + " is larger than BLOB_MAX_UNCOMPRESSED_SIZE";
+            return BW_EINVAL;
+        }
+    std::vector<uint64_t> off(n);
     uint64_t out = 0;
     for (uint64_t i = 0; i < n; i++) {
-        if (src_len[i] > BW_BLOB_MAX_UNCOMPRESSED_SIZE) return BW_EINVAL;  // BlobTooLarge, pack.rs:32-34
-        c->pk_stage_off[i] = out;
+        off[i] = out;
         out += (bw_zstd_store_size(src_len[i]) + 15) & ~15ull;
     }
     if (int rc = ensure(c, c->pk_stage, out + 16)) return rc;
-    if (int rc = zstd_compress(c->stream, c->zw, d_src, src_off, src_len, n, P<uint8_t>(c->pk_stage),
-                               c->pk_stage_off.data(), frame_len, c->err)) {
-        c->pk_stage_off.clear();
-        c->pk_stage_len.clear();
+    if (int rc = zstd_compress(c->stream, c->zw, d_src, src_off, src_len, n, P<uint8_t>(c->pk_stage), off.data(),
+                               frame_len, c->err))
         return rc;
-    }
-    for (uint64_t i = 0; i < n; i++) c->pk_stage_len[i] = frame_len[i];
+    c->pk_stage_off = std::move(off);
+    c->pk_stage_len.assign(frame_len, frame_len + n);
     return BW_OK;
 }
 
@@ -1842,7 +1925,10 @@ extern "C" int bw_pack_build_compressed(bw_ctx* c, const uint8_t prk[32], const 
 // staging source, the packfiles come back into the caller's buffer (synchronous).
 extern "C" int bw_pack_compress(bw_ctx* c, const uint8_t* src, const uint64_t* src_off, const uint64_t* src_len,
                                 uint64_t n, uint64_t* frame_len) {
-    if (!c || (n && (!src || !src_off || !src_len || !frame_len))) return BW_EINVAL;
+    if (!c || (n && (!src_off || !src_len || !frame_len))) return BW_EINVAL;
+    // src may be NULL when every blob is empty (a queue of empty files has no bytes to point at)
+    for (uint64_t i = 0; i < n && !src; i++)
+        if (src_len[i]) return BW_EINVAL;
     hipSetDevice(c->device);
     std::vector<uint64_t> so(n);
     uint64_t in = 0;

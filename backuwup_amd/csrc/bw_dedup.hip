@@ -340,19 +340,22 @@ void launch_bucket_expand(hipStream_t st, const uint64_t* counts, uint32_t n_src
 // Source side: verdicts of my buckets back to blob order.
 __global__ void k_bucket_scatter(const uint8_t* __restrict__ verdict, const uint64_t* __restrict__ perm,
                                  const uint64_t* __restrict__ counts, uint32_t n_owners, uint64_t cap,
-                                 uint8_t* __restrict__ is_dup) {
+                                 uint8_t* __restrict__ is_dup, uint8_t* __restrict__ packed) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t o = i / cap, k = i % cap;
     if (o >= n_owners || k >= counts[o]) return;
-    is_dup[perm[i]] = verdict[i];
+    const uint64_t j = perm[i];
+    const uint8_t v = verdict[i];
+    is_dup[j] = v;
+    if (packed) packed[j * sizeof(bw_blob) + offsetof(bw_blob, is_dup)] = v;
 }
 
 void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, const uint64_t* counts,
-                           uint32_t n_owners, uint64_t cap, uint8_t* is_dup) {
+                           uint32_t n_owners, uint64_t cap, uint8_t* is_dup, uint8_t* packed) {
     const uint64_t n = (uint64_t)n_owners * cap;
     if (!n) return;
     hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, verdict, perm, counts,
-                       n_owners, cap, is_dup);
+                       n_owners, cap, is_dup, packed);
 }
 
 // ------------------------------------------------------------------ result records

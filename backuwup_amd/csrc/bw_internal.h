@@ -156,8 +156,9 @@ void launch_bucket_gather(hipStream_t st, const uint8_t* buckets, const uint64_t
                           uint8_t* out, uint64_t* n_out);
 void launch_bucket_expand(hipStream_t st, const uint64_t* counts, uint32_t n_src, uint64_t cap, const uint8_t* v_in,
                           uint8_t* v_out);
+// packed (may be null): the batch's bw_blob records, whose is_dup byte is written as well
 void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, const uint64_t* counts,
-                           uint32_t n_owners, uint64_t cap, uint8_t* is_dup);
+                           uint32_t n_owners, uint64_t cap, uint8_t* is_dup, uint8_t* packed = nullptr);
 void launch_pack(hipStream_t st, const uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
                  const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs);
 
@@ -221,6 +222,16 @@ uint8_t* message_stage(bw_ctx* c, size_t bytes);
 // verdict.  Synchronous; hashes (n x 32) and dup are host arrays.
 int hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const uint64_t* offs, const uint64_t* lens,
                   uint64_t n, bool dedup, uint8_t* hashes, uint8_t* dup);
+
+// ------------------------------------------------------------------ exchange transport (bw_comm.hip)
+int comm_rank(const bw_comm* c);
+int comm_world(const bw_comm* c);
+int comm_device(const bw_comm* c);
+uint64_t& comm_cap(bw_comm* c);
+// all-to-all of equal splits: d_recv[r * bytes ..] = rank r's d_send[my_rank * bytes ..]; on st
+int comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t bytes, hipStream_t st, std::string& err);
+// *out = max of v over the ranks (synchronous); scratch = device, >= 2 * world * 8 bytes
+int comm_max(bw_comm* c, uint64_t v, uint64_t* out, void* scratch, hipStream_t st, std::string& err);
 
 // ------------------------------------------------------------------ packfiles / index files (bw_pack.hip)
 constexpr uint32_t ZSTD_BLOCK = 131072;           // zstd ZSTD_BLOCKSIZE_MAX

@@ -299,7 +299,11 @@ inline std::vector<std::pair<PackfileId, std::vector<uint8_t>>> write_packfiles_
         kinds.push_back((uint8_t)blobs[i].kind);
         nb.insert(nb.end(), nonces.at(i).begin(), nonces.at(i).end());
     }
-    check(bw_pack_compress(ctx.get(), data.data(), offs.data(), lens.data(), lens.size(), frame.data()), ctx.get());
+    // all-empty queues (e.g. one empty file) leave `data` empty: hand the library a real pointer anyway
+    static const uint8_t none[1] = {0};
+    check(bw_pack_compress(ctx.get(), data.empty() ? none : data.data(), offs.data(), lens.data(), lens.size(),
+                           frame.data()),
+          ctx.get());
     uint64_t np = 0, total = 0;
     const int rc = bw_pack_plan(frame.data(), frame.size(), 0, nullptr, 0, &np, &total);
     if (rc != BW_ENOSPC && rc != BW_OK) check(rc);

@@ -47,7 +47,8 @@ enum {
     BW_ECOLLISION = -5, /* two distinct digests share a 64-bit table key: verdicts withheld    */
     BW_ESTATE = -6,     /* call order violated (e.g. bw_results before a batch was submitted)   */
     BW_ECRYPTO = -7,    /* an AES-GCM tag did not verify (PackfileError::CryptoError)           */
-    BW_EFORMAT = -8     /* bincode deserialization failed (PackfileError::SerializationError)   */
+    BW_EFORMAT = -8,    /* bincode deserialization failed (PackfileError::SerializationError)   */
+    BW_ECOMM = -9       /* the exchange transport failed (RCCL, or the caller's host all-to-all) */
 };
 
 /* fastcdc::v2020 size bounds (asserted by FastCDC::with_level) */
@@ -169,7 +170,10 @@ enum {
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 
 /* Whole front end for a batch of files stored back to back in a host buffer: chunk -> hash
- * -> dedup; synchronous; results in canonical order. */
+ * -> dedup; synchronous; results in canonical order.  Like every synchronous helper here
+ * (bw_fastcdc_chunks, bw_blake3_hash(_many), bw_tree_blobs) it runs in a slot of its own outside
+ * the ticket ring: it neither drops a batch the caller holds a ticket for nor changes which batch
+ * bw_results / bw_batch_views(0) name.  A too-small cap gives BW_ENOSPC (call again). */
 int bw_process_files(bw_ctx* ctx, const uint8_t* data, uint64_t data_len,
                      const uint64_t* file_off, const uint64_t* file_len, uint64_t n_files,
                      const bw_params* params, bw_blob* out, uint64_t cap, uint64_t* n_out);
@@ -243,6 +247,40 @@ int bw_index_check_insert_buckets(bw_ctx* ctx, const uint8_t* d_buckets, const u
 int bw_scatter_buckets(bw_ctx* ctx, const uint8_t* d_verdicts, const uint64_t* d_perm, const uint64_t* d_counts,
                        uint32_t n_owners, uint64_t cap, uint8_t* d_is_dup);
 
+/* ---- multi-GPU dedup behind one call per batch (RCCL over xGMI) ----
+ * The index partitioned by digest prefix across the ranks of a node replaces the one BlobIndex
+ * behind the packer mutex (packfile/mod.rs:77, blob_index.rs:130-148, pack.rs:37).  Every rank
+ * keeps its shard in its own context's index (or a bw_index its contexts share), submits its
+ * batches with BW_F_NO_DEDUP, and then calls bw_exchange_dedup once per batch, in the same batch
+ * order on every rank.  Files are sharded rank-major (rank r's batch k holds canonical files
+ * before rank r+1's batch k), so the owner gates the received buckets in canonical order.
+ * A communicator moves bytes between the ranks with an all-to-all of equal splits, either
+ *   - over RCCL: rank 0 draws an id with bw_comm_unique_id, the caller hands those 128 bytes to
+ *     every rank (any channel), and each rank calls bw_comm_init (blocks until all joined); or
+ *   - through the caller's own host transport (bw_comm_init_host): fn(user, send, recv, bytes)
+ *     must deliver send[r * bytes ..] to rank r's recv[my_rank * bytes ..] for every rank r;
+ *     buffers are pinned host memory, world * bytes long; nonzero return = failure. */
+#define BW_COMM_ID_BYTES 128u
+typedef struct bw_comm bw_comm;
+typedef int (*bw_host_all_to_all)(void* user, const void* send, void* recv, uint64_t bytes_per_rank);
+int bw_comm_unique_id(uint8_t id[BW_COMM_ID_BYTES]);
+/* world: a power of two <= 256; device must be the device of the contexts it serves. */
+int bw_comm_init(int device, int rank, int world, const uint8_t id[BW_COMM_ID_BYTES], bw_comm** out);
+int bw_comm_init_host(int device, int rank, int world, bw_host_all_to_all fn, void* user, bw_comm** out);
+void bw_comm_destroy(bw_comm* comm);
+const char* bw_comm_last_error(const bw_comm* comm);
+/* Digest slots per (source, owner) bucket for the session: 0 (default) = agreed at the first
+ * exchange as the largest max_blobs over the ranks (one synchronous all-to-all).  A later batch
+ * with more blobs for one owner than the capacity sets the sticky BW_ENOSPC of bw_index_check. */
+int bw_comm_set_capacity(bw_comm* comm, uint64_t cap);
+/* Batch `ticket` of ctx (0 = the most recent; submitted with BW_F_NO_DEDUP, else BW_ESTATE):
+ * partition its digests by owner = digest[0] >> (8 - log2 world), all-to-all of the counts and
+ * the buckets, the owner's gate against ctx's index, all-to-all of the verdicts back, scattered
+ * into the batch's is_dup (bw_wait / bw_batch_views see them).  Enqueued on ctx's stream with no
+ * host synchronization (RCCL; the host transport synchronizes inside).  Every rank calls it for
+ * its k-th batch in the same order. */
+int bw_exchange_dedup(bw_ctx* ctx, bw_comm* comm, uint64_t ticket);
+
 /* ---- tree blobs: split_serialize_tree + add_tree_to_blobs, dir_packer.rs:314-390 ----
  * Tree { kind: TreeKind, name: String, metadata: TreeMetadata { size, mtime, ctime: Option<u64> },
  *        children: Vec<BlobHash>, next_sibling: Option<BlobHash> }   (filesystem/mod.rs:63-77)
@@ -282,7 +320,7 @@ int bw_tree_serialize(const bw_tree* tree, const uint8_t* next_sibling, uint8_t*
  * first, each earlier piece with its successor's hash as next_sibling), then the dedup gate over
  * all pieces in canonical order (skipped with BW_F_NO_DEDUP in flags).  tree_hashes[32*i] = the
  * tree's hash (its first piece).  out (may be NULL) receives every piece; *n_out = pieces.
- * Runs through the context's batch machinery: read a batch's results before calling it. */
+ * Synchronous; runs in the context's own helper slot, so batches held by ticket stay readable. */
 int bw_tree_blobs(bw_ctx* ctx, const bw_tree* trees, uint64_t n, uint32_t flags, uint8_t* tree_hashes,
                   bw_tree_blob* out, uint64_t cap, uint64_t* n_out);
 

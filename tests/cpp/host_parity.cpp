@@ -122,5 +122,14 @@ int main() {
         for (auto x : pk.second) printf("%02x", x);
         printf("\n");
     }
+    // a queue of nothing but one empty file: the mirror's staging vector stays empty
+    Blob empty;
+    empty.hash = blake3::hash(ctx, data.data(), 0);
+    empty.kind = BlobKind::FileChunk;
+    for (const auto& pk : write_packfiles_zstd(ctx, prk, {empty}, {zn[0]}, zids)) {
+        printf("packfile-zstd-empty %zu ", pk.second.size());
+        for (auto x : pk.second) printf("%02x", x);
+        printf("\n");
+    }
     return 0;
 }

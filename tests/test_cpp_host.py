@@ -78,3 +78,9 @@ def test_cpp_mirror_parity(tmp_path, oracle):
     zwant = po.write_packfiles(prk, zb, zids)
     zgot = [bytes.fromhex(l.split()[2]) for l in out if l.startswith("packfile-zstd ")]
     assert zgot == [b for _, b in zwant] and len(zgot) >= 1
+    # all-empty queue (one empty file): one packfile holding one empty level-3 frame
+    e = (oracle.blake3(b""), 0, zb[0][2], po.seal_blob_payload(prk, oracle.blake3(b""), zb[0][2],
+                                                             oracle.zstd3_compress(b"")))
+    ewant = po.write_packfiles(prk, [e], zids[:1])
+    egot = [bytes.fromhex(l.split()[2]) for l in out if l.startswith("packfile-zstd-empty ")]
+    assert egot == [b for _, b in ewant]

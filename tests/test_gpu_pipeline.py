@@ -71,6 +71,33 @@ def test_tickets_ring(oracle):
             c.wait(tickets[3] + 1)
 
 
+def test_sync_helpers_leave_held_tickets_alone(oracle):
+    """the synchronous helpers (tree blobs, blake3.hash, process_files, fastcdc_chunks)
+    run outside the ticket ring.  With the default depth of 2, two submitted batches stay readable
+    after them, and bw_results still names the most recent submitted batch."""
+    import torch
+    data, offs, lens = small_files(2000, seed=61)
+    batches = _slices(data, offs, lens, [(0, 1000), (1000, 2000)])
+    want = oracle_session(oracle, batches)
+    devs = [torch.from_numpy(d).cuda() for d, _, _ in batches]
+    torch.cuda.synchronize()
+    with Context(0) as c:
+        c.index_reset()
+        tickets = [c.submit_device(t.data_ptr(), d.size, o, l) for t, (d, o, l) in zip(devs, batches)]
+        spec = (0, "f", 5, 1700000000, None, bytes(range(64)))
+        hashes, _ = c.tree_blobs([make_tree(*spec)], dedup=False)
+        assert bytes(hashes[0]) == oracle.split_serialize_tree(*spec)[0][1]
+        m = splitmix_bytes(8, 5000)
+        assert c.blake3(m) == oracle.blake3(m)
+        assert c.fastcdc_chunks(splitmix_bytes(9, 20000), *SMALL) == oracle.fastcdc(splitmix_bytes(9, 20000), *SMALL)
+        sm, so, sl = small_files(50, seed=62)
+        pf = c.process_files(sm, so, sl, make_params(flags=BW_F_NO_DEDUP))
+        assert np.array_equal(pf["digest"], oracle.process_files(sm, so, sl)["digest"])
+        for k in (0, 1):
+            blobs_equal(c.wait(tickets[k]), want[k], k)
+        blobs_equal(c.results(), want[1])
+
+
 @pytest.mark.parametrize("nctx,order", [(2, 0), (3, 1)])
 def test_shared_index_two_contexts_six_batches(oracle, nctx, order):
     """One session, two (three) contexts on their own streams, one index: six batches of C1 (tree
@@ -340,6 +367,105 @@ def test_device_shard_ops_two_ranks_one_gpu(oracle):
             assert np.array_equal(dig, want["digest"]) and np.array_equal(dup, want["is_dup"]), (batch, r)
             n_checked += int(want["is_dup"].sum())
     assert n_checked > 0
+
+
+def test_exchange_dedup_rccl_world1_c_abi(oracle):
+    """bw_comm_init (RCCL, world size 1) + bw_exchange_dedup per batch: four NO_DEDUP batches on
+    two contexts sharing one index, each sent through the exchange (partition, RCCL all-to-alls,
+    owner gate, verdicts back); bw_wait returns the verdicts of one global index."""
+    import torch
+    from backuwup_amd.comm import Comm, unique_id
+    data, offs, lens = small_files(4000, seed=71)
+    batches = _slices(data, offs, lens, [(0, 1000), (1000, 2000), (0, 1000), (2000, 4000)])
+    want = oracle_session(oracle, batches)
+    devs = [torch.from_numpy(d).cuda() for d, _, _ in batches]
+    torch.cuda.synchronize()
+    ix = Index(0)
+    cs = [Context(0), Context(0)]
+    comm = Comm.rccl(0, 0, 1, unique_id())
+    try:
+        for c in cs:
+            c.set_stream(torch.cuda.Stream().cuda_stream)
+            c.attach_index(ix)
+        cs[0].index_reset(1 << 16)
+        p = make_params(flags=BW_F_NO_DEDUP)
+        tickets = []
+        for k, (t, (d, o, l)) in enumerate(zip(devs, batches)):
+            tk = cs[k % 2].submit_device(t.data_ptr(), d.size, o, l, p)
+            cs[k % 2].exchange_dedup(comm, tk)
+            tickets.append(tk)
+        for k, tk in enumerate(tickets):
+            blobs_equal(cs[k % 2].wait(tk), want[k], k)
+        assert cs[0].wait(tickets[2])["is_dup"].all()
+        cs[0].index_check()
+        # a batch gated locally already cannot go through the exchange again
+        tk = cs[0].submit_device(devs[0].data_ptr(), batches[0][0].size, batches[0][1], batches[0][2])
+        with pytest.raises(BwError) as e:
+            cs[0].exchange_dedup(comm, tk)
+        assert e.value.rc == BW_ESTATE
+    finally:
+        for c in cs:
+            c.close()
+        comm.close()
+        ix.close()
+
+
+def _two_rank_c_worker(rank, world, port, q):
+    """One rank of the exchange through the C entry point (bw_exchange_dedup) with the caller's
+    host transport (bw_comm_init_host over gloo): two ranks share the one GPU, which RCCL refuses."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from backuwup_amd.comm import Comm, gloo_all_to_all
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data, offs, lens = small_files(6000, seed=56)
+        per = len(lens) // world
+        out = []
+        with Context(0) as c, Comm.host(0, rank, world, gloo_all_to_all()) as comm:
+            c.index_reset(1 << 16)
+            for batch in range(3):  # batch-major, then rank-major canonical order
+                lo = ((batch % 2) * world + rank) * per // 2
+                hi = lo + per // 2 - 7 * rank * (batch == 2)  # ragged: the ranks' batch sizes differ
+                b = _slices(data, offs, lens, [(lo, hi)])[0]
+                t_dev = torch.from_numpy(b[0]).cuda()
+                tk = c.submit_device(t_dev.data_ptr(), b[0].size, b[1], b[2], make_params(flags=BW_F_NO_DEDUP))
+                c.exchange_dedup(comm, tk)
+                res = c.wait(tk)
+                out.append((lo, hi, res["digest"].copy(), res["is_dup"].copy()))
+            c.index_check()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
+    """bw_exchange_dedup with two processes on the one GPU: every verdict equals one global index
+    over the canonical order (batch, rank, position), including a repeated batch (all duplicates)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_two_rank_c_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data, offs, lens = small_files(6000, seed=56)
+    ix = oracle.Index()
+    for batch in range(3):
+        for r in range(2):
+            lo, hi, dig, dup = got[r][batch]
+            want = oracle.process_files(*_slices(data, offs, lens, [(lo, hi)])[0], index=ix)
+            assert np.array_equal(dig, want["digest"]) and np.array_equal(dup, want["is_dup"]), (batch, r)
+    assert got[0][2][3].all()  # batch 2 repeats batch 0 on rank 0
 
 
 @pytest.mark.parametrize("scan_waves,latency,loads", [(8, 0, 1), (16, 1, 1), (8, 1, 0), (16, 0, 0)])
