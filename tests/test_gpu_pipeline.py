@@ -383,11 +383,13 @@ def test_exchange_dedup_rccl_world1_c_abi(oracle):
     ix = Index(0)
     cs = [Context(0), Context(0)]
     comm = Comm.rccl(0, 0, 1, unique_id())
+    comm2 = None
     try:
         for c in cs:
             c.set_stream(torch.cuda.Stream().cuda_stream)
             c.attach_index(ix)
         cs[0].index_reset(1 << 16)
+        comm.set_capacity(2000)  # the largest batch's bound (batch 3 holds 2000 small files)
         p = make_params(flags=BW_F_NO_DEDUP)
         tickets = []
         for k, (t, (d, o, l)) in enumerate(zip(devs, batches)):
@@ -403,10 +405,24 @@ def test_exchange_dedup_rccl_world1_c_abi(oracle):
         with pytest.raises(BwError) as e:
             cs[0].exchange_dedup(comm, tk)
         assert e.value.rc == BW_ESTATE
+        # capacity agreed at the first exchange (batch 0's 1000-blob bound): a later, larger batch
+        # overflows its bucket and says so instead of returning incomplete verdicts
+        from backuwup_amd._lib import BW_ENOSPC
+        cs[0].index_reset(1 << 16)
+        comm2 = Comm.rccl(0, 0, 1, unique_id())
+        for k in (0, 3):
+            d, o, l = batches[k]
+            tk = cs[0].submit_device(devs[k].data_ptr(), d.size, o, l, p)
+            cs[0].exchange_dedup(comm2, tk)
+        with pytest.raises(BwError) as e:
+            cs[0].wait(tk)
+        assert e.value.rc == BW_ENOSPC
     finally:
         for c in cs:
             c.close()
         comm.close()
+        if comm2 is not None:
+            comm2.close()
         ix.close()
 
 
