@@ -228,6 +228,183 @@ __global__ __launch_bounds__(256, MINW) void k_b3_groups(const uint8_t* __restri
     }
 }
 
+// ---------------------------------------------------------------- aligned-line leaf pass
+// k_b3_lines: the same work as k_b3_groups (one lane per aligned 4-leaf group), fed from whole
+// aligned 128-byte lines.  A group's bytes start at an arbitrary offset o of their first line, so
+// the 132-byte pair loads of b3_leaf_pairs touch every line twice, one compression pair apart,
+// and L2 has often evicted it in between (k_b3_groups fetched 1.41x its bytes).  Here every line
+// is loaded once (8 x 16-byte aligned loads per lane): lines p and p + 1 sit in registers (a, c)
+// and block b's 16 message words are cut at dword offset Q = o / 4 + 16 (b mod 2) of a || c with
+// the byte shift o mod 4.  Q must be a compile-time register index, so it is dispatched through a
+// switch on its wave-uniform value: every group of a blob has the blob's start offset mod 128
+// (4096 is a multiple of 128), so a wave whose lanes all lie in one blob shares one Q; a wave
+// across blobs takes the per-lane path of k_b3_groups instead.  The leaves' chaining values wait
+// in LDS and the group's parents are merged after the loop, so the loop holds no parent
+// compression.  A group's last line may extend past its blob's end: an aligned 128-byte line never
+// crosses a page, so the load is safe, and bytes at or past the end are masked out.
+
+// The alignbytes are volatile asm: as builtins, the optimizer either merges the cases into one
+// block fed by a ring indexed with the case number (scratch memory) or hoists every possible
+// word pair out of the switch (64 alignbytes and 224 VGPRs per block instead of 16).
+template <int Q>
+__device__ __forceinline__ void b3_cut16(const uint32_t a[32], const uint32_t c[32], uint32_t sh, uint32_t m[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t lo = Q + i < 32 ? a[Q + i] : c[Q + i - 32];
+        const uint32_t hi = Q + i + 1 < 32 ? a[Q + i + 1] : c[Q + i + 1 - 32];
+        asm volatile("v_alignbyte_b32 %0, %1, %2, %3" : "=v"(m[i]) : "v"(hi), "v"(lo), "v"(sh));
+    }
+}
+
+#define B3_CUT_CASE(q) \
+    case q: b3_cut16<q>(a, c, sh, m); break;
+#define B3_CUT_CASE8(q) \
+    B3_CUT_CASE(q) B3_CUT_CASE(q + 1) B3_CUT_CASE(q + 2) B3_CUT_CASE(q + 3) B3_CUT_CASE(q + 4) \
+    B3_CUT_CASE(q + 5) B3_CUT_CASE(q + 6) B3_CUT_CASE(q + 7)
+
+// m = the 16 words at dword offset u + 16 * H (u wave-uniform, 0..31) of a || c, shifted by sh bytes
+template <int H>
+__device__ __forceinline__ void b3_cut(const uint32_t a[32], const uint32_t c[32], uint32_t u, uint32_t sh,
+                                       uint32_t m[16]) {
+    if (H == 0) {
+        switch (u) { B3_CUT_CASE8(0) B3_CUT_CASE8(8) B3_CUT_CASE8(16) B3_CUT_CASE8(24) default: break; }
+    } else {
+        switch (u + 16) { B3_CUT_CASE8(16) B3_CUT_CASE8(24) B3_CUT_CASE8(32) B3_CUT_CASE8(40) default: break; }
+    }
+}
+
+// An aligned line of zeros: the target of the loads past a group's last line, so every load is
+// unconditional
+__device__ __attribute__((aligned(128))) uint4 g_b3_zero_line[8];
+
+__device__ __forceinline__ void b3_line_load(const uint4* __restrict__ src, uint32_t w[32]) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint4 v = src[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+}
+
+// One block of a group in k_b3_lines: mask past the blob's end, compress, and at a leaf's end
+// park its chaining value in LDS.
+__device__ __forceinline__ void b3_line_block(uint32_t m[16], uint32_t blk, uint32_t glen, uint32_t nblk, uint64_t n,
+                                              uint64_t first, uint32_t cv[8], uint32_t (*s_leaf)[8][256], int me) {
+    const uint32_t left = glen - 64 * blk;
+    const uint32_t blen = glen == 0 ? 0 : (left < 64 ? left : 64);
+    if (blen < 64) {  // the blob's last block: bytes at or past its end are zero
+        const uint32_t whole = blen >> 2, rem = blen & 3;
+        const uint32_t pmask = rem ? 0xffffffffu >> (32 - 8 * rem) : 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++) m[i] = i < whole ? m[i] : (i == whole ? m[i] & pmask : 0);
+    }
+    const uint32_t bil = blk & 15, leaf = blk >> 4;
+    const bool last = bil == 15 || blk + 1 == nblk;
+    if (bil == 0) b3_iv(cv);
+    uint32_t flags = bil == 0 ? B3_CHUNK_START : 0;
+    if (last) flags |= B3_CHUNK_END | (n == 1 ? B3_ROOT : 0);
+    b3_compress(cv, m, blen, first + leaf, flags);
+    if (last) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) s_leaf[leaf][i][me] = cv[i];
+    }
+}
+
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restrict__ data, const uint64_t* ctr,
+                                                        BlobArrays b, uint32_t* __restrict__ cv_buf,
+                                                        uint8_t* __restrict__ digests) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ctr[C_NGROUPS]) return;
+    const uint64_t nb = ctr[C_NBLOBS];
+    uint64_t lo = 0, hi = nb;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (b.goff[mid] <= g) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint64_t blob = lo - 1;
+    BW_ASSERT(lo >= 1 && blob < b.cap);
+    const uint64_t start = b.start[blob], len = b.len[blob], gi = g - b.goff[blob];
+    BW_ASSERT(start + len <= b.data_len && gi * 4 * B3_LEAF_BYTES <= (len ? len - 1 : 0));
+    const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
+    const uint64_t first = gi * 4;
+    const uint32_t k = (uint32_t)(n - first < 4 ? n - first : 4);
+    __shared__ uint32_t s_leaf[4][8][256];  // the group's leaf chaining values, word-major
+    const int me = threadIdx.x;
+    const uint8_t* gp = data + start + gi * 4 * B3_LEAF_BYTES;
+    const uint32_t o = (uint32_t)((uintptr_t)gp & 127);
+    const uint32_t q = o >> 2, sh = o & 3;
+    const uint32_t uq = __builtin_amdgcn_readfirstlane(q);
+    uint32_t cv[8];
+    if (__builtin_amdgcn_ballot_w64(q != uq) == 0) {
+        // the whole wave at one line offset: whole aligned lines, each loaded once
+        const uint64_t rest = len - gi * 4 * B3_LEAF_BYTES;
+        const uint32_t glen = len == 0 ? 0 : (uint32_t)(rest < 4 * B3_LEAF_BYTES ? rest : 4 * B3_LEAF_BYTES);
+        const uint32_t nblk = glen == 0 ? 1 : (glen + 63) / 64;
+        const uint4* lp = (const uint4*)(gp - o);
+        const uint32_t nlines = glen == 0 ? 0 : (o + glen + 127) / 128;
+        uint32_t a[32], c[32];
+        b3_line_load(nlines > 0 ? lp : g_b3_zero_line, a);
+        b3_line_load(nlines > 1 ? lp + 8 : g_b3_zero_line, c);
+        // two pairs per turn, the lines' roles alternating (a = line p, c = line p + 1, then the
+        // other way round), so the loop carries the two lines without copies
+#pragma unroll 1
+        for (uint32_t p = 0;; p += 2) {
+            uint32_t m[16];
+            b3_cut<0>(a, c, uq, sh, m);
+            b3_line_block(m, 2 * p, glen, nblk, n, first, cv, s_leaf, me);
+            if (2 * p + 1 >= nblk) break;
+            b3_cut<1>(a, c, uq, sh, m);
+            b3_line_load(p + 2 < nlines ? lp + 8 * (p + 2) : g_b3_zero_line, a);
+            b3_line_block(m, 2 * p + 1, glen, nblk, n, first, cv, s_leaf, me);
+            if (2 * p + 2 >= nblk) break;
+            b3_cut<0>(c, a, uq, sh, m);
+            b3_line_block(m, 2 * p + 2, glen, nblk, n, first, cv, s_leaf, me);
+            if (2 * p + 3 >= nblk) break;
+            b3_cut<1>(c, a, uq, sh, m);
+            b3_line_load(p + 3 < nlines ? lp + 8 * (p + 3) : g_b3_zero_line, c);
+            b3_line_block(m, 2 * p + 3, glen, nblk, n, first, cv, s_leaf, me);
+            if (2 * p + 4 >= nblk) break;
+        }
+    } else {
+        // a wave across blobs: each lane streams its own leaves with the 132-byte pair loads
+        for (uint32_t t = 0; t < k; t++) {
+            const uint64_t li = first + t, ls = start + li * B3_LEAF_BYTES;
+            const uint64_t lrest = len - li * B3_LEAF_BYTES;
+            const uint32_t ll = len == 0 ? 0 : (uint32_t)(lrest < B3_LEAF_BYTES ? lrest : B3_LEAF_BYTES);
+            b3_leaf_pairs(data, ls, ll, start + len, li, n == 1 ? B3_ROOT : 0, cv);
+#pragma unroll
+            for (int i = 0; i < 8; i++) s_leaf[t][i][me] = cv[i];
+        }
+    }
+    // the group's subtree: P(P(l0, l1), P(l2, l3)), or the ragged tail's merge of 2 or 3 leaves
+    uint32_t acc[8], r[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc[i] = s_leaf[0][i][me];
+    if (k >= 2) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) r[i] = s_leaf[1][i][me];
+        b3_parent(acc, r, (n == 2 || (n == 4 && false)) ? B3_ROOT : 0, acc);
+    }
+    if (k == 4) {
+        uint32_t l2[8], l3[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) { l2[i] = s_leaf[2][i][me]; l3[i] = s_leaf[3][i][me]; }
+        b3_parent(l2, l3, 0, r);
+        b3_parent(acc, r, n == 4 ? B3_ROOT : 0, acc);
+    } else if (k == 3) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) r[i] = s_leaf[2][i][me];
+        b3_parent(acc, r, n == 3 ? B3_ROOT : 0, acc);
+    }
+    if (n <= 4) store_digest(digests + blob * 32, acc);
+    else {
+        uint32_t* o8 = cv_buf + g * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i++) o8[i] = acc[i];
+    }
+}
+
 // Upper levels of a small blob (4 < n <= B3_SMALL_LEAVES leaves), one lane per blob: a batch of
 // many small files (C4) keeps every lane busy instead of one wave per blob with <= 8 lanes
 // active.  The level-2 nodes are merged left to right on a stack of complete subtrees that lives
@@ -419,7 +596,13 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
 #ifndef BW_B3_DYN_LDS
 #define BW_B3_DYN_LDS 0  // A/B: extra LDS per block caps the blocks per CU (occupancy experiments)
 #endif
-    if (loads == B3_LOADS_PAIRS)
+#ifndef BW_B3_LINES_MINW
+#define BW_B3_LINES_MINW 3  // blocks of 256 per CU: 3 = 3 waves per SIMD (168 VGPRs; at 4 the ring spills)
+#endif
+    if (loads == B3_LOADS_LINES)
+        hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data, ctr, b,
+                           cv_buf, digests);
+    else if (loads == B3_LOADS_PAIRS)
         hipLaunchKernelGGL((k_b3_groups<false, 1, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), BW_B3_DYN_LDS, st,
                            data, ctr, b, cv_buf, digests);
     else

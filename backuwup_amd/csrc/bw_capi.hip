@@ -58,6 +58,13 @@ struct Slot {
     uint64_t ticket = 0;  // 0: empty
     uint64_t max_blobs = 0;
     bool dedup = false;
+    // Results staged for the host as the batch's last stream operations: the counters (with the
+    // index's state after the batch's gate) and the first res_n packed records, in pinned memory,
+    // so a wait is one event synchronization and a memcpy instead of three device round trips.
+    PinBuf res;
+    uint64_t res_n = 0;
+    hipEvent_t done = nullptr;   // the staged copies landed
+    uint64_t mark = 0;           // the index's enq_total right after this batch's gate
 };
 
 }  // namespace
@@ -91,9 +98,9 @@ struct bw_ctx {
 
     // per-batch device workspace (shared by the slots: batches run one after another on `stream`)
     DevBuf tile_count, tile_slots, tile_off, tile_btot, cand, ovf;
-    DevBuf segs, cfiles, units, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
+    DevBuf meta, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
-    DevBuf cv, cv2, fstart, data, scratch, ucnt, ubtot;
+    DevBuf cv, cv2, data, scratch, ucnt, ubtot;
     DevBuf bk_blk, bk_pack, bk_v;  // multi-GPU exchange buckets (bw_partition_buckets, ...)
     // bw_exchange_dedup: my buckets and the ones received, their source positions, the counts
     // (mine, received, and scratch for the capacity agreement), verdicts out and back
@@ -103,6 +110,7 @@ struct bw_ctx {
     Slot slots[MAX_DEPTH];
     int depth = 2;
     uint64_t next_ticket = 1, last_ticket = 0;
+    uint64_t last_n = 0;  // blobs of the last batch read back (sizes the next batches' staged results)
     // the synchronous helpers (bw_process_files, bw_fastcdc_chunks, bw_blake3_hash(_many), tree
     // blobs) run in a slot of their own outside the ring: they never drop a batch the caller still
     // holds a ticket for, and leave last_ticket (bw_results, bw_batch_views) unchanged
@@ -487,7 +495,8 @@ extern "C" int bw_create(int device, bw_ctx** out) {
         Slot& sl = s < MAX_DEPTH ? c->slots[s] : c->sync_slot;
         if (hipEventCreateWithFlags(&sl.meta_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&sl.input_free, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
             bw_destroy(c);
             return BW_EHIP;
         }
@@ -506,10 +515,10 @@ extern "C" void bw_destroy(bw_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->copy) hipStreamSynchronize(c->copy);
-    DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->segs,
-                     &c->cfiles, &c->units, &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
+    DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->meta,
+                     &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
-                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2, &c->fstart,
+                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
                      &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage,
@@ -525,6 +534,8 @@ extern "C" void bw_destroy(bw_ctx* c) {
         free_dev(s.packed);
         free_dev(s.input);
         free_host(s.meta);
+        free_host(s.res);
+        if (s.done) hipEventDestroy(s.done);
         if (s.meta_done) hipEventDestroy(s.meta_done);
         if (s.input_free) hipEventDestroy(s.input_free);
         if (s.copied) hipEventDestroy(s.copied);
@@ -609,7 +620,7 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             zstd_work_limits(c->zw, 0, v);
             return BW_OK;
         case BW_OPT_B3_LOADS:
-            if (v > B3_LOADS_PAIRS) return BW_EINVAL;
+            if (v > B3_LOADS_LINES) return BW_EINVAL;
             c->b3_loads = (int)v;
             return BW_OK;
         case BW_OPT_STAGE_CHUNK:
@@ -731,9 +742,26 @@ static int validate_batch(bw_ctx* c, uint64_t data_len, const uint64_t* foff, co
     return BW_OK;
 }
 
+// Queue the host copies of a batch's results behind its kernels on the context stream: the
+// counters and the first res_n packed records (about twice the previous batch's blob count: a
+// guess, the rest is copied at the wait if the batch has more) into the slot's pinned buffer.
+static int stage_results(bw_ctx* c, Slot& s) {
+    const uint64_t want = std::min<uint64_t>(s.max_blobs, std::max<uint64_t>(1024, 2 * c->last_n + 1024));
+    if (s.res.cap < C_COUNT * 8 + want * sizeof(bw_blob)) {
+        HIPCHK(c, hipEventSynchronize(s.done));  // the buffer may still be the target of the slot's last copy
+        if (int rc = ensure_host(c, s.res, C_COUNT * 8 + want * sizeof(bw_blob))) return rc;
+    }
+    uint8_t* h = (uint8_t*)s.res.p;
+    HIPCHK(c, hipMemcpyAsync(h, s.ctr.p, C_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
+    if (want) HIPCHK(c, hipMemcpyAsync(h + C_COUNT * 8, s.packed.p, want * sizeof(bw_blob), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(s.done, c->stream));
+    s.res_n = want;
+    return BW_OK;
+}
+
 // Enqueue one batch (bytes at d_data, in HBM) into slot `s` on the context stream.
 static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
-                  const uint64_t* flen, uint64_t nf, const bw_params* prm) {
+                  const uint64_t* flen, uint64_t nf, const bw_params* prm, bool stage = true) {
     Masks mk;
     if (int rc = validate_batch(c, data_len, foff, flen, nf, prm, &mk)) return rc;
     if (data_len && !d_data) return BW_EINVAL;
@@ -887,9 +915,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     int rc = 0;
     rc |= ensure(c, c->tile_off, (n_tiles + 1) * 8);
     rc |= ensure(c, c->tile_btot, (n_tiles / 1024 + 2) * 8);
-    rc |= ensure(c, c->segs, nseg * sizeof(SegDesc));
-    rc |= ensure(c, c->cfiles, ncf * sizeof(CFileDesc));
-    rc |= ensure(c, c->units, nunits * sizeof(UnitDesc));
+    rc |= ensure(c, c->meta, meta_bytes);  // segs | cfiles | units | fstart, as staged
     rc |= ensure(c, c->chains, nseg * CHAIN_CAP * 8);
     rc |= ensure(c, c->chain_n, nseg * 4);
     rc |= ensure(c, c->chain_cptr, nseg * 8);
@@ -911,7 +937,6 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     rc |= ensure(c, s.digests, max_blobs * 32);
     rc |= ensure(c, s.is_dup, max_blobs);
     rc |= ensure(c, s.packed, max_blobs * sizeof(bw_blob));
-    rc |= ensure(c, c->fstart, nf * 8);
     rc |= ensure(c, c->ucnt, 2 * nunits * 8);
     rc |= ensure(c, c->ubtot, 2 * (nunits / 1024 + 2) * 8);
     if (rc) return BW_ENOMEM;
@@ -932,10 +957,12 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     auto up = [&](DevBuf& dst, const void* src, size_t bytes) -> hipError_t {
         return bytes ? hipMemcpyAsync(dst.p, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
     };
-    HIPCHK(c, up(c->segs, segs, nseg * sizeof(SegDesc)));
-    HIPCHK(c, up(c->cfiles, cfs, ncf * sizeof(CFileDesc)));
-    HIPCHK(c, up(c->units, units, nunits * sizeof(UnitDesc)));
-    HIPCHK(c, up(c->fstart, fstart_h, nf * 8));
+    // one copy: the tables lie back to back in the staging and keep that layout on the device
+    HIPCHK(c, up(c->meta, segs, meta_bytes));
+    SegDesc* d_segs = P<SegDesc>(c->meta);
+    CFileDesc* d_cfs = (CFileDesc*)(d_segs + nseg);
+    UnitDesc* d_units = (UnitDesc*)(d_cfs + ncf);
+    uint64_t* d_fstart = (uint64_t*)(d_units + nunits);
     HIPCHK(c, hipEventRecord(s.meta_done, c->stream));
     s.meta_pending = true;
     phase(2);
@@ -986,16 +1013,16 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
                        P<uint64_t>(c->tile_btot));
     prof_mark(c, BW_STAGE_RESOLVE, lat);
     if (ncf) {
-        launch_chains(lat, d_data, data_len, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, P<SegDesc>(c->segs),
+        launch_chains(lat, d_data, data_len, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr, d_segs,
                       nseg, P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->chain_cptr),
                       P<uint64_t>(c->merge), force_serial);
         launch_resolve(lat, d_data, data_len, mk, P<uint64_t>(c->cand), P<uint64_t>(c->tile_off), ctr,
-                       P<SegDesc>(c->segs), nseg, P<CFileDesc>(c->cfiles), ncf, P<uint64_t>(c->chains),
+                       d_segs, nseg, d_cfs, ncf, P<uint64_t>(c->chains),
                        P<uint32_t>(c->chain_n), P<uint64_t>(c->merge), P<uint64_t>(c->seg_M), P<uint32_t>(c->seg_cnt),
                        P<uint32_t>(c->cf_invalid), P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), force_serial);
     }
     prof_mark(c, BW_STAGE_ASSEMBLE, lat);
-    launch_assemble(lat, ctr, P<UnitDesc>(c->units), nunits, P<SegDesc>(c->segs), P<CFileDesc>(c->cfiles),
+    launch_assemble(lat, ctr, d_units, nunits, d_segs, d_cfs,
                     P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->seg_M), P<uint32_t>(c->cf_invalid),
                     P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), b, P<uint64_t>(c->ucnt),
                     P<uint64_t>(c->ubtot));
@@ -1034,11 +1061,12 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     if (do_dedup) {
         if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup), lat))
             return r4;
+        s.mark = c->idx_mark;
     }
     phase(4);
     prof_mark(c, BW_STAGE_PACK, lat);
-    launch_pack(lat, ctr, b, P<uint64_t>(c->fstart), P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
-                P<uint8_t>(s.packed), max_blobs);
+    launch_pack(lat, ctr, b, d_fstart, P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
+                P<uint8_t>(s.packed), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr);
     if (split) {  // the batch ends on the context stream (the caller's order)
         prof_mark(c, BW_N_STAGES, lat);
         HIPCHK(c, hipEventRecord(c->e_end, lat));
@@ -1049,6 +1077,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     HIPCHK(c, hipGetLastError());
     s.max_blobs = max_blobs;
     s.dedup = do_dedup;
+    if (stage)
+        if (int r5 = stage_results(c, s)) return r5;
     phase(5);
     c->host_batches += c->host_timing;
     return BW_OK;
@@ -1163,17 +1193,40 @@ extern "C" int bw_host_unregister(void* p) {
 // Results of the batch in slot s (waits for it).  Repeatable until the ring reuses the slot.
 static int slot_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t* n_out) {
     hipSetDevice(c->device);
-    uint64_t ctr[C_COUNT];
-    HIPCHK(c, hipMemcpyAsync(ctr, s.ctr.p, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventSynchronize(s.done));  // the staged counters and records have landed
+    const uint64_t* ctr = (const uint64_t*)s.res.p;
     if (ctr[C_CANDTOTAL] > ctr[C_NCAND])  // exact anyway; give later batches the room they need
         c->cand_override = std::max(c->cand_override, ctr[C_CANDTOTAL] + 1024);
-    *n_out = ctr[C_NBLOBS];
-    if (s.dedup)
-        if (int rc = check_collision(c)) return rc;
-    if (ctr[C_NBLOBS] > cap) return BW_ENOSPC;
-    if (ctr[C_NBLOBS] && out)
-        HIPCHK(c, hipMemcpy(out, s.packed.p, ctr[C_NBLOBS] * sizeof(bw_blob), hipMemcpyDeviceToHost));
+    const uint64_t n = ctr[C_NBLOBS];
+    *n_out = n;
+    c->last_n = n;
+    if (s.dedup) {
+        if (ctr[C_IX_VALID]) {  // the index state right after this batch's gate
+            bw_index* x = c->idx;
+            {
+                std::lock_guard<std::mutex> lk(x->mu);
+                x->log_hi = std::min(x->log_hi, ctr[C_IX_LOGLEN] + (x->enq_total - std::min(x->enq_total, s.mark)));
+            }
+            if (ctr[C_COLLIDE]) {
+                c->err = "64-bit key collision between distinct digests";
+                return BW_ECOLLISION;
+            }
+            if (ctr[C_IX_OVF]) {
+                c->err = "a batch had more blobs than its exchange bucket capacity (verdicts incomplete)";
+                return BW_ENOSPC;
+            }
+        } else if (int rc = check_collision(c)) {
+            return rc;
+        }
+    }
+    if (n > cap) return BW_ENOSPC;
+    if (n && out) {
+        const uint64_t k = std::min(n, s.res_n);
+        memcpy(out, (const uint8_t*)s.res.p + C_COUNT * 8, k * sizeof(bw_blob));
+        if (n > k)  // more blobs than staged: the rest straight from the device
+            HIPCHK(c, hipMemcpy(out + k, P<uint8_t>(s.packed) + k * sizeof(bw_blob), (n - k) * sizeof(bw_blob),
+                                hipMemcpyDeviceToHost));
+    }
     return BW_OK;
 }
 
@@ -1217,10 +1270,10 @@ static int upload_data(bw_ctx* c, const uint8_t* data, uint64_t len) {
 // A synchronous helper's batch: bytes already in c->data, enqueued into the context's own slot
 // (outside the ticket ring).
 static int submit_sync(bw_ctx* c, uint64_t data_len, const uint64_t* foff, const uint64_t* flen, uint64_t nf,
-                       const bw_params* prm) {
+                       const bw_params* prm, bool stage = true) {
     Slot& s = c->sync_slot;
     s.ticket = 0;
-    return submit(c, s, P<uint8_t>(c->data), data_len, foff, flen, nf, prm);
+    return submit(c, s, P<uint8_t>(c->data), data_len, foff, flen, nf, prm, stage);
 }
 
 extern "C" int bw_process_files(bw_ctx* c, const uint8_t* data, uint64_t data_len, const uint64_t* foff,
@@ -1296,7 +1349,7 @@ int bw::hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const ui
     bw_params_default(&p);
     p.flags = dedup ? 0 : BW_F_NO_DEDUP;
     p.small_file_threshold = ~0ull;  // every message is one whole blob, in the order given
-    if (int rc = submit_sync(c, total, offs, lens, n, &p)) return rc;
+    if (int rc = submit_sync(c, total, offs, lens, n, &p, false)) return rc;
     Slot& s = c->sync_slot;
     HIPCHK(c, hipMemcpyAsync(hashes, s.digests.p, n * 32, hipMemcpyDeviceToHost, c->stream));
     if (dedup) HIPCHK(c, hipMemcpyAsync(dup, s.is_dup.p, n, hipMemcpyDeviceToHost, c->stream));
@@ -1431,9 +1484,11 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     if (int r = comm_all_to_all(comm, c->ex_v.p, c->ex_rv.p, cap, st, c->err)) return r;
     launch_bucket_scatter(st, P<uint8_t>(c->ex_rv), P<uint64_t>(c->ex_perm), cnt, W, cap, P<uint8_t>(s->is_dup),
                           P<uint8_t>(s->packed));
+    launch_index_snapshot(st, P<uint64_t>(c->idx->dstate), P<uint64_t>(s->ctr));
     HIPCHK(c, hipGetLastError());
     s->dedup = true;  // bw_wait now reports the index's sticky errors for this batch
-    return BW_OK;
+    s->mark = c->idx_mark;
+    return stage_results(c, *s);  // the records staged at submit predate the verdicts
 }
 
 // ------------------------------------------------------------------ stage timing API

@@ -360,9 +360,25 @@ void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_
 
 // ------------------------------------------------------------------ result records
 
-__global__ void k_pack(const uint64_t* ctr, BlobArrays b, const uint64_t* __restrict__ file_start,
-                       const uint8_t* __restrict__ digests, const uint8_t* __restrict__ is_dup, uint8_t* __restrict__ out) {
+__device__ __forceinline__ void index_snapshot(const uint64_t* dstate, uint64_t* ctr) {
+    ctr[C_COLLIDE] = dstate[D_COLLIDE];
+    ctr[C_NUNIQUE] = dstate[D_NUNIQUE];
+    ctr[C_IX_OVF] = dstate[D_BUCKET_OVF];
+    ctr[C_IX_LOGLEN] = dstate[D_LOGLEN];
+    ctr[C_IX_VALID] = 1;
+}
+
+__global__ void k_index_snapshot(const uint64_t* dstate, uint64_t* ctr) { index_snapshot(dstate, ctr); }
+
+void launch_index_snapshot(hipStream_t st, const uint64_t* dstate, uint64_t* ctr) {
+    hipLaunchKernelGGL(k_index_snapshot, dim3(1), dim3(1), 0, st, dstate, ctr);
+}
+
+__global__ void k_pack(uint64_t* ctr, BlobArrays b, const uint64_t* __restrict__ file_start,
+                       const uint8_t* __restrict__ digests, const uint8_t* __restrict__ is_dup, uint8_t* __restrict__ out,
+                       const uint64_t* dstate) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0 && dstate) index_snapshot(dstate, ctr);  // the gate ran before this kernel on the stream
     if (k >= ctr[C_NBLOBS]) return;
     uint64_t* o = (uint64_t*)(out + k * 72);
     const uint32_t f = b.file[k];
@@ -378,11 +394,10 @@ __global__ void k_pack(const uint64_t* ctr, BlobArrays b, const uint64_t* __rest
     o[8] = is_dup ? (uint64_t)is_dup[k] : 0;
 }
 
-void launch_pack(hipStream_t st, const uint64_t* ctr, BlobArrays b, const uint64_t* file_start, const uint8_t* digests,
-                 const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs) {
-    if (!max_blobs) return;
-    hipLaunchKernelGGL(k_pack, dim3((unsigned)((max_blobs + 255) / 256)), dim3(256), 0, st, ctr, b, file_start,
-                       digests, is_dup, out);
+void launch_pack(hipStream_t st, uint64_t* ctr, BlobArrays b, const uint64_t* file_start, const uint8_t* digests,
+                 const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs, const uint64_t* dstate) {
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)((max_blobs + 255) / 256 + (max_blobs == 0))), dim3(256), 0, st, ctr, b,
+                       file_start, digests, is_dup, out, dstate);
 }
 
 }  // namespace bw

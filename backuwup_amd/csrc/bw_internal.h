@@ -44,6 +44,11 @@ enum Ctr : int {
     C_DEDUPN = 9,    // blobs handed to the index
     C_TRUNC = 10,    // first byte position whose candidates did not fit the array (BW_NONE: all fit);
                      // the walkers scan the bytes themselves from there on
+    // the index's state right after the batch's gate (snapshot by k_pack / k_index_snapshot), read
+    // back with the staged results: C_COLLIDE, C_NUNIQUE and these
+    C_IX_OVF = 11,    // an exchange bucket overflowed (D_BUCKET_OVF)
+    C_IX_LOGLEN = 12, // log length (D_LOGLEN)
+    C_IX_VALID = 13,  // 1 = the snapshot was taken
     C_COUNT = 16
 };
 static_assert(SCAN_STRIP_SMALL % (4 * SCAN_STEP) == 0, "k_scan consumes four 64-byte steps per iteration");
@@ -120,8 +125,9 @@ void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const
                      BlobArrays b, uint64_t max_blobs);
 
 // ------------------------------------------------------------------ launchers (bw_blake3.hip)
-// how k_b3_groups feeds its compressions: one 64-byte block ahead (prefetch) or block pairs
-enum { B3_LOADS_PREFETCH = 0, B3_LOADS_PAIRS = 1 };
+// how the leaf pass feeds its compressions: one 64-byte block ahead (prefetch), block pairs, or
+// whole aligned 128-byte lines through a register ring (k_b3_lines)
+enum { B3_LOADS_PREFETCH = 0, B3_LOADS_PAIRS = 1, B3_LOADS_LINES = 2 };
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b,
                    uint64_t max_blobs, uint64_t max_groups, uint32_t* cv_buf,
                    uint32_t* cv_tmp /* like cv_buf */, uint8_t* digests, int max_leaves,
@@ -159,8 +165,11 @@ void launch_bucket_expand(hipStream_t st, const uint64_t* counts, uint32_t n_src
 // packed (may be null): the batch's bw_blob records, whose is_dup byte is written as well
 void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, const uint64_t* counts,
                            uint32_t n_owners, uint64_t cap, uint8_t* is_dup, uint8_t* packed = nullptr);
-void launch_pack(hipStream_t st, const uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
-                 const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs);
+// dstate (may be null): the index state snapshot into ctr[C_COLLIDE, C_NUNIQUE, C_IX_*]
+void launch_pack(hipStream_t st, uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
+                 const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs,
+                 const uint64_t* dstate);
+void launch_index_snapshot(hipStream_t st, const uint64_t* dstate, uint64_t* ctr);
 
 // ------------------------------------------------------------------ sealing (bw_seal.hip)
 // BW_SEAL_MAX_INFO (include/backuwup_gpu.h): HKDF info bytes that fit one HMAC block with 0x01 + padding

@@ -146,8 +146,9 @@ def main():
     ap.add_argument("--pack-l3", action="store_true",
                     help="also time the full chain on the last batch's unique blobs: level-3 zstd on the GPU, "
                          "the packfile grouping over the frame sizes, sealing + layout (§8f rows 2-4)")
-    ap.add_argument("--b3-loads", type=int, default=None, choices=[0, 1],
-                    help="k_b3_groups loads (BW_OPT_B3_LOADS): 0 = one block ahead, 1 = block pairs")
+    ap.add_argument("--b3-loads", type=int, default=None, choices=[0, 1, 2],
+                    help="BLAKE3 leaf loads (BW_OPT_B3_LOADS): 0 = one block ahead, 1 = block pairs, "
+                         "2 = aligned lines (k_b3_lines)")
     ap.add_argument("--scan-waves", type=int, default=None, choices=[8, 16], help="BW_OPT_SCAN_WAVES")
     ap.add_argument("--latency-stream", type=int, default=None, choices=[0, 1], help="BW_OPT_LATENCY_STREAM")
     ap.add_argument("--order-hash", type=int, default=None, choices=[0, 1], help="BW_OPT_ORDER_HASH")
@@ -178,7 +179,7 @@ def main():
     import torch.distributed as dist
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
-    from backuwup_amd._lib import (BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
+    from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
                                    BW_OPT_SCAN_WAVES, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
@@ -348,14 +349,16 @@ def main():
     dom = max(["scan", "b3_leaf"], key=lambda s: per[s])
     algo = processed if dom == "b3_leaf" else n
     achieved = algo / (per[dom] * 1e-3) / 1e9
-    kernel = {"scan": "k_scan", "b3_leaf": "k_b3_groups"}[dom]
+    loads = args.b3_loads if args.b3_loads is not None else BW_B3_LOADS_DEFAULT
+    leaf_kernel = "k_b3_lines" if loads == 2 else "k_b3_groups"
+    kernel = {"scan": "k_scan", "b3_leaf": leaf_kernel}[dom]
     traffic, traffic_src = pmc_traffic(args, kernel)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": kernel,
                 "algorithmic_bytes_per_launch": algo,
                 "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
-    if kernel == "k_b3_groups":
+    if kernel == leaf_kernel:
         # the limit this kernel actually meets: integer VALU issue (B3_VALU_CEILING_GBS)
         roofline["valu_issue"] = {"ceiling": B3_VALU_CEILING_GBS, "unit": "GB/s",
                                   "frac": round(achieved / B3_VALU_CEILING_GBS, 4)}
@@ -371,11 +374,11 @@ def main():
         roofline["power_missing"] = power_missing
     if iso is not None:
         # live durations above include the overlap with the other batch in flight
-        a_iso = algo / (iso["b3_leaf" if kernel == "k_b3_groups" else "scan"] * 1e-3) / 1e9
+        a_iso = algo / (iso["b3_leaf" if kernel == leaf_kernel else "scan"] * 1e-3) / 1e9
         roofline["live_shares_gpu_with"] = "the other batches in flight (%d contexts)" % len(ctxs)
         roofline["isolated"] = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
                                 "valu_issue_frac": (round(a_iso / B3_VALU_CEILING_GBS, 4)
-                                                    if kernel == "k_b3_groups" else None),
+                                                    if kernel == leaf_kernel else None),
                                 "stage_ms_per_step": {k: round(v, 3) for k, v in iso.items()}}
 
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None

@@ -157,7 +157,8 @@ enum {
     BW_OPT_SCAN_SMALL_BYTES = 2, /* batches below this many bytes scan half-size tiles (default 4 GiB) */
     BW_OPT_CAND_CAP = 3,         /* test hook: fixed candidate array capacity (0 = sized per batch)  */
     BW_OPT_STAGE_CHUNK = 4,      /* pinned staging chunk for pageable bw_submit_host input (64 MiB)  */
-    BW_OPT_B3_LOADS = 5,         /* k_b3_groups loads: 0 = one block ahead, 1 = block pairs (default) */
+    BW_OPT_B3_LOADS = 5,         /* BLAKE3 leaf pass loads: 0 = one block ahead, 1 = 132-byte block pairs,
+                                    2 = aligned 128-byte lines through a register ring (k_b3_lines) */
     BW_OPT_SCAN_WAVES = 6,       /* gear-scan workgroup: 16 waves (default) or 8 (leaves LDS for BLAKE3) */
     BW_OPT_LATENCY_STREAM = 7,   /* 1: the small kernels between the passes on a high-priority stream */
     BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (768 KiB of hash tables each; 16384) */

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from backuwup_amd import make_params
-from backuwup_amd._lib import BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE, BwError
+from backuwup_amd._lib import BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE, BW_OPT_B3_LOADS, BwError
 from backuwup_amd.synth import splitmix_bytes
 
 pytestmark = pytest.mark.gpu
@@ -31,9 +31,18 @@ KAT = {
 }
 
 
-def test_blake3_kat(ctx):
+# every BLAKE3 test runs with each leaf-pass loader: 0 = one block ahead, 1 = 132-byte block pairs
+# (k_b3_groups), 2 = aligned 128-byte lines through a register ring (k_b3_lines), default
+@pytest.fixture(params=[0, 1, 2], ids=["prefetch", "pairs", "lines"])
+def b3ctx(ctx, request):
+    ctx.set_option(BW_OPT_B3_LOADS, request.param)
+    yield ctx
+    ctx.set_option(BW_OPT_B3_LOADS, 1)  # the context default
+
+
+def test_blake3_kat(b3ctx):
     for msg, hexd in KAT.items():
-        assert ctx.blake3(msg).hex() == hexd
+        assert b3ctx.blake3(msg).hex() == hexd
 
 
 # the official test-vector lengths (input byte i = i % 251) plus the tree-shape edges
@@ -42,13 +51,15 @@ TV_LENS = [0, 1, 63, 64, 65, 127, 128, 1023, 1024, 1025, 2048, 2049, 3072, 3073,
            1048576, 1048577, 3145728]
 
 
-def test_blake3_lengths(ctx, oracle):
+def test_blake3_lengths(b3ctx, oracle):
+    ctx = b3ctx
     for n in TV_LENS:
         msg = (np.arange(n) % 251).astype(np.uint8)
         assert ctx.blake3(msg) == oracle.blake3(msg), n
 
 
-def test_blake3_tree_shapes_batched(ctx, oracle):
+def test_blake3_tree_shapes_batched(b3ctx, oracle):
+    ctx = b3ctx
     # every leaf count around the group (4 leaves), lane-per-blob (<= 64 leaves) and wave-per-blob
     # tree paths, ragged and exact, hashed in one batch
     lens = [k * 1024 + d for k in range(1, 140) for d in (-1, 0, 1)]
@@ -60,7 +71,8 @@ def test_blake3_tree_shapes_batched(ctx, oracle):
         assert bytes(got[i]) == oracle.blake3(data[o:o + l]), l
 
 
-def test_blake3_upper_tree_levels(ctx, oracle):
+def test_blake3_upper_tree_levels(b3ctx, oracle):
+    ctx = b3ctx
     # wave-per-blob upper tree: leaf counts around its global passes (more than 64 level-2 nodes,
     # i.e. > 259 leaves) and the register levels below them, every spine-bit pattern near powers
     # of two, next to lane-per-blob blobs in the same launch
@@ -75,7 +87,8 @@ def test_blake3_upper_tree_levels(ctx, oracle):
         assert bytes(got[i]) == oracle.blake3(data[o:o + l]), l
 
 
-def test_blake3_many_unaligned(ctx, oracle):
+def test_blake3_many_unaligned(b3ctx, oracle):
+    ctx = b3ctx
     rng = np.random.default_rng(7)
     data = splitmix_bytes(11, 6 << 20)
     n = 400
@@ -88,12 +101,37 @@ def test_blake3_many_unaligned(ctx, oracle):
         assert bytes(got[i]) == oracle.blake3(data[o:o + l]), (o, l)
 
 
-def test_blake3_message_at_buffer_end(ctx, oracle):
+def test_blake3_message_at_buffer_end(b3ctx, oracle):
+    ctx = b3ctx
     # last message ends exactly at the caller's buffer end (bounds-safe tail loads)
     for n in [1, 3, 67, 1021, 4099, 70001]:
         data = splitmix_bytes(n, n + 5)
         got = ctx.blake3_many(data, [5], [n])
         assert bytes(got[0]) == oracle.blake3(data[5:]), n
+
+
+def test_blake3_line_ring_offsets(b3ctx, oracle):
+    """k_b3_lines' two paths: whole waves inside one blob at each of the 128 start offsets of a
+    128-byte line (the ring, one switch case per offset and block half), and waves across blobs
+    (the per-lane fallback).  Blob lengths end at every position of the last block and leaf."""
+    ctx = b3ctx
+    rng = np.random.default_rng(128)
+    lens, offs, pos = [], [], 7
+    for o in range(128):
+        n = 64 * 4096 + int(rng.integers(0, 70000))  # >= 64 groups: whole waves in the blob
+        pos += (o - pos) % 128
+        offs.append(pos)
+        lens.append(n)
+        pos += n + int(rng.integers(1, 300))
+    for k in range(200):  # small blobs packed tightly: waves straddle blobs with mixed offsets
+        n = int(rng.integers(0, 20000))
+        offs.append(pos)
+        lens.append(n)
+        pos += n + int(rng.integers(0, 5))
+    data = splitmix_bytes(129, pos + 16)
+    got = ctx.blake3_many(data, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint64))
+    for i, (o, l) in enumerate(zip(offs, lens)):
+        assert bytes(got[i]) == oracle.blake3(data[o:o + l]), (i, o % 128, l)
 
 
 # ------------------------------------------------------------------ FastCDC

@@ -484,7 +484,8 @@ def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
     assert got[0][2][3].all()  # batch 2 repeats batch 0 on rank 0
 
 
-@pytest.mark.parametrize("scan_waves,latency,loads", [(8, 0, 1), (16, 1, 1), (8, 1, 0), (16, 0, 0)])
+@pytest.mark.parametrize("scan_waves,latency,loads", [(8, 0, 1), (16, 1, 1), (8, 1, 0), (16, 0, 0), (16, 0, 2),
+                                                     (8, 1, 2)])
 def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads):
     """The scheduling variants (8-wave scan blocks, the high-priority latency stream, both BLAKE3
     load modes) change only where and when kernels run: results equal the oracle, including two
