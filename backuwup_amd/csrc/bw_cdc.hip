@@ -14,14 +14,15 @@
 // Pipeline (all on the stream, no host round trip):
 //   k_scan      gear hash at every byte, LDS lane-replicated table, one-v_and prefilter per
 //               byte; flagged 64-byte blocks made exact by the wave at the end of each tile
-//   k_tile_partial/k_tile_top  exclusive scan of per-tile counts -> candidate array offsets
+//   k_tile_partial  exclusive scan of per-tile counts -> candidate array offsets (block scans; the
+//               grid's last block scans the block totals)
 //   k_rescan<false> exact counts of overflowed tiles (candidate-dense data, small parameters)
 //   k_compact   copy slots; k_rescan<true> writes the overflowed tiles' candidates
 //   k_chains    one wave per segment: speculative boundary chain from the segment start
 //   k_extend    continue each chain until it merges with the next segment's chain (CDC resync)
 //   k_resolve   prefix-max of merge points -> true chain entry of every segment, validity
 //   k_fallback  serial wave walker for files whose chains did not merge (exact, slower)
-//   k_unit_*    canonical-order blob table + BLAKE3 group offsets (count, scan, emit)
+//   k_unit_*    canonical-order blob table + BLAKE3 group offsets (count + scan, emit)
 //   k_cut_hash  Chunk.hash (the crate's returned gear state) for every CDC chunk
 #include "bw_device.h"
 #include "bw_internal.h"
@@ -340,6 +341,41 @@ __device__ __forceinline__ uint64_t block_excl_segmax(uint32_t f, uint64_t v, ui
     return r;
 }
 
+// The "last block done" pattern: every block of a grid counts itself in *done once its results
+// are written; the block that completes the count returns true, with every other block's writes
+// visible, and resets the counter.  Folds a one-block follow-up kernel into the grid before it.
+__device__ __forceinline__ bool last_block_done(uint64_t* done) {
+    __shared__ bool last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd((unsigned long long*)done, 1ull) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) {
+        __threadfence();  // acquire: the other blocks' results
+        if (threadIdx.x == 0) *done = 0;
+    }
+    return last;
+}
+
+// Exclusive scan, in place, of n block totals by one block of T threads; returns the grand total.
+template <int T>
+__device__ __forceinline__ uint64_t scan_totals(uint64_t* tot, uint64_t n, uint64_t* s) {
+    const uint64_t per = (n + T - 1) / T, lo = threadIdx.x * per;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    uint64_t sum = 0;
+    for (uint64_t i = lo; i < hi; i++) sum += tot[i];
+    uint64_t total;
+    uint64_t run = block_excl_sum<T>(sum, s, &total);
+    for (uint64_t i = lo; i < hi; i++) {
+        const uint64_t t = tot[i];
+        tot[i] = run;
+        run += t;
+    }
+    return total;
+}
+
 // ======================================================================== candidate compaction
 
 constexpr int BLK = 1024;
@@ -350,7 +386,8 @@ constexpr int BLK = 1024;
 constexpr int TS_BLOCK = 256;  // threads per block, 4 counts each
 
 __global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint32_t* __restrict__ cnt, uint64_t n,
-                                                           uint64_t* __restrict__ off, uint64_t* __restrict__ btot) {
+                                                           uint64_t* __restrict__ off, uint64_t* __restrict__ btot,
+                                                           uint64_t cap, uint64_t* ctr) {
     __shared__ uint64_t s[TS_BLOCK];
     const uint64_t i0 = ((uint64_t)blockIdx.x * TS_BLOCK + threadIdx.x) * 4;
     uint32_t c[4] = {0, 0, 0, 0};
@@ -367,22 +404,13 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint32_t* __res
     for (int k = 0; k < 4; k++)
         if (i0 + k < n) { off[i0 + k] = run; run += c[k]; }
     if (threadIdx.x == 0) btot[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(BLK) void k_tile_top(uint64_t* __restrict__ btot, uint64_t nb, uint64_t n_tiles,
-                                                  uint64_t* __restrict__ off, uint64_t cap, uint64_t* ctr) {
-    __shared__ uint64_t s[BLK];
-    const uint64_t per = (nb + BLK - 1) / BLK, lo = threadIdx.x * per;
-    const uint64_t hi = lo + per < nb ? lo + per : nb;
-    uint64_t sum = 0;
-    for (uint64_t i = lo; i < hi; i++) sum += btot[i];
-    uint64_t total;
-    uint64_t run = block_excl_sum<BLK>(sum, s, &total);
-    for (uint64_t i = lo; i < hi; i++) { const uint64_t t = btot[i]; btot[i] = run; run += t; }
+    // the last block scans the block totals (what a separate one-block kernel did)
+    if (!last_block_done(&ctr[C_DONE_TILES])) return;
+    const uint64_t all = scan_totals<TS_BLOCK>(btot, gridDim.x, s);
     if (threadIdx.x == 0) {
-        off[n_tiles] = total;
-        ctr[C_NCAND] = total < cap ? total : cap;
-        ctr[C_CANDTOTAL] = total;
+        off[n] = all;
+        ctr[C_NCAND] = all < cap ? all : cap;
+        ctr[C_CANDTOTAL] = all;
         ctr[C_TRUNC] = BW_NONE;  // lowered by k_compact when the array cannot hold every candidate
     }
 }
@@ -460,8 +488,8 @@ void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint6
     const uint64_t nb = (n_tiles + 4 * TS_BLOCK - 1) / (4 * TS_BLOCK);
     hipLaunchKernelGGL(k_rescan<false>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
                        cand, cand_cap, tile_count, ctr);
-    hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, tile_count, n_tiles, tile_off, btot);
-    hipLaunchKernelGGL(k_tile_top, dim3(1), dim3(BLK), 0, st, btot, nb, n_tiles, tile_off, cand_cap, ctr);
+    hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, tile_count, n_tiles, tile_off, btot,
+                       cand_cap, ctr);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count, tile_slots,
                        tile_off, btot, n_tiles, cand, cand_cap, mk.tile_shift, ctr);
     hipLaunchKernelGGL(k_rescan<true>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
@@ -645,7 +673,7 @@ void launch_chains(hipStream_t st, const uint8_t* data, uint64_t data_len, const
 // M_j (first true chunk start inside chain j) = file start for a file's first segment, else
 // max(merge[first .. j-1]).  Segment j contributes its chain entries in [M_j, M_{j+1}).
 __global__ __launch_bounds__(BLK) void k_resolve(const SegDesc* __restrict__ segs, uint64_t nseg,
-                                                 const CFileDesc* __restrict__ cfiles,
+                                                 const CFileDesc* __restrict__ cfiles, uint64_t ncf,
                                                  const uint64_t* __restrict__ chains,
                                                  const uint32_t* __restrict__ chain_n,
                                                  const uint64_t* __restrict__ merge, uint64_t* __restrict__ seg_M,
@@ -653,6 +681,8 @@ __global__ __launch_bounds__(BLK) void k_resolve(const SegDesc* __restrict__ seg
                                                  int force_serial) {
     __shared__ uint64_t s_v[BLK];
     __shared__ uint32_t s_f[BLK];
+    for (uint64_t f = threadIdx.x; f < ncf; f += BLK) cf_invalid[f] = 0;  // (was a memset before the launch)
+    __syncthreads();
     const uint64_t per = (nseg + BLK - 1) / BLK, lo = threadIdx.x * per;
     const uint64_t hi = lo + per < nseg ? lo + per : nseg;
     // local aggregate of (starts-new-file, max merge)
@@ -737,8 +767,7 @@ void launch_resolve(hipStream_t st, const uint8_t* data, uint64_t data_len, cons
                     const uint64_t* merge, uint64_t* seg_M, uint32_t* seg_cnt, uint32_t* cf_invalid,
                     uint64_t* fb_starts, uint64_t* fb_count, int force_serial) {
     if (!nseg) return;
-    hipMemsetAsync(cf_invalid, 0, ncf * sizeof(uint32_t), st);
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(BLK), 0, st, segs, nseg, cfiles, chains, chain_n, merge, seg_M,
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(BLK), 0, st, segs, nseg, cfiles, ncf, chains, chain_n, merge, seg_M,
                        seg_cnt, cf_invalid, force_serial);
     Walker W{data, cand, 0, nullptr, mk, 0, data_len};
     const unsigned grid = (unsigned)((ncf + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
@@ -813,33 +842,28 @@ __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDe
 constexpr int AS_BLOCK = 256;                      // threads per block, 4 units each
 constexpr uint64_t AS_UNITS = 4ull * AS_BLOCK;     // units per partial-scan block
 
-__global__ __launch_bounds__(256) void k_unit_count(const UnitDesc* __restrict__ units, uint64_t nunits,
-                                                    const SegDesc* __restrict__ segs,
-                                                    const CFileDesc* __restrict__ cfiles,
-                                                    const uint64_t* __restrict__ chains,
-                                                    const uint32_t* __restrict__ chain_n,
-                                                    const uint64_t* __restrict__ seg_M,
-                                                    const uint32_t* __restrict__ cf_invalid,
-                                                    const uint64_t* __restrict__ fb_starts,
-                                                    const uint64_t* __restrict__ fb_count, BlobArrays b,
-                                                    uint64_t* __restrict__ ucb, uint64_t* __restrict__ ucg) {
-    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nunits) return;
-    uint64_t nb, ng;
-    unit_blobs<false>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, 0, 0, nb, ng);
-    ucb[u] = nb;
-    ucg[u] = ng;
-}
-
-__global__ __launch_bounds__(AS_BLOCK) void k_unit_partial(uint64_t* __restrict__ ucb, uint64_t* __restrict__ ucg,
-                                                           uint64_t n, uint64_t* __restrict__ bt_b,
-                                                           uint64_t* __restrict__ bt_g) {
+// Per-unit blob/group counts (4 units per thread), their exclusive scan inside the block, and in
+// the grid's last block the scan of the block totals (the batch's blob and group counts).
+__global__ __launch_bounds__(AS_BLOCK) void k_unit_count(const UnitDesc* __restrict__ units, uint64_t nunits,
+                                                         const SegDesc* __restrict__ segs,
+                                                         const CFileDesc* __restrict__ cfiles,
+                                                         const uint64_t* __restrict__ chains,
+                                                         const uint32_t* __restrict__ chain_n,
+                                                         const uint64_t* __restrict__ seg_M,
+                                                         const uint32_t* __restrict__ cf_invalid,
+                                                         const uint64_t* __restrict__ fb_starts,
+                                                         const uint64_t* __restrict__ fb_count, BlobArrays b,
+                                                         uint64_t* __restrict__ ucb, uint64_t* __restrict__ ucg,
+                                                         uint64_t* __restrict__ bt_b, uint64_t* __restrict__ bt_g,
+                                                         uint64_t* ctr) {
     __shared__ uint64_t s[AS_BLOCK];
     const uint64_t i0 = ((uint64_t)blockIdx.x * AS_BLOCK + threadIdx.x) * 4;
     uint64_t cb[4], cg[4], sb = 0, sg = 0;
     for (int k = 0; k < 4; k++) {
-        cb[k] = i0 + k < n ? ucb[i0 + k] : 0;
-        cg[k] = i0 + k < n ? ucg[i0 + k] : 0;
+        cb[k] = cg[k] = 0;
+        if (i0 + k < nunits)
+            unit_blobs<false>(units[i0 + k], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b,
+                              0, 0, cb[k], cg[k]);
         sb += cb[k];
         sg += cg[k];
     }
@@ -847,7 +871,7 @@ __global__ __launch_bounds__(AS_BLOCK) void k_unit_partial(uint64_t* __restrict_
     uint64_t rb = block_excl_sum<AS_BLOCK>(sb, s, &tb);
     uint64_t rg = block_excl_sum<AS_BLOCK>(sg, s, &tg);
     for (int k = 0; k < 4; k++)
-        if (i0 + k < n) {
+        if (i0 + k < nunits) {
             ucb[i0 + k] = rb;
             ucg[i0 + k] = rg;
             rb += cb[k];
@@ -857,28 +881,9 @@ __global__ __launch_bounds__(AS_BLOCK) void k_unit_partial(uint64_t* __restrict_
         bt_b[blockIdx.x] = tb;
         bt_g[blockIdx.x] = tg;
     }
-}
-
-__global__ __launch_bounds__(BLK) void k_unit_top(uint64_t* __restrict__ bt_b, uint64_t* __restrict__ bt_g,
-                                                  uint64_t nb, uint64_t* ctr) {
-    __shared__ uint64_t s[BLK];
-    const uint64_t per = (nb + BLK - 1) / BLK, lo = threadIdx.x * per;
-    const uint64_t hi = lo + per < nb ? lo + per : nb;
-    uint64_t sb = 0, sg = 0;
-    for (uint64_t i = lo; i < hi; i++) {
-        sb += bt_b[i];
-        sg += bt_g[i];
-    }
-    uint64_t totb, totg;
-    uint64_t rb = block_excl_sum<BLK>(sb, s, &totb);
-    uint64_t rg = block_excl_sum<BLK>(sg, s, &totg);
-    for (uint64_t i = lo; i < hi; i++) {
-        const uint64_t tb = bt_b[i], tg = bt_g[i];
-        bt_b[i] = rb;
-        bt_g[i] = rg;
-        rb += tb;
-        rg += tg;
-    }
+    if (!last_block_done(&ctr[C_DONE_UNITS])) return;
+    const uint64_t totb = scan_totals<AS_BLOCK>(bt_b, gridDim.x, s);
+    const uint64_t totg = scan_totals<AS_BLOCK>(bt_g, gridDim.x, s);
     if (threadIdx.x == 0) {
         ctr[C_NBLOBS] = totb;
         ctr[C_NGROUPS] = totg;
@@ -912,16 +917,11 @@ void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint6
                      uint64_t* ucnt, uint64_t* ubtot) {
     const uint64_t nblk = (nunits + AS_UNITS - 1) / AS_UNITS;
     uint64_t *ucb = ucnt, *ucg = ucnt + nunits, *bt_b = ubtot, *bt_g = ubtot + nblk + 1;
-    const unsigned g = (unsigned)((nunits + 255) / 256);
-    if (nunits) {
-        hipLaunchKernelGGL(k_unit_count, dim3(g), dim3(256), 0, st, units, nunits, segs, cfiles, chains, chain_n, seg_M,
-                           cf_invalid, fb_starts, fb_count, b, ucb, ucg);
-        hipLaunchKernelGGL(k_unit_partial, dim3((unsigned)nblk), dim3(AS_BLOCK), 0, st, ucb, ucg, nunits, bt_b, bt_g);
-    }
-    hipLaunchKernelGGL(k_unit_top, dim3(1), dim3(BLK), 0, st, bt_b, bt_g, nblk, ctr);
-    if (nunits)
-        hipLaunchKernelGGL(k_unit_emit, dim3(g), dim3(256), 0, st, units, nunits, segs, cfiles, chains, chain_n, seg_M,
-                           cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g);
+    if (!nunits) return;  // ctr's blob and group counts stay 0 (zeroed at submit)
+    hipLaunchKernelGGL(k_unit_count, dim3((unsigned)nblk), dim3(AS_BLOCK), 0, st, units, nunits, segs, cfiles, chains,
+                       chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g, ctr);
+    hipLaunchKernelGGL(k_unit_emit, dim3((unsigned)((nunits + 255) / 256)), dim3(256), 0, st, units, nunits, segs,
+                       cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g);
 }
 
 // ======================================================================== Chunk.hash

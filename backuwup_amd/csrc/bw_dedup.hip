@@ -10,11 +10,11 @@
 //
 // Layout: a digest log (32 B per blob ever submitted, position = canonical sequence number)
 // and an open-addressing table of {key = first 8 digest bytes, seq = min position}.
-//   k_append  copy the batch digests to the log tail
-//   k_claim   CAS the key into a slot, atomicMin the sequence number (first occurrence wins)
-//   k_verdict dup iff the slot's winner is an earlier position holding the same 32 bytes; a
-//             different digest behind the same 64-bit key is reported (BW_ECOLLISION), never
-//             silently merged.
+//   k_append_claim  copy the batch digests to the log tail; CAS each key into a slot and
+//                   atomicMin the sequence number (first occurrence wins)
+//   k_verdict       dup iff the slot's winner is an earlier position holding the same 32 bytes; a
+//                   different digest behind the same 64-bit key is reported (BW_ECOLLISION),
+//                   never silently merged; the last block advances the log length.
 #include "bw_device.h"
 #include "bw_internal.h"
 
@@ -47,20 +47,9 @@ __device__ __forceinline__ uint64_t batch_n(const uint64_t* n_dev, uint64_t n_ho
     return n_dev ? *n_dev : n_host;
 }
 
-__global__ void k_append(uint8_t* __restrict__ log, const uint64_t* dstate, const uint8_t* __restrict__ digests,
-                         const uint64_t* n_dev, uint64_t n_host) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= batch_n(n_dev, n_host)) return;
-    const uint64_t base = dstate[D_LOGLEN];
-    const uint4* s = (const uint4*)(digests + i * 32);
-    uint4* d = (uint4*)(log + (base + i) * 32);
-    d[0] = s[0];
-    d[1] = s[1];
-}
-
-// Claim log[lo + i] for i < n into the table.
-__device__ __forceinline__ void claim(uint64_t* table, uint64_t cap, const uint8_t* log, uint64_t seq) {
-    const uint64_t key = digest_key(log + seq * 32), mask = cap - 1;
+// Claim position seq, whose digest's key is `key`, into the table: the first occurrence wins.
+__device__ __forceinline__ void claim_key(uint64_t* table, uint64_t cap, uint64_t key, uint64_t seq) {
+    const uint64_t mask = cap - 1;
     uint64_t s = fmix64(key) & mask;
     for (;;) {
         unsigned long long* kp = (unsigned long long*)&table[2 * s];
@@ -77,51 +66,74 @@ __device__ __forceinline__ void claim(uint64_t* table, uint64_t cap, const uint8
     }
 }
 
-__global__ void k_claim(uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
-                        const uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= batch_n(n_dev, n_host)) return;
-    claim(table, cap, log, dstate[D_LOGLEN] + i);
+__device__ __forceinline__ void claim(uint64_t* table, uint64_t cap, const uint8_t* log, uint64_t seq) {
+    claim_key(table, cap, digest_key(log + seq * 32), seq);
 }
 
-__global__ void k_verdict(const uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
-                          uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host, uint8_t* __restrict__ is_dup) {
+// The batch's digests to the log tail, each claimed at its position as it is written.
+__global__ void k_append_claim(uint64_t* __restrict__ table, uint64_t cap, uint8_t* __restrict__ log,
+                               const uint64_t* dstate, const uint8_t* __restrict__ digests, const uint64_t* n_dev,
+                               uint64_t n_host) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= batch_n(n_dev, n_host)) return;
     const uint64_t seq = dstate[D_LOGLEN] + i;
-    const uint8_t* d = log + seq * 32;
-    const uint64_t key = digest_key(d), mask = cap - 1;
-    uint64_t s = fmix64(key) & mask;
-    while (table[2 * s] != key) s = (s + 1) & mask;
-    const uint64_t w = table[2 * s + 1];
-    uint8_t v;
-    if (w == seq) {
-        v = 0;
-        atomicAdd((unsigned long long*)&dstate[D_NUNIQUE], 1ull);
-    } else {
-        const uint4* a = (const uint4*)(log + w * 32);
-        const uint4* b = (const uint4*)d;
-        const uint4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
-        const bool same = a0.x == b0.x && a0.y == b0.y && a0.z == b0.z && a0.w == b0.w && a1.x == b1.x &&
-                          a1.y == b1.y && a1.z == b1.z && a1.w == b1.w;
-        v = same ? 1 : 2;
-        if (!same) atomicOr((unsigned long long*)&dstate[D_COLLIDE], 1ull);
-    }
-    if (is_dup) is_dup[i] = v;
+    const uint4* s = (const uint4*)(digests + i * 32);
+    const uint4 s0 = s[0], s1 = s[1];
+    uint4* d = (uint4*)(log + seq * 32);
+    d[0] = s0;
+    d[1] = s1;
+    const uint64_t key = ((uint64_t)s0.y << 32) | s0.x;
+    claim_key(table, cap, key ? key : 1, seq);
 }
 
-__global__ void k_advance(uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) dstate[D_LOGLEN] += batch_n(n_dev, n_host);
+// Verdicts of the batch (after every claim); the last block to finish advances the log length,
+// which every block read first (no separate launch).
+__global__ void k_verdict(const uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
+                          uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host, uint8_t* __restrict__ is_dup) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n = batch_n(n_dev, n_host);
+    const uint64_t base = dstate[D_LOGLEN];
+    if (i < n) {
+        const uint64_t seq = base + i;
+        const uint8_t* d = log + seq * 32;
+        const uint64_t key = digest_key(d), mask = cap - 1;
+        uint64_t s = fmix64(key) & mask;
+        while (table[2 * s] != key) s = (s + 1) & mask;
+        const uint64_t w = table[2 * s + 1];
+        uint8_t v;
+        if (w == seq) {
+            v = 0;
+            atomicAdd((unsigned long long*)&dstate[D_NUNIQUE], 1ull);
+        } else {
+            const uint4* a = (const uint4*)(log + w * 32);
+            const uint4* b = (const uint4*)d;
+            const uint4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+            const bool same = a0.x == b0.x && a0.y == b0.y && a0.z == b0.z && a0.w == b0.w && a1.x == b1.x &&
+                              a1.y == b1.y && a1.z == b1.z && a1.w == b1.w;
+            v = same ? 1 : 2;
+            if (!same) atomicOr((unsigned long long*)&dstate[D_COLLIDE], 1ull);
+        }
+        if (is_dup) is_dup[i] = v;
+    }
+    __shared__ bool last;
+    __syncthreads();  // every thread of the block has read D_LOGLEN
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd((unsigned long long*)&dstate[D_DONE], 1ull) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {  // every block has read D_LOGLEN: advance it for the next gate
+        dstate[D_LOGLEN] = base + n;
+        dstate[D_DONE] = 0;
+    }
 }
 
 void launch_dedup(hipStream_t st, uint64_t* table, uint64_t cap, uint8_t* log, uint64_t* dstate,
                   const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n, uint8_t* is_dup) {
     if (!max_n) return;
     const dim3 g((unsigned)((max_n + 255) / 256)), b(256);
-    hipLaunchKernelGGL(k_append, g, b, 0, st, log, dstate, digests, n_dev, n_host);
-    hipLaunchKernelGGL(k_claim, g, b, 0, st, table, cap, log, dstate, n_dev, n_host);
+    hipLaunchKernelGGL(k_append_claim, g, b, 0, st, table, cap, log, dstate, digests, n_dev, n_host);
     hipLaunchKernelGGL(k_verdict, g, b, 0, st, table, cap, log, dstate, n_dev, n_host, is_dup);
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st, dstate, n_dev, n_host);
 }
 
 __global__ void k_rehash(uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,

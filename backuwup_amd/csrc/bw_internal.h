@@ -49,6 +49,8 @@ enum Ctr : int {
     C_IX_OVF = 11,    // an exchange bucket overflowed (D_BUCKET_OVF)
     C_IX_LOGLEN = 12, // log length (D_LOGLEN)
     C_IX_VALID = 13,  // 1 = the snapshot was taken
+    C_DONE_TILES = 14, // blocks of the tile-count scan that finished (its last block scans the totals)
+    C_DONE_UNITS = 15, // blocks of the unit-count scan that finished (likewise)
     C_COUNT = 16
 };
 static_assert(SCAN_STRIP_SMALL % (4 * SCAN_STEP) == 0, "k_scan consumes four 64-byte steps per iteration");
@@ -139,7 +141,8 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),
 // st[1] = distinct digests, st[2] = collision flag.
 // st[3] = an exchange bucket overflowed (a batch had more blobs than the agreed capacity).
-enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_COLLIDE = 2, D_BUCKET_OVF = 3, D_COUNT = 4 };
+// st[4] = blocks of the running gate's verdict pass that finished (its last block advances st[0]).
+enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_COLLIDE = 2, D_BUCKET_OVF = 3, D_DONE = 4, D_COUNT = 5 };
 void launch_table_clear(hipStream_t st, uint64_t* table, uint64_t cap);
 // Append n digests (n from *n_dev if non-null, else n_host) to the log and decide them in
 // order: is_dup[i] (may be null) = digest seen at an earlier log position.
