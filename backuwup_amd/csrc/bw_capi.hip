@@ -65,6 +65,9 @@ struct Slot {
     uint64_t res_n = 0;
     hipEvent_t done = nullptr;   // the staged copies landed
     uint64_t mark = 0;           // the index's enq_total right after this batch's gate
+    // a batch split by BW_OPT_SPLIT: its tail part is ticket tail_ticket of the context's helper,
+    // holding files [tail_file0, n_files)
+    uint64_t tail_ticket = 0, tail_file0 = 0;
 };
 
 }  // namespace
@@ -111,6 +114,16 @@ struct bw_ctx {
     int depth = 2;
     uint64_t next_ticket = 1, last_ticket = 0;
     uint64_t last_n = 0;  // blobs of the last batch read back (sizes the next batches' staged results)
+    // Intra-batch pipelining (BW_OPT_SPLIT): a multi-file batch below split_max bytes is cut by
+    // bytes into a head (this context) and a tail (a helper context on its own stream, attached to
+    // the same index), with the two scans and the two BLAKE3 passes each run in order, so the
+    // tail's scan runs beside the head's hashing: one batch in flight still keeps the scan (HBM)
+    // and BLAKE3 (VALU) side by side.  The gates stay in file order (head, then tail).
+    int split = 2;
+    uint64_t split_min = 64ull << 20, split_max = 4ull << 30;
+    bw_ctx* helper = nullptr;
+    bool is_helper = false;
+    hipEvent_t e_split = nullptr, e_tail = nullptr;
     // the synchronous helpers (bw_process_files, bw_fastcdc_chunks, bw_blake3_hash(_many), tree
     // blobs) run in a slot of their own outside the ring: they never drop a batch the caller still
     // holds a ticket for, and leave last_ticket (bw_results, bw_batch_views) unchanged
@@ -126,7 +139,7 @@ struct bw_ctx {
     uint64_t scan_small_bytes = SCAN_SMALL_BYTES;
     bool order_hash = false;  // BW_OPT_ORDER_HASH
     uint64_t cand_cap_forced = 0;
-    int b3_loads = B3_LOADS_PAIRS;
+    int b3_loads = B3_LOADS_LINES;  // k_b3_lines: 1.07x fetch (pairs 1.42x), -6 % time isolated
     int scan_waves = 16;
     // latency stream: the small kernels between the two big passes (compaction, boundary
     // resolution, assembly, upper tree levels, gate, records) on a high-priority stream, so they
@@ -507,6 +520,9 @@ extern "C" int bw_create(int device, bw_ctx** out) {
 
 extern "C" void bw_destroy(bw_ctx* c) {
     if (!c) return;
+    if (c->helper) bw_destroy(c->helper);  // its batches end before this context's buffers go
+    for (hipEvent_t e : {c->e_split, c->e_tail})
+        if (e) hipEventDestroy(e);
     if (c->host_timing && c->host_batches)
         fprintf(stderr, "bw host ms/batch over %llu batches: meta %.3f bufs %.3f upload %.3f launch %.3f gate %.3f tail %.3f\n",
                 (unsigned long long)c->host_batches, c->host_ms[0] / c->host_batches, c->host_ms[1] / c->host_batches,
@@ -587,17 +603,26 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             c->depth = (int)v;
             for (Slot& s : c->slots) s.ticket = 0;  // earlier tickets are no longer addressable
             c->last_ticket = 0;
+            if (c->helper) return bw_set_option(c->helper, opt, v);
             return BW_OK;
-        case BW_OPT_SCAN_SMALL_BYTES: c->scan_small_bytes = v; return BW_OK;
+        case BW_OPT_SPLIT:
+            if (v < 1 || v > 2) return BW_EINVAL;
+            c->split = (int)v;
+            return BW_OK;
+        case BW_OPT_SCAN_SMALL_BYTES:
+            c->scan_small_bytes = v;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_ORDER_HASH:
             if (v > 1) return BW_EINVAL;
             c->order_hash = v != 0;
             return BW_OK;
-        case BW_OPT_CAND_CAP: c->cand_cap_forced = v; return BW_OK;
+        case BW_OPT_CAND_CAP:
+            c->cand_cap_forced = v;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_SCAN_WAVES:
             if (v != 8 && v != 16) return BW_EINVAL;
             c->scan_waves = (int)v;
-            return BW_OK;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_LATENCY_STREAM:
             if (v && !c->hi) {
                 hipSetDevice(c->device);
@@ -622,7 +647,7 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
         case BW_OPT_B3_LOADS:
             if (v > B3_LOADS_LINES) return BW_EINVAL;
             c->b3_loads = (int)v;
-            return BW_OK;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_STAGE_CHUNK:
             if (v < 4096) return BW_EINVAL;
             hipSetDevice(c->device);
@@ -665,6 +690,7 @@ extern "C" int bw_attach_index(bw_ctx* c, bw_index* x) {
     c->idx = x;
     c->idx_mark = 0;
     if (old != c->own_idx) index_release(old);
+    if (c->helper) return bw_attach_index(c->helper, x);
     return BW_OK;
 }
 
@@ -761,7 +787,7 @@ static int stage_results(bw_ctx* c, Slot& s) {
 
 // Enqueue one batch (bytes at d_data, in HBM) into slot `s` on the context stream.
 static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
-                  const uint64_t* flen, uint64_t nf, const bw_params* prm, bool stage = true) {
+                  const uint64_t* flen, uint64_t nf, const bw_params* prm, bool stage = true, bool order_force = false) {
     Masks mk;
     if (int rc = validate_batch(c, data_len, foff, flen, nf, prm, &mk)) return rc;
     if (data_len && !d_data) return BW_EINVAL;
@@ -938,7 +964,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     rc |= ensure(c, s.is_dup, max_blobs);
     rc |= ensure(c, s.packed, max_blobs * sizeof(bw_blob));
     rc |= ensure(c, c->ucnt, 2 * nunits * 8);
-    rc |= ensure(c, c->ubtot, 2 * (nunits / 1024 + 2) * 8);
+    rc |= ensure(c, c->ubtot, 2 * (nunits / 256 + 2) * 8);
     if (rc) return BW_ENOMEM;
     // candidate array: 4x the expected count (2^-popcount(mask) per byte) plus slack.  A batch that
     // finds more stays exact (the walkers test the bytes past the array's end, C_TRUNC) and the
@@ -981,7 +1007,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     if (ncf_pre) {
         bw_index* x = c->idx;
         std::unique_lock<std::mutex> lk(x->mu, std::defer_lock);
-        if (c->order_hash) {
+        if (c->order_hash || order_force) {
             lk.lock();
             if (x->scan_tail_set) HIPCHK(c, hipStreamWaitEvent(st, x->scan_tail, 0));
         }
@@ -990,7 +1016,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
             c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
             return BW_EINVAL;
         }
-        if (c->order_hash) {
+        if (c->order_hash || order_force) {
             HIPCHK(c, hipEventRecord(x->scan_tail, st));
             x->scan_tail_set = true;
         }
@@ -1039,14 +1065,14 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         hipEvent_t between = c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : (split ? c->e_b3 : nullptr);
         bw_index* x = c->idx;
         std::unique_lock<std::mutex> lk(x->mu, std::defer_lock);
-        if (c->order_hash) {
+        const bool order = c->order_hash || order_force;
+        if (order) {
             lk.lock();
             if (x->hash_tail_set) HIPCHK(c, hipStreamWaitEvent(st, x->hash_tail, 0));
         }
         launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint32_t>(c->cv2),
-                      P<uint8_t>(s.digests), max_leaves, between, c->b3_loads, lat,
-                      c->order_hash ? x->hash_tail : nullptr);
-        if (c->order_hash) x->hash_tail_set = true;
+                      P<uint8_t>(s.digests), max_leaves, between, c->b3_loads, lat, order ? x->hash_tail : nullptr);
+        if (order) x->hash_tail_set = true;
     } else {
         prof_mark(c, BW_STAGE_B3TREE, st);
         if (split) {
@@ -1100,14 +1126,86 @@ static const bw_params* params_or_default(const bw_params* prm, bw_params* def) 
     return def;
 }
 
+// The helper context of BW_OPT_SPLIT: same device, index and kernel options, its own stream.
+static int ensure_helper(bw_ctx* c) {
+    if (c->helper) return BW_OK;
+    bw_ctx* h = nullptr;
+    if (int rc = bw_create(c->device, &h)) return rc;
+    h->is_helper = true;
+    h->depth = c->depth;
+    h->scan_small_bytes = c->scan_small_bytes;
+    h->cand_cap_forced = c->cand_cap_forced;
+    h->b3_loads = c->b3_loads;
+    h->scan_waves = c->scan_waves;
+    if (int rc = bw_attach_index(h, c->idx)) {
+        bw_destroy(h);
+        return rc;
+    }
+    if (c->prof) bw_profile_enable(h, 1);
+    if (!c->e_split) HIPCHK(c, hipEventCreateWithFlags(&c->e_split, hipEventDisableTiming));
+    if (!c->e_tail) HIPCHK(c, hipEventCreateWithFlags(&c->e_tail, hipEventDisableTiming));
+    c->helper = h;
+    return BW_OK;
+}
+
+// First file of the tail part, or 0 = do not split.  Splits only batches that gate through the
+// index (a NO_DEDUP batch's device views feed the multi-GPU exchange whole), hold at least two
+// files, and are large enough to amortise the second submission but small enough that one batch
+// in flight leaves the scan and BLAKE3 passes apart (large batches fill the chip either way).
+static uint64_t split_point(bw_ctx* c, uint64_t data_len, const uint64_t* flen, uint64_t nf, const bw_params* prm) {
+    if (c->split < 2 || c->is_helper || nf < 2 || (prm->flags & (BW_F_NO_DEDUP | BW_F_NO_HASH))) return 0;
+    if (data_len > c->split_max) return 0;
+    uint64_t total = 0;
+    for (uint64_t f = 0; f < nf; f++) total += flen[f];
+    if (total < c->split_min) return 0;
+    uint64_t acc = 0;
+    for (uint64_t f = 0; f + 1 < nf; f++) {  // the head ends at the first file that reaches half the bytes
+        acc += flen[f];
+        if (2 * acc >= total) return f + 1;
+    }
+    return nf - 1;
+}
+
+// Submit into slot s of c, split into a head (here) and a tail (c's helper) when split_point says
+// so.  d_data is already ordered on c's stream (caller data, or the slot's input after stream_in).
+static int submit_split(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
+                        const uint64_t* flen, uint64_t nf, const bw_params* prm) {
+    s.tail_ticket = 0;
+    Masks mk;
+    if (int rc = validate_batch(c, data_len, foff, flen, nf, prm, &mk)) return rc;
+    const uint64_t f0 = split_point(c, data_len, flen, nf, prm);
+    if (!f0) return submit(c, s, d_data, data_len, foff, flen, nf, prm);
+    if (int rc = ensure_helper(c)) return rc;
+    bw_ctx* h = c->helper;
+    HIPCHK(c, hipEventRecord(c->e_split, c->stream));  // the tail sees what the caller ordered before
+    if (int rc = submit(c, s, d_data, data_len, foff, flen, f0, prm, true, true)) return rc;
+    HIPCHK(c, hipStreamWaitEvent(h->stream, c->e_split, 0));
+    uint64_t t2 = 0;
+    Slot& s2 = claim_slot(h, &t2);
+    if (int rc = submit(h, s2, d_data, data_len, foff + f0, flen + f0, nf - f0, prm, true, true)) {
+        s2.ticket = 0;
+        c->err = "tail part: " + h->err;
+        return rc;
+    }
+    // the batch ends on c's stream once both parts have (the caller's order, and the slot's input
+    // is free only after the tail's BLAKE3 read it too)
+    HIPCHK(c, hipEventRecord(c->e_tail, h->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->e_tail, 0));
+    HIPCHK(c, hipEventRecord(s.input_free, c->stream));
+    s.tail_ticket = t2;
+    s.tail_file0 = f0;
+    return BW_OK;
+}
+
 extern "C" int bw_submit_device(bw_ctx* c, const uint8_t* d_data, uint64_t data_len, const uint64_t* foff,
                                 const uint64_t* flen, uint64_t nf, const bw_params* prm, uint64_t* ticket) {
     if (!c) return BW_EINVAL;
     if (ticket) *ticket = 0;
     bw_params def;
     prm = params_or_default(prm, &def);
+    hipSetDevice(c->device);
     Slot& s = claim_slot(c, ticket);
-    if (int rc = submit(c, s, d_data, data_len, foff, flen, nf, prm)) {
+    if (int rc = submit_split(c, s, d_data, data_len, foff, flen, nf, prm)) {
         s.ticket = 0;
         if (ticket) *ticket = 0;
         return rc;
@@ -1172,7 +1270,7 @@ extern "C" int bw_submit_host(bw_ctx* c, const uint8_t* data, uint64_t data_len,
     hipSetDevice(c->device);
     Slot& s = claim_slot(c, ticket);
     int rc = stream_in(c, s, data, data_len);
-    if (!rc) rc = submit(c, s, P<uint8_t>(s.input), data_len, foff, flen, nf, prm);
+    if (!rc) rc = submit_split(c, s, P<uint8_t>(s.input), data_len, foff, flen, nf, prm);
     if (rc) {
         s.ticket = 0;
         if (ticket) *ticket = 0;
@@ -1230,6 +1328,31 @@ static int slot_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t
     return BW_OK;
 }
 
+// Results of a batch that may have been split: the head's blobs, then the tail's with their file
+// indices shifted back to the batch's numbering.
+static int batch_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t* n_out) {
+    if (!s.tail_ticket) return slot_results(c, s, out, cap, n_out);
+    Slot* t = c->helper ? slot_of(c->helper, s.tail_ticket) : nullptr;
+    if (!t) {
+        c->err = "the batch's tail part is no longer held by the helper context";
+        return BW_ESTATE;
+    }
+    uint64_t na = 0, nb = 0;
+    if (int rc = slot_results(c, s, nullptr, 0, &na)) return rc;
+    if (int rc = slot_results(c->helper, *t, nullptr, 0, &nb)) {
+        c->err = "tail part: " + c->helper->err;
+        return rc;
+    }
+    *n_out = na + nb;
+    c->last_n = na + nb;
+    if (na + nb > cap) return BW_ENOSPC;
+    if (!out) return BW_OK;
+    if (int rc = slot_results(c, s, out, na, &na)) return rc;
+    if (int rc = slot_results(c->helper, *t, out + na, nb, &nb)) return rc;
+    for (uint64_t i = 0; i < nb; i++) out[na + i].file += s.tail_file0;
+    return BW_OK;
+}
+
 extern "C" int bw_wait(bw_ctx* c, uint64_t ticket, bw_blob* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return BW_EINVAL;
     Slot* s = slot_of(c, ticket);
@@ -1237,20 +1360,24 @@ extern "C" int bw_wait(bw_ctx* c, uint64_t ticket, bw_blob* out, uint64_t cap, u
         c->err = "ticket " + std::to_string(ticket) + " is not (or no longer) held by the context";
         return BW_ESTATE;
     }
-    return slot_results(c, *s, out, cap, n_out);
+    return batch_results(c, *s, out, cap, n_out);
 }
 
 extern "C" int bw_results(bw_ctx* c, bw_blob* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return BW_EINVAL;
     Slot* s = slot_of(c, c->last_ticket);
     if (!s) return BW_ESTATE;
-    return slot_results(c, *s, out, cap, n_out);
+    return batch_results(c, *s, out, cap, n_out);
 }
 
 extern "C" int bw_batch_device_views(bw_ctx* c, uint64_t* n_blobs, const uint8_t** d_digests, uint8_t** d_is_dup) {
     if (!c) return BW_EINVAL;
     Slot* s = slot_of(c, c->last_ticket);
     if (!s) return BW_ESTATE;
+    if (s->tail_ticket) {
+        c->err = "the batch was split in two parts (BW_OPT_SPLIT): no single device view";
+        return BW_ESTATE;
+    }
     hipSetDevice(c->device);
     uint64_t n = 0;
     HIPCHK(c, hipMemcpyAsync(&n, (uint64_t*)s->ctr.p + C_NBLOBS, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1382,6 +1509,10 @@ extern "C" int bw_batch_views(bw_ctx* c, uint64_t ticket, const uint64_t** d_n_b
     if (!c) return BW_EINVAL;
     Slot* s = slot_of(c, ticket ? ticket : c->last_ticket);
     if (!s) return BW_ESTATE;
+    if (s->tail_ticket) {
+        c->err = "the batch was split in two parts (BW_OPT_SPLIT): no single device view";
+        return BW_ESTATE;
+    }
     if (d_n_blobs) *d_n_blobs = P<uint64_t>(s->ctr) + C_NBLOBS;
     if (d_digests) *d_digests = P<uint8_t>(s->digests);
     if (d_is_dup) *d_is_dup = P<uint8_t>(s->is_dup);
@@ -1495,6 +1626,8 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
 
 extern "C" int bw_profile_enable(bw_ctx* c, int on) {
     if (!c) return BW_EINVAL;
+    if (c->helper)
+        if (int rc = bw_profile_enable(c->helper, on)) return rc;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     for (int k = 0; k < 2; k++) {
@@ -1512,8 +1645,12 @@ extern "C" int bw_profile_read(bw_ctx* c, double* stage_ms, uint64_t* n_batches)
     if (!c) return BW_EINVAL;
     prof_collect(c, 0);
     prof_collect(c, 1);
+    if (c->helper) {  // split batches: the tail parts' stage times add to the batch's
+        prof_collect(c->helper, 0);
+        prof_collect(c->helper, 1);
+    }
     if (stage_ms)
-        for (int i = 0; i < BW_N_STAGES; i++) stage_ms[i] = c->stage_ms[i];
+        for (int i = 0; i < BW_N_STAGES; i++) stage_ms[i] = c->stage_ms[i] + (c->helper ? c->helper->stage_ms[i] : 0);
     if (n_batches) *n_batches = c->prof_batches;
     return BW_OK;
 }

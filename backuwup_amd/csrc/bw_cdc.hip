@@ -839,11 +839,12 @@ __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDe
 // (C4) spreads over the chip: per-unit blob/group counts (one thread per unit), a two-level
 // exclusive scan of the counts (1024 units per block, then one block over the block totals),
 // and the emit pass writing each unit's blobs at its offsets.
-constexpr int AS_BLOCK = 256;                      // threads per block, 4 units each
-constexpr uint64_t AS_UNITS = 4ull * AS_BLOCK;     // units per partial-scan block
+constexpr int AS_BLOCK = 256;                      // threads per block, one unit each
+constexpr uint64_t AS_UNITS = AS_BLOCK;            // units per partial-scan block
 
-// Per-unit blob/group counts (4 units per thread), their exclusive scan inside the block, and in
-// the grid's last block the scan of the block totals (the batch's blob and group counts).
+// Per-unit blob/group counts (one unit per thread: a CDC segment's count walks up to 128 chain
+// entries, so four per thread made C1's pass 4x longer), their exclusive scan inside the block,
+// and in the grid's last block the scan of the block totals (the batch's blob and group counts).
 __global__ __launch_bounds__(AS_BLOCK) void k_unit_count(const UnitDesc* __restrict__ units, uint64_t nunits,
                                                          const SegDesc* __restrict__ segs,
                                                          const CFileDesc* __restrict__ cfiles,
@@ -857,26 +858,18 @@ __global__ __launch_bounds__(AS_BLOCK) void k_unit_count(const UnitDesc* __restr
                                                          uint64_t* __restrict__ bt_b, uint64_t* __restrict__ bt_g,
                                                          uint64_t* ctr) {
     __shared__ uint64_t s[AS_BLOCK];
-    const uint64_t i0 = ((uint64_t)blockIdx.x * AS_BLOCK + threadIdx.x) * 4;
-    uint64_t cb[4], cg[4], sb = 0, sg = 0;
-    for (int k = 0; k < 4; k++) {
-        cb[k] = cg[k] = 0;
-        if (i0 + k < nunits)
-            unit_blobs<false>(units[i0 + k], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b,
-                              0, 0, cb[k], cg[k]);
-        sb += cb[k];
-        sg += cg[k];
-    }
+    const uint64_t u = (uint64_t)blockIdx.x * AS_BLOCK + threadIdx.x;
+    uint64_t nb = 0, ng = 0;
+    if (u < nunits)
+        unit_blobs<false>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, 0, 0, nb,
+                          ng);
     uint64_t tb, tg;
-    uint64_t rb = block_excl_sum<AS_BLOCK>(sb, s, &tb);
-    uint64_t rg = block_excl_sum<AS_BLOCK>(sg, s, &tg);
-    for (int k = 0; k < 4; k++)
-        if (i0 + k < nunits) {
-            ucb[i0 + k] = rb;
-            ucg[i0 + k] = rg;
-            rb += cb[k];
-            rg += cg[k];
-        }
+    const uint64_t rb = block_excl_sum<AS_BLOCK>(nb, s, &tb);
+    const uint64_t rg = block_excl_sum<AS_BLOCK>(ng, s, &tg);
+    if (u < nunits) {
+        ucb[u] = rb;
+        ucg[u] = rg;
+    }
     if (threadIdx.x == 0) {
         bt_b[blockIdx.x] = tb;
         bt_g[blockIdx.x] = tg;

@@ -158,15 +158,21 @@ enum {
     BW_OPT_CAND_CAP = 3,         /* test hook: fixed candidate array capacity (0 = sized per batch)  */
     BW_OPT_STAGE_CHUNK = 4,      /* pinned staging chunk for pageable bw_submit_host input (64 MiB)  */
     BW_OPT_B3_LOADS = 5,         /* BLAKE3 leaf pass loads: 0 = one block ahead, 1 = 132-byte block pairs,
-                                    2 = aligned 128-byte lines through a register ring (k_b3_lines) */
+                                    2 = aligned 128-byte lines through registers (k_b3_lines, default) */
     BW_OPT_SCAN_WAVES = 6,       /* gear-scan workgroup: 16 waves (default) or 8 (leaves LDS for BLAKE3) */
     BW_OPT_LATENCY_STREAM = 7,   /* 1: the small kernels between the passes on a high-priority stream */
     BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (768 KiB of hash tables each; 16384) */
     BW_OPT_ZSTD_BATCH_BYTES = 9, /* bw_zstd_*: input bytes per internal batch (~4.2x in scratch; 8 GiB) */
-    BW_OPT_ORDER_HASH = 10       /* 1: the scans and the BLAKE3 leaf passes of the contexts sharing an
+    BW_OPT_ORDER_HASH = 10,      /* 1: the scans and the BLAKE3 leaf passes of the contexts sharing an
                                     index run one at a time each, in submission order (a batch's scan
                                     then overlaps the previous batch's hashing); 0 (default): as soon
                                     as their inputs are ready */
+    BW_OPT_SPLIT = 11            /* 2 (default): a batch of >= 2 files between 64 MiB and 4 GiB that
+                                    gates through the index runs as two parts on two streams (head
+                                    files here, tail files on a helper context), scans and BLAKE3
+                                    passes in order, so one batch in flight keeps the scan beside
+                                    the hashing; 1: off.  bw_batch_views / bw_batch_device_views of a
+                                    split batch return BW_ESTATE (NO_DEDUP batches are never split) */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 

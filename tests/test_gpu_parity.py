@@ -32,12 +32,12 @@ KAT = {
 
 
 # every BLAKE3 test runs with each leaf-pass loader: 0 = one block ahead, 1 = 132-byte block pairs
-# (k_b3_groups), 2 = aligned 128-byte lines through a register ring (k_b3_lines), default
+# (k_b3_groups), 2 = aligned 128-byte lines through registers (k_b3_lines, the default)
 @pytest.fixture(params=[0, 1, 2], ids=["prefetch", "pairs", "lines"])
 def b3ctx(ctx, request):
     ctx.set_option(BW_OPT_B3_LOADS, request.param)
     yield ctx
-    ctx.set_option(BW_OPT_B3_LOADS, 1)  # the context default
+    ctx.set_option(BW_OPT_B3_LOADS, 2)  # the context default
 
 
 def test_blake3_kat(b3ctx):

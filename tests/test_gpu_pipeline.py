@@ -71,6 +71,64 @@ def test_tickets_ring(oracle):
             c.wait(tickets[3] + 1)
 
 
+def test_split_batches_match_unsplit(oracle):
+    """BW_OPT_SPLIT: multi-file batches of 64 MiB - 4 GiB run as a head (this context) and a tail
+    (a helper context) with their scans and BLAKE3 passes in order.  Four batches of a tree corpus
+    over two contexts sharing an index, with the split on and off: the blobs (file indices in the
+    batch's numbering), digests and verdicts equal the oracle either way, also from pinned host
+    memory, with depth 3 rings; a split batch has no single device view."""
+    import torch
+    from backuwup_amd._lib import BW_OPT_SPLIT
+    data, offs, lens = tree_corpus(320 << 20, seed=91, max_file=40 << 20)
+    nf = len(lens)
+    bounds = [(0, nf // 3), (nf // 3, 2 * nf // 3), (2 * nf // 3, nf), (0, nf // 3)]
+    batches = _slices(data, offs, lens, bounds)
+    assert all(int(l.sum()) >= (64 << 20) and len(l) >= 2 for _, _, l in batches)
+    want = oracle_session(oracle, batches)
+    devs = [torch.from_numpy(d).cuda() for d, _, _ in batches]
+    torch.cuda.synchronize()
+    for split in (2, 1):
+        ix = Index(0)
+        cs = [Context(0), Context(0)]
+        try:
+            for c in cs:
+                c.set_stream(torch.cuda.Stream().cuda_stream)
+                c.attach_index(ix)
+                c.set_option(BW_OPT_SPLIT, split)
+                c.set_option(BW_OPT_DEPTH, 3)
+            cs[0].index_reset(1 << 16)
+            tickets = [cs[k % 2].submit_device(t.data_ptr(), d.size, o, l) for k, (t, (d, o, l)) in
+                       enumerate(zip(devs, batches))]
+            for k, t in enumerate(tickets):
+                blobs_equal(cs[k % 2].wait(t), want[k], (split, k))
+            blobs_equal(cs[1].results(), want[3], (split, "results"))
+            if split == 2:
+                with pytest.raises(BwError) as e:
+                    cs[1].batch_views(tickets[3])
+                assert e.value.rc == BW_ESTATE
+            cs[0].index_check()
+        finally:
+            for c in cs:
+                c.close()
+            ix.close()
+    # the same batches from pinned host memory on one context (split on by default)
+    pinned = []
+    for d, _, _ in batches:
+        t = torch.empty(d.size, dtype=torch.uint8, pin_memory=True)
+        t.numpy()[:] = d
+        pinned.append(t)
+    with Context(0) as c:
+        c.index_reset(1 << 16)
+        tickets = [c.submit_host(t.data_ptr(), o, l, data_len=d.size) for t, (d, o, l) in zip(pinned[:2], batches)]
+        got = [c.wait(tickets[0])]
+        tickets.append(c.submit_host(pinned[2].data_ptr(), batches[2][1], batches[2][2], data_len=batches[2][0].size))
+        got.append(c.wait(tickets[1]))
+        tickets.append(c.submit_host(pinned[3].data_ptr(), batches[3][1], batches[3][2], data_len=batches[3][0].size))
+        got += [c.wait(tickets[2]), c.wait(tickets[3])]
+        for k in range(4):
+            blobs_equal(got[k], want[k], ("pinned", k))
+
+
 def test_sync_helpers_leave_held_tickets_alone(oracle):
     """the synchronous helpers (tree blobs, blake3.hash, process_files, fastcdc_chunks)
     run outside the ticket ring.  With the default depth of 2, two submitted batches stay readable

@@ -4,7 +4,8 @@ mean batch period (scan start to next scan start), the busy time (union of the b
 the idle gap inside the batch and between batches, and the mean duration and count of every kernel
 per batch, so the fixed costs a single batch in flight cannot hide are visible by name.
 
-Usage: trace_batches.py run_kernel_trace.csv [skip_batches] [out.json]"""
+Usage: trace_batches.py run_kernel_trace.csv [skip_batches] [out.json] [scans_per_batch]
+(scans_per_batch = 2 for batches split into a head and a tail part, BW_OPT_SPLIT)"""
 import collections
 import csv
 import json
@@ -17,7 +18,8 @@ def main():
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     ks = [(r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1],
            int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "bw::" in r["Kernel_Name"]]
-    starts = [s for n, s, e in ks if n == "k_scan"]
+    per_batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    starts = [s for n, s, e in ks if n == "k_scan"][::per_batch]
     if len(starts) < skip + 3:
         raise SystemExit("too few batches in the trace")
     starts = starts[skip:-1]
