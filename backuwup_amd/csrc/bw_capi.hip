@@ -119,7 +119,7 @@ struct bw_ctx {
     // the same index), with the two scans and the two BLAKE3 passes each run in order, so the
     // tail's scan runs beside the head's hashing: one batch in flight still keeps the scan (HBM)
     // and BLAKE3 (VALU) side by side.  The gates stay in file order (head, then tail).
-    int split = 2;
+    int split = 1;  // off by default: measured slower on C1
     uint64_t split_min = 64ull << 20, split_max = 4ull << 30;
     bw_ctx* helper = nullptr;
     bool is_helper = false;
@@ -1051,9 +1051,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     launch_assemble(lat, ctr, d_units, nunits, d_segs, d_cfs,
                     P<uint64_t>(c->chains), P<uint32_t>(c->chain_n), P<uint64_t>(c->seg_M), P<uint32_t>(c->cf_invalid),
                     P<uint64_t>(c->fb_starts), P<uint64_t>(c->fb_count), b, P<uint64_t>(c->ucnt),
-                    P<uint64_t>(c->ubtot));
-    if (ncf) launch_cut_hash(lat, d_data, mk, ctr, b, max_blobs);
-    else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, lat));
+                    P<uint64_t>(c->ubtot), d_data, mk);  // also writes Chunk.hash
     if (split) {
         HIPCHK(c, hipEventRecord(c->e_lat, lat));
         HIPCHK(c, hipStreamWaitEvent(st, c->e_lat, 0));
@@ -1337,9 +1335,9 @@ static int batch_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_
         c->err = "the batch's tail part is no longer held by the helper context";
         return BW_ESTATE;
     }
-    uint64_t na = 0, nb = 0;
-    if (int rc = slot_results(c, s, nullptr, 0, &na)) return rc;
-    if (int rc = slot_results(c->helper, *t, nullptr, 0, &nb)) {
+    uint64_t na = 0, nb = 0;  // the parts' counts first (no copy, no capacity limit)
+    if (int rc = slot_results(c, s, nullptr, ~0ull, &na)) return rc;
+    if (int rc = slot_results(c->helper, *t, nullptr, ~0ull, &nb)) {
         c->err = "tail part: " + c->helper->err;
         return rc;
     }

@@ -16,14 +16,14 @@
 //               byte; flagged 64-byte blocks made exact by the wave at the end of each tile
 //   k_tile_partial  exclusive scan of per-tile counts -> candidate array offsets (block scans; the
 //               grid's last block scans the block totals)
-//   k_rescan<false> exact counts of overflowed tiles (candidate-dense data, small parameters)
-//   k_compact   copy slots; k_rescan<true> writes the overflowed tiles' candidates
+//               (it first rescans its overflowed tiles for exact counts: candidate-dense data)
+//   k_compact   copy slots; overflowed tiles are rescanned by their block and written in place
 //   k_chains    one wave per segment: speculative boundary chain from the segment start
 //   k_extend    continue each chain until it merges with the next segment's chain (CDC resync)
 //   k_resolve   prefix-max of merge points -> true chain entry of every segment, validity
 //   k_fallback  serial wave walker for files whose chains did not merge (exact, slower)
 //   k_unit_*    canonical-order blob table + BLAKE3 group offsets (count + scan, emit)
-//   k_cut_hash  Chunk.hash (the crate's returned gear state) for every CDC chunk
+//   k_unit_emit also writes each CDC chunk's Chunk.hash (the crate's returned gear state)
 #include "bw_device.h"
 #include "bw_internal.h"
 
@@ -380,15 +380,80 @@ __device__ __forceinline__ uint64_t scan_totals(uint64_t* tot, uint64_t n, uint6
 
 constexpr int BLK = 1024;
 
-// Candidate offsets: a three-kernel scan over the per-tile counts (tiles are 128 KiB, so a
-// 16 GiB batch has 131072 of them): block-local scans of 1024 counts, one block over the block
-// totals, then compaction adds the block base and copies the slots.
+// Exact ordered re-scan of a tile on the overflow list (candidate-dense data or small parameters)
+// by a whole block of RESCAN_THREADS: WRITE = false returns the tile's candidate count (before the
+// offset scan), WRITE = true also stores its candidates from cand[base] on (after it).  s_gear is
+// the plain 256-entry table in LDS.
+constexpr int RESCAN_THREADS = 256;
+
+template <bool WRITE>
+__device__ uint64_t rescan_tile(const uint8_t* __restrict__ data, uint64_t n_bytes, const Masks& mk, uint64_t tile,
+                                uint64_t base, uint64_t* __restrict__ cand, uint64_t cap, const uint64_t* s_gear,
+                                uint64_t* s_scan) {
+    const uint64_t rs = (1ull << mk.tile_shift) / RESCAN_THREADS;  // bytes per thread
+    const uint64_t ss = (tile << mk.tile_shift) + (uint64_t)threadIdx.x * rs;
+    const uint64_t se = ss + rs < n_bytes ? ss + rs : n_bytes;
+    uint64_t mine = 0, total = 0;
+    for (int pass = 0; pass < (WRITE ? 2 : 1); pass++) {
+        uint64_t h = 0, w = 0;
+        if (pass == 1) w = base + block_excl_sum<RESCAN_THREADS>(mine, s_scan, nullptr);
+        if (ss < n_bytes) {
+            for (uint64_t p = ss >= 64 ? ss - 64 : 0; p < se; p++) {
+                h = (h << 1) + s_gear[data[p]];
+                if (p < ss) continue;
+                const bool S = (h & mk.mask_s) == 0, L = (h & mk.mask_l) == 0;
+                if (S || L) {
+                    if (pass == 0) mine++;
+                    else if (w < cap) cand[w++] = p | (S ? BW_CAND_S : 0) | (L ? BW_CAND_L : 0);
+                }
+            }
+        }
+    }
+    if (!WRITE) block_excl_sum<RESCAN_THREADS>(mine, s_scan, &total);
+    __syncthreads();
+    return total;
+}
+
+// The overflowed tiles in [t0, t1), each by the whole block (WRITE as in rescan_tile).  The list
+// is short (empty on random data at backuwup's parameters): every block reads all of it.
+template <bool WRITE>
+__device__ void rescan_range(const uint8_t* __restrict__ data, uint64_t n_bytes, const Masks& mk,
+                             const uint32_t* __restrict__ ovf, uint64_t novf, uint64_t t0, uint64_t t1,
+                             uint32_t* __restrict__ tile_count, const uint64_t* __restrict__ off,
+                             uint64_t* __restrict__ cand, uint64_t cap, uint64_t* s_gear, uint64_t* s_scan) {
+    bool loaded = false;
+    for (uint64_t k = 0; k < novf; k++) {
+        const uint64_t tile = ovf[k];
+        if (tile < t0 || tile >= t1) continue;
+        if (!loaded) {
+            for (int i = threadIdx.x; i < 256; i += blockDim.x) s_gear[i] = c_gear[i];
+            __syncthreads();
+            loaded = true;
+        }
+        const uint64_t total = rescan_tile<WRITE>(data, n_bytes, mk, tile, WRITE ? off[tile] : 0, cand, cap, s_gear,
+                                                  s_scan);
+        if (!WRITE && threadIdx.x == 0) tile_count[tile] = (uint32_t)total | TILE_OVF;
+    }
+    __syncthreads();
+}
+
+// Candidate offsets: a scan over the per-tile counts (tiles are 128 KiB, so a 16 GiB batch has
+// 131072 of them): block-local scans of 1024 counts, the last block over the block totals, then
+// compaction adds the block base and copies the slots.
 constexpr int TS_BLOCK = 256;  // threads per block, 4 counts each
 
-__global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint32_t* __restrict__ cnt, uint64_t n,
-                                                           uint64_t* __restrict__ off, uint64_t* __restrict__ btot,
-                                                           uint64_t cap, uint64_t* ctr) {
+__global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint8_t* __restrict__ data, uint64_t n_bytes, Masks mk,
+                                                           const uint32_t* __restrict__ ovf, uint32_t* __restrict__ cnt,
+                                                           uint64_t n, uint64_t* __restrict__ off,
+                                                           uint64_t* __restrict__ btot, uint64_t cap, uint64_t* ctr) {
     __shared__ uint64_t s[TS_BLOCK];
+    __shared__ uint64_t s_gear[256];
+    // exact counts of this block's overflowed tiles first (what a separate k_rescan<false> did)
+    const uint64_t novf = ctr[C_NOVF];
+    if (novf) {
+        const uint64_t t0 = (uint64_t)blockIdx.x * 4 * TS_BLOCK, t1 = t0 + 4 * TS_BLOCK;
+        rescan_range<false>(data, n_bytes, mk, ovf, novf, t0, t1 < n ? t1 : n, cnt, nullptr, nullptr, 0, s_gear, s);
+    }
     const uint64_t i0 = ((uint64_t)blockIdx.x * TS_BLOCK + threadIdx.x) * 4;
     uint32_t c[4] = {0, 0, 0, 0};
     if (i0 + 4 <= n) {
@@ -420,64 +485,31 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint32_t* __res
 // bytes at and beyond that position themselves (walk_next), so an undersized array never changes
 // a boundary and a batch never has to be re-run (which would break the dedup order of a shared
 // index).
-__global__ void k_compact(const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ slots,
-                          uint64_t* __restrict__ off, const uint64_t* __restrict__ bbase, uint64_t n_tiles,
-                          uint64_t* __restrict__ cand, uint64_t cap, uint32_t tile_shift, uint64_t* ctr) {
+__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ data, uint64_t n_bytes, Masks mk,
+                                                 const uint32_t* __restrict__ ovf, const uint32_t* __restrict__ cnt,
+                                                 const uint64_t* __restrict__ slots, uint64_t* __restrict__ off,
+                                                 const uint64_t* __restrict__ bbase, uint64_t n_tiles,
+                                                 uint64_t* __restrict__ cand, uint64_t cap, uint64_t* ctr) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_tiles) return;
-    const uint64_t o = off[t] + bbase[t / (4 * TS_BLOCK)];
-    off[t] = o;  // final offset: the walkers start their candidate cursor here
-    const uint32_t c = cnt[t];
-    if (o + (c & ~TILE_OVF) > cap) atomicMin((unsigned long long*)&ctr[C_TRUNC], (unsigned long long)(t << tile_shift));
-    if (!(c & TILE_OVF)) {  // overflowed tiles are written by k_rescan<true>
-        for (uint32_t i = 0; i < c; i++)
-            if (o + i < cap) cand[o + i] = slots[t * SCAN_CAP + i];
+    if (t < n_tiles) {
+        const uint64_t o = off[t] + bbase[t / (4 * TS_BLOCK)];
+        off[t] = o;  // final offset: the walkers start their candidate cursor here
+        const uint32_t c = cnt[t];
+        if (o + (c & ~TILE_OVF) > cap)
+            atomicMin((unsigned long long*)&ctr[C_TRUNC], (unsigned long long)(t << mk.tile_shift));
+        if (!(c & TILE_OVF)) {  // overflowed tiles are written by the block below
+            for (uint32_t i = 0; i < c; i++)
+                if (o + i < cap) cand[o + i] = slots[t * SCAN_CAP + i];
+        }
     }
-}
-
-// Exact ordered re-scan of the tiles on the overflow list (candidate-dense data or small
-// parameters): WRITE = false counts a tile's candidates before the offset scan (tile_count =
-// count | TILE_OVF), WRITE = true stores them at the tile's offset after it.
-constexpr int RESCAN_THREADS = 256;
-
-template <bool WRITE>
-__global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __restrict__ data, uint64_t n_bytes,
-                                                           Masks mk, const uint32_t* __restrict__ ovf,
-                                                           const uint64_t* __restrict__ off,
-                                                           uint64_t* __restrict__ cand, uint64_t cap,
-                                                           uint32_t* __restrict__ tile_count, const uint64_t* ctr) {
-    __shared__ uint64_t s_gear[256];
-    __shared__ uint64_t s_scan[RESCAN_THREADS];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_gear[i] = c_gear[i];
-    __syncthreads();
+    // this block's overflowed tiles, at their final offsets (what a separate k_rescan<true> did)
     const uint64_t novf = ctr[C_NOVF];
-    for (uint64_t k = blockIdx.x; k < novf; k += gridDim.x) {
-        const uint64_t tile = ovf[k];
-        const uint64_t rs = (1ull << mk.tile_shift) / RESCAN_THREADS;  // bytes per thread
-        const uint64_t ss = (tile << mk.tile_shift) + (uint64_t)threadIdx.x * rs;
-        const uint64_t se = ss + rs < n_bytes ? ss + rs : n_bytes;
-        uint64_t mine = 0;
-        for (int pass = 0; pass < (WRITE ? 2 : 1); pass++) {
-            uint64_t h = 0, w = 0;
-            if (pass == 1) w = off[tile] + block_excl_sum<RESCAN_THREADS>(mine, s_scan, nullptr);
-            if (ss < n_bytes) {
-                for (uint64_t p = ss >= 64 ? ss - 64 : 0; p < se; p++) {
-                    h = (h << 1) + s_gear[data[p]];
-                    if (p < ss) continue;
-                    const bool S = (h & mk.mask_s) == 0, L = (h & mk.mask_l) == 0;
-                    if (S || L) {
-                        if (pass == 0) mine++;
-                        else if (w < cap) cand[w++] = p | (S ? BW_CAND_S : 0) | (L ? BW_CAND_L : 0);
-                    }
-                }
-            }
-        }
-        if (!WRITE) {
-            uint64_t total;
-            block_excl_sum<RESCAN_THREADS>(mine, s_scan, &total);
-            if (threadIdx.x == 0) tile_count[tile] = (uint32_t)total | TILE_OVF;
-        }
-        __syncthreads();
+    if (novf) {
+        __shared__ uint64_t s_gear[256], s_scan[RESCAN_THREADS];
+        __syncthreads();  // the block's final offsets are written
+        const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x, t1 = t0 + blockDim.x;
+        rescan_range<true>(data, n_bytes, mk, ovf, novf, t0, t1 < n_tiles ? t1 : n_tiles, nullptr, off, cand, cap,
+                           s_gear, s_scan);
     }
 }
 
@@ -486,14 +518,10 @@ void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint6
                     uint64_t cand_cap, uint32_t* ovf_list, uint64_t* ctr, uint64_t* btot) {
     if (!n_tiles) return;
     const uint64_t nb = (n_tiles + 4 * TS_BLOCK - 1) / (4 * TS_BLOCK);
-    hipLaunchKernelGGL(k_rescan<false>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
-                       cand, cand_cap, tile_count, ctr);
-    hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, tile_count, n_tiles, tile_off, btot,
-                       cand_cap, ctr);
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, tile_count, tile_slots,
-                       tile_off, btot, n_tiles, cand, cand_cap, mk.tile_shift, ctr);
-    hipLaunchKernelGGL(k_rescan<true>, dim3(64), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_off,
-                       cand, cand_cap, tile_count, ctr);
+    hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, data, n_bytes, mk, ovf_list,
+                       tile_count, n_tiles, tile_off, btot, cand_cap, ctr);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, data, n_bytes, mk, ovf_list,
+                       tile_count, tile_slots, tile_off, btot, n_tiles, cand, cand_cap, ctr);
 }
 
 // ======================================================================== the boundary walker
@@ -782,12 +810,36 @@ __device__ __forceinline__ uint64_t groups_of(uint64_t len) {
     return (leaves + 3) / 4;
 }
 
-// Emit (or just count) the blobs of unit u.  Returns blob and group counts.
+// Chunk.hash of the CDC chunk [s, s + len) of a file ending at fe, by one thread (the serial form
+// of a 64-lane wave sum): the crate returns h_p (odd p) or h_p << 1 (even p, the two-byte loop
+// keeps the even half-step shifted), h of the last tested position when no position cut, and 0
+// for a tail of <= min bytes.  At most 64 terms.
+__device__ uint64_t cut_hash_serial(const uint8_t* __restrict__ data, const Masks& mk, uint64_t s, uint64_t len,
+                                    uint64_t fe) {
+    const uint64_t rem = fe - s;
+    if (rem <= mk.min) return 0;
+    const uint64_t remaining = rem > mk.max ? mk.max : rem;
+    const uint64_t r2 = remaining & ~1ull;
+    uint64_t p;
+    if (len == remaining) {
+        if (r2 <= mk.s0) return 0;
+        p = r2 - 1;
+    } else {
+        p = len;
+    }
+    uint64_t out = 0;
+    for (uint64_t j = 0; j < 64 && j <= p && p - j >= mk.s0; j++) out += c_gear[data[s + p - j]] << j;
+    return (p & 1) == 0 ? out << 1 : out;
+}
+
+// Emit (or just count) the blobs of unit u.  Returns blob and group counts.  Emitting also writes
+// each CDC chunk's Chunk.hash (data and mk are used only then).
 template <bool WRITE>
 __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDesc* cfiles, const uint64_t* chains,
                            const uint32_t* chain_n, const uint64_t* seg_M, const uint32_t* cf_invalid,
                            const uint64_t* fb_starts, const uint64_t* fb_count, BlobArrays b, uint64_t bbase,
-                           uint64_t gbase, uint64_t& nb, uint64_t& ng) {
+                           uint64_t gbase, uint64_t& nb, uint64_t& ng, const uint8_t* data = nullptr,
+                           const Masks* mk = nullptr) {
     nb = 0;
     ng = 0;
     auto emit = [&](uint64_t start, uint64_t end, uint32_t kind, uint64_t fend) {
@@ -802,6 +854,7 @@ __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDe
             b.file[k] = u.file;
             b.kind[k] = kind;
             b.fend[k] = fend;
+            b.ghash[k] = kind ? cut_hash_serial(data, *mk, start, len, fend) : 0;
         }
         nb++;
         ng += groups_of(len);
@@ -895,63 +948,27 @@ __global__ __launch_bounds__(256) void k_unit_emit(const UnitDesc* __restrict__ 
                                                    const uint64_t* __restrict__ fb_count, BlobArrays b,
                                                    const uint64_t* __restrict__ ucb, const uint64_t* __restrict__ ucg,
                                                    const uint64_t* __restrict__ bt_b,
-                                                   const uint64_t* __restrict__ bt_g) {
+                                                   const uint64_t* __restrict__ bt_g,
+                                                   const uint8_t* __restrict__ data, Masks mk) {
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nunits) return;
     const uint64_t bb = ucb[u] + bt_b[u / AS_UNITS], gb = ucg[u] + bt_g[u / AS_UNITS];
     uint64_t nb, ng;
     unit_blobs<true>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, bb, gb, nb,
-                     ng);
+                     ng, data, &mk);
 }
 
 void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint64_t nunits, const SegDesc* segs,
                      const CFileDesc* cfiles, const uint64_t* chains, const uint32_t* chain_n, const uint64_t* seg_M,
                      const uint32_t* cf_invalid, const uint64_t* fb_starts, const uint64_t* fb_count, BlobArrays b,
-                     uint64_t* ucnt, uint64_t* ubtot) {
+                     uint64_t* ucnt, uint64_t* ubtot, const uint8_t* data, const Masks& mk) {
     const uint64_t nblk = (nunits + AS_UNITS - 1) / AS_UNITS;
     uint64_t *ucb = ucnt, *ucg = ucnt + nunits, *bt_b = ubtot, *bt_g = ubtot + nblk + 1;
     if (!nunits) return;  // ctr's blob and group counts stay 0 (zeroed at submit)
     hipLaunchKernelGGL(k_unit_count, dim3((unsigned)nblk), dim3(AS_BLOCK), 0, st, units, nunits, segs, cfiles, chains,
                        chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g, ctr);
     hipLaunchKernelGGL(k_unit_emit, dim3((unsigned)((nunits + 255) / 256)), dim3(256), 0, st, units, nunits, segs,
-                       cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g);
-}
-
-// ======================================================================== Chunk.hash
-
-// The crate returns its running gear state with the cut: h_p (odd p) or h_p << 1 (even p, the
-// two-byte loop keeps the even half-step shifted), h of the last tested position when no
-// position cut, and 0 for a tail of <= min bytes.  One wave per CDC chunk, <= 64 terms.
-__global__ __launch_bounds__(256) void k_cut_hash(const uint8_t* __restrict__ data, Masks mk,
-                                                  const uint64_t* ctr, BlobArrays b) {
-    const uint64_t k = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
-    if (k >= ctr[C_NBLOBS]) return;
-    const int lane = bw_lane();
-    if (b.kind[k] == 0) { if (lane == 0) b.ghash[k] = 0; return; }
-    const uint64_t s = b.start[k], len = b.len[k], fe = b.fend[k];
-    const uint64_t rem = fe - s;
-    uint64_t out = 0;
-    if (rem > mk.min) {
-        const uint64_t remaining = rem > mk.max ? mk.max : rem;
-        const uint64_t r2 = remaining & ~1ull;
-        uint64_t p = BW_NONE;
-        if (len == remaining) { if (r2 > mk.s0) p = r2 - 1; }
-        else p = len;
-        if (p != BW_NONE) {
-            const uint64_t q = p - (uint64_t)lane;
-            uint64_t term = 0;
-            if ((uint64_t)lane <= p && q >= mk.s0) term = c_gear[data[s + q]] << lane;
-            out = bw_wave_sum64(term);
-            if ((p & 1) == 0) out <<= 1;
-        }
-    }
-    if (lane == 0) b.ghash[k] = out;
-}
-
-void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* ctr, BlobArrays b,
-                     uint64_t max_blobs) {
-    if (!max_blobs) return;
-    hipLaunchKernelGGL(k_cut_hash, dim3((unsigned)((max_blobs + 3) / 4)), dim3(256), 0, st, data, mk, ctr, b);
+                       cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g, data, mk);
 }
 
 }  // namespace bw

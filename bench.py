@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--scan-waves", type=int, default=None, choices=[8, 16], help="BW_OPT_SCAN_WAVES")
     ap.add_argument("--latency-stream", type=int, default=None, choices=[0, 1], help="BW_OPT_LATENCY_STREAM")
     ap.add_argument("--order-hash", type=int, default=None, choices=[0, 1], help="BW_OPT_ORDER_HASH")
+    ap.add_argument("--split", type=int, default=None, choices=[1, 2],
+                    help="BW_OPT_SPLIT: 2 = multi-file batches of 64 MiB-4 GiB as a head and a tail part on two streams")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
@@ -180,7 +182,7 @@ def main():
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
     from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
-                                   BW_OPT_SCAN_WAVES, STAGES)
+                                   BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -228,6 +230,8 @@ def main():
             c.set_option(BW_OPT_LATENCY_STREAM, args.latency_stream)
         if args.order_hash is not None:
             c.set_option(BW_OPT_ORDER_HASH, args.order_hash)
+        if args.split is not None:
+            c.set_option(BW_OPT_SPLIT, args.split)
         if args.host_stream and nctx > 1:
             c.set_option(BW_OPT_DEPTH, 1)  # contexts alternate: one HBM input buffer each is enough
         ctxs.append(c)

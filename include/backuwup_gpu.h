@@ -167,12 +167,13 @@ enum {
                                     index run one at a time each, in submission order (a batch's scan
                                     then overlaps the previous batch's hashing); 0 (default): as soon
                                     as their inputs are ready */
-    BW_OPT_SPLIT = 11            /* 2 (default): a batch of >= 2 files between 64 MiB and 4 GiB that
-                                    gates through the index runs as two parts on two streams (head
-                                    files here, tail files on a helper context), scans and BLAKE3
-                                    passes in order, so one batch in flight keeps the scan beside
-                                    the hashing; 1: off.  bw_batch_views / bw_batch_device_views of a
-                                    split batch return BW_ESTATE (NO_DEDUP batches are never split) */
+    BW_OPT_SPLIT = 11            /* 2: a batch of >= 2 files between 64 MiB and 4 GiB that gates
+                                    through the index runs as two parts on two streams (head files
+                                    here, tail files on a helper context), scans and BLAKE3 passes in
+                                    order, meant to keep the scan beside the hashing with one batch
+                                    in flight; 1 (default): off -- measured slower (the tail's scan
+                                    waits for CUs held by the head's hashing).  bw_batch_views /
+                                    bw_batch_device_views of a split batch return BW_ESTATE */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 

@@ -80,8 +80,10 @@ def test_split_batches_match_unsplit(oracle):
     import torch
     from backuwup_amd._lib import BW_OPT_SPLIT
     data, offs, lens = tree_corpus(320 << 20, seed=91, max_file=40 << 20)
-    nf = len(lens)
-    bounds = [(0, nf // 3), (nf // 3, 2 * nf // 3), (2 * nf // 3, nf), (0, nf // 3)]
+    nf, cum = len(lens), np.cumsum(lens)
+    b1 = int(np.searchsorted(cum, cum[-1] / 3)) + 1
+    b2 = int(np.searchsorted(cum, 2 * cum[-1] / 3)) + 1
+    bounds = [(0, b1), (b1, b2), (b2, nf), (0, b1)]  # about a third of the bytes each
     batches = _slices(data, offs, lens, bounds)
     assert all(int(l.sum()) >= (64 << 20) and len(l) >= 2 for _, _, l in batches)
     want = oracle_session(oracle, batches)
