@@ -23,7 +23,7 @@
 //   k_resolve   prefix-max of merge points -> true chain entry of every segment, validity
 //   k_fallback  serial wave walker for files whose chains did not merge (exact, slower)
 //   k_unit_*    canonical-order blob table + BLAKE3 group offsets (count + scan, emit)
-//   k_unit_emit also writes each CDC chunk's Chunk.hash (the crate's returned gear state)
+//   k_cut_hash  Chunk.hash (the crate's returned gear state) for every CDC chunk
 #include "bw_device.h"
 #include "bw_internal.h"
 
@@ -810,36 +810,12 @@ __device__ __forceinline__ uint64_t groups_of(uint64_t len) {
     return (leaves + 3) / 4;
 }
 
-// Chunk.hash of the CDC chunk [s, s + len) of a file ending at fe, by one thread (the serial form
-// of a 64-lane wave sum): the crate returns h_p (odd p) or h_p << 1 (even p, the two-byte loop
-// keeps the even half-step shifted), h of the last tested position when no position cut, and 0
-// for a tail of <= min bytes.  At most 64 terms.
-__device__ uint64_t cut_hash_serial(const uint8_t* __restrict__ data, const Masks& mk, uint64_t s, uint64_t len,
-                                    uint64_t fe) {
-    const uint64_t rem = fe - s;
-    if (rem <= mk.min) return 0;
-    const uint64_t remaining = rem > mk.max ? mk.max : rem;
-    const uint64_t r2 = remaining & ~1ull;
-    uint64_t p;
-    if (len == remaining) {
-        if (r2 <= mk.s0) return 0;
-        p = r2 - 1;
-    } else {
-        p = len;
-    }
-    uint64_t out = 0;
-    for (uint64_t j = 0; j < 64 && j <= p && p - j >= mk.s0; j++) out += c_gear[data[s + p - j]] << j;
-    return (p & 1) == 0 ? out << 1 : out;
-}
-
-// Emit (or just count) the blobs of unit u.  Returns blob and group counts.  Emitting also writes
-// each CDC chunk's Chunk.hash (data and mk are used only then).
+// Emit (or just count) the blobs of unit u.  Returns blob and group counts.
 template <bool WRITE>
 __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDesc* cfiles, const uint64_t* chains,
                            const uint32_t* chain_n, const uint64_t* seg_M, const uint32_t* cf_invalid,
                            const uint64_t* fb_starts, const uint64_t* fb_count, BlobArrays b, uint64_t bbase,
-                           uint64_t gbase, uint64_t& nb, uint64_t& ng, const uint8_t* data = nullptr,
-                           const Masks* mk = nullptr) {
+                           uint64_t gbase, uint64_t& nb, uint64_t& ng) {
     nb = 0;
     ng = 0;
     auto emit = [&](uint64_t start, uint64_t end, uint32_t kind, uint64_t fend) {
@@ -854,7 +830,6 @@ __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDe
             b.file[k] = u.file;
             b.kind[k] = kind;
             b.fend[k] = fend;
-            b.ghash[k] = kind ? cut_hash_serial(data, *mk, start, len, fend) : 0;
         }
         nb++;
         ng += groups_of(len);
@@ -948,27 +923,63 @@ __global__ __launch_bounds__(256) void k_unit_emit(const UnitDesc* __restrict__ 
                                                    const uint64_t* __restrict__ fb_count, BlobArrays b,
                                                    const uint64_t* __restrict__ ucb, const uint64_t* __restrict__ ucg,
                                                    const uint64_t* __restrict__ bt_b,
-                                                   const uint64_t* __restrict__ bt_g,
-                                                   const uint8_t* __restrict__ data, Masks mk) {
+                                                   const uint64_t* __restrict__ bt_g) {
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nunits) return;
     const uint64_t bb = ucb[u] + bt_b[u / AS_UNITS], gb = ucg[u] + bt_g[u / AS_UNITS];
     uint64_t nb, ng;
     unit_blobs<true>(units[u], segs, cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, bb, gb, nb,
-                     ng, data, &mk);
+                     ng);
 }
 
 void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint64_t nunits, const SegDesc* segs,
                      const CFileDesc* cfiles, const uint64_t* chains, const uint32_t* chain_n, const uint64_t* seg_M,
                      const uint32_t* cf_invalid, const uint64_t* fb_starts, const uint64_t* fb_count, BlobArrays b,
-                     uint64_t* ucnt, uint64_t* ubtot, const uint8_t* data, const Masks& mk) {
+                     uint64_t* ucnt, uint64_t* ubtot) {
     const uint64_t nblk = (nunits + AS_UNITS - 1) / AS_UNITS;
     uint64_t *ucb = ucnt, *ucg = ucnt + nunits, *bt_b = ubtot, *bt_g = ubtot + nblk + 1;
     if (!nunits) return;  // ctr's blob and group counts stay 0 (zeroed at submit)
     hipLaunchKernelGGL(k_unit_count, dim3((unsigned)nblk), dim3(AS_BLOCK), 0, st, units, nunits, segs, cfiles, chains,
                        chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g, ctr);
     hipLaunchKernelGGL(k_unit_emit, dim3((unsigned)((nunits + 255) / 256)), dim3(256), 0, st, units, nunits, segs,
-                       cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g, data, mk);
+                       cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g);
+}
+
+// ======================================================================== Chunk.hash
+
+// The crate returns its running gear state with the cut: h_p (odd p) or h_p << 1 (even p, the
+// two-byte loop keeps the even half-step shifted), h of the last tested position when no
+// position cut, and 0 for a tail of <= min bytes.  One wave per CDC chunk, <= 64 terms.
+__global__ __launch_bounds__(256) void k_cut_hash(const uint8_t* __restrict__ data, Masks mk,
+                                                  const uint64_t* ctr, BlobArrays b) {
+    const uint64_t k = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    if (k >= ctr[C_NBLOBS]) return;
+    const int lane = bw_lane();
+    if (b.kind[k] == 0) { if (lane == 0) b.ghash[k] = 0; return; }
+    const uint64_t s = b.start[k], len = b.len[k], fe = b.fend[k];
+    const uint64_t rem = fe - s;
+    uint64_t out = 0;
+    if (rem > mk.min) {
+        const uint64_t remaining = rem > mk.max ? mk.max : rem;
+        const uint64_t r2 = remaining & ~1ull;
+        uint64_t p = BW_NONE;
+        if (len == remaining) { if (r2 > mk.s0) p = r2 - 1; }
+        else p = len;
+        if (p != BW_NONE) {
+            const uint64_t q = p - (uint64_t)lane;
+            uint64_t term = 0;
+            if ((uint64_t)lane <= p && q >= mk.s0) term = c_gear[data[s + q]] << lane;
+            out = bw_wave_sum64(term);
+            if ((p & 1) == 0) out <<= 1;
+        }
+    }
+    if (lane == 0) b.ghash[k] = out;
+}
+
+void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* ctr, BlobArrays b,
+                     uint64_t max_blobs) {
+    if (!max_blobs) return;
+    hipLaunchKernelGGL(k_cut_hash, dim3((unsigned)((max_blobs + 3) / 4)), dim3(256), 0, st, data, mk, ctr, b);
 }
 
 }  // namespace bw

@@ -122,8 +122,9 @@ void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint6
                      const SegDesc* segs, const CFileDesc* cfiles, const uint64_t* chains,
                      const uint32_t* chain_n, const uint64_t* seg_M, const uint32_t* cf_invalid,
                      const uint64_t* fb_starts, const uint64_t* fb_count, BlobArrays b,
-                     uint64_t* ucnt /* 2 * nunits */, uint64_t* ubtot /* 2 * (nunits / 256 + 2) */,
-                     const uint8_t* data, const Masks& mk);
+                     uint64_t* ucnt /* 2 * nunits */, uint64_t* ubtot /* 2 * (nunits / 256 + 2) */);
+void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* ctr,
+                     BlobArrays b, uint64_t max_blobs);
 
 
 // ------------------------------------------------------------------ launchers (bw_blake3.hip)
