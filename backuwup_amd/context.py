@@ -550,6 +550,13 @@ class Context:
         check(self._L.bw_profile_read(self.h, ms, ctypes.byref(n)), self.h)
         return {s: ms[i] for i, s in enumerate(_lib.STAGES)}, n.value
 
+    def calibrate_b3(self, ms=100.0):
+        """The BLAKE3 leaf pass's compression from registers on every CU for about `ms` ms:
+        {gbs, ghz, bytes_per_clk_cu, launch_ms} -- the pass's integer-issue ceiling on this chip."""
+        out = (ctypes.c_double * 4)()
+        check(self._L.bw_calibrate_b3(self.h, float(ms), out), self.h)
+        return {"gbs": out[0], "ghz": out[1], "bytes_per_clk_cu": out[2], "launch_ms": out[3]}
+
     # -------------------------------------------------------------- multi-GPU helpers (device pointers)
     def partition_by_owner(self, d_digests, n, n_owners, d_out, d_perm):
         counts = np.zeros(n_owners, dtype=np.uint64)

@@ -586,6 +586,42 @@ __global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArray
     }
 }
 
+#ifndef BW_B3_LINES_MINW
+#define BW_B3_LINES_MINW 3  // blocks of 256 per CU: 3 = 3 waves per SIMD (168 VGPRs; at 4 the ring spills)
+#endif
+
+// Roofline calibration: the leaf pass's compression (b3_compress, the same instruction forms)
+// from registers, no memory traffic, at the leaf pass's occupancy.  Wave 0 of every block stamps
+// shader cycles (s_memtime) and 100 MHz real time (s_memrealtime), so the bytes per shader clock
+// do not depend on the DVFS state the run happens to meet.
+__global__ __launch_bounds__(256, BW_B3_LINES_MINW) void k_b3_calib(uint32_t blocks_per_lane, uint32_t* sink,
+                                                                    uint64_t* stamps) {
+    uint32_t cv[8], m[16];
+    b3_iv(cv);
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = threadIdx.x * 16 + i + blockIdx.x;
+    uint64_t t0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (uint32_t k = 0; k < blocks_per_lane; k++) {
+        m[0] ^= k;
+        b3_compress(cv, m, 64, k, 0);
+    }
+    if (threadIdx.x == 0) {
+        stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
+        stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
+    if (cv[0] == 0x9e3779b9u && cv[1] == 0x7f4a7c15u) sink[0] = cv[2];  // keeps the chain live
+}
+
+void launch_b3_calib(hipStream_t st, uint32_t n_blocks, uint32_t blocks_per_lane, uint32_t* sink, uint64_t* stamps) {
+    hipLaunchKernelGGL(k_b3_calib, dim3(n_blocks), dim3(256), 0, st, blocks_per_lane, sink, stamps);
+}
+
+uint32_t b3_calib_blocks_per_cu() { return BW_B3_LINES_MINW; }
+
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
                    uint64_t max_groups, uint32_t* cv_buf, uint32_t* cv_tmp, uint8_t* digests, int max_leaves,
                    hipEvent_t between, int loads, hipStream_t upper, hipEvent_t leaf_done) {
@@ -595,9 +631,6 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     }
 #ifndef BW_B3_DYN_LDS
 #define BW_B3_DYN_LDS 0  // A/B: extra LDS per block caps the blocks per CU (occupancy experiments)
-#endif
-#ifndef BW_B3_LINES_MINW
-#define BW_B3_LINES_MINW 3  // blocks of 256 per CU: 3 = 3 waves per SIMD (168 VGPRs; at 4 the ring spills)
 #endif
     if (loads == B3_LOADS_LINES)
         hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data, ctr, b,

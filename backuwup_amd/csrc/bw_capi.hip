@@ -85,6 +85,7 @@ struct bw_index {
     uint64_t enq_total = 0;  // sum of the upper bounds of every append ever enqueued
     hipEvent_t tail = nullptr;
     bool tail_set = false;
+    hipStream_t tail_stream = nullptr;  // the stream `tail` was last recorded on
     // With BW_OPT_ORDER_HASH, the scans and the BLAKE3 leaf passes of the contexts attached here
     // run one at a time each, in submission order, so a batch's scan shares the GPU with the
     // previous batch's hashing rather than two hashing passes sharing it while the scans wait.
@@ -185,6 +186,8 @@ struct bw_ctx {
 
     // stage timing: two event sets, alternated per batch so recording never waits on the GPU
     bool prof = false;
+    uint32_t prof_mask = (1u << BW_N_STAGES) - 1;  // stages whose start is marked (BW_OPT_PROFILE_MASK)
+    int scan_first = 2;                             // BW_OPT_SCAN_FIRST
     hipEvent_t ev[2][BW_N_STAGES + 1] = {};
     bool ev_pending[2] = {false, false};
     int ev_set = 0;
@@ -283,19 +286,28 @@ static uint64_t seg_len_for(const Masks& mk) {
 
 // ------------------------------------------------------------------ stage timing
 
+// Stage i's time runs from its mark to the next recorded one (prof_mask: the marks recorded; the
+// batch-end mark BW_N_STAGES always is).  Every event recorded between two kernels costs the
+// stream ~5.5 us of idle time (profiles/r03: k_scan -> k_tile_partial with a mark between them
+// 5.7 us, kernels without one 0), so the bench's timed region marks only its dominant kernels.
 static void prof_collect(bw_ctx* c, int set) {
     if (!c->ev_pending[set]) return;
     hipEventSynchronize(c->ev[set][BW_N_STAGES]);
+    const uint32_t mask = c->prof_mask | (1u << BW_N_STAGES);
     for (int i = 0; i < BW_N_STAGES; i++) {
+        if (!((mask >> i) & 1)) continue;
+        int j = i + 1;
+        while (!((mask >> j) & 1)) j++;
         float ms = 0;
-        if (hipEventElapsedTime(&ms, c->ev[set][i], c->ev[set][i + 1]) == hipSuccess) c->stage_ms[i] += ms;
+        if (hipEventElapsedTime(&ms, c->ev[set][i], c->ev[set][j]) == hipSuccess) c->stage_ms[i] += ms;
     }
     c->prof_batches++;
     c->ev_pending[set] = false;
 }
 
 static void prof_mark(bw_ctx* c, int stage, hipStream_t st = nullptr) {
-    if (c->prof) hipEventRecord(c->ev[c->ev_set][stage], st ? st : c->stream);
+    if (c->prof && (stage == BW_N_STAGES || ((c->prof_mask >> stage) & 1)))
+        hipEventRecord(c->ev[c->ev_set][stage], st ? st : c->stream);
 }
 
 // ------------------------------------------------------------------ the index object
@@ -336,11 +348,14 @@ struct IndexOp {
     std::lock_guard<std::mutex> lk;
     explicit IndexOp(bw_ctx* cc, hipStream_t s = nullptr)
         : c(cc), x(cc->idx), st(s ? s : cc->stream), lk(cc->idx->mu) {
-        if (x->tail_set) hipStreamWaitEvent(st, x->tail, 0);
+        // the previous operation on this same stream is ordered already (and a wait costs the
+        // stream an idle gap like any event operation)
+        if (x->tail_set && x->tail_stream != st) hipStreamWaitEvent(st, x->tail, 0);
     }
     ~IndexOp() {
         hipEventRecord(x->tail, st);
         x->tail_set = true;
+        x->tail_stream = st;
     }
 };
 
@@ -648,6 +663,14 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             if (v > B3_LOADS_LINES) return BW_EINVAL;
             c->b3_loads = (int)v;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
+        case BW_OPT_PROFILE_MASK:
+            if (v == 0 || v >= (1u << BW_N_STAGES)) return BW_EINVAL;
+            c->prof_mask = (uint32_t)v;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
+        case BW_OPT_SCAN_FIRST:
+            if (v > 2) return BW_EINVAL;
+            c->scan_first = (int)v;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_STAGE_CHUNK:
             if (v < 4096) return BW_EINVAL;
             hipSetDevice(c->device);
@@ -825,6 +848,41 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         rc0 |= ensure(c, s.ctr, C_COUNT * 8);
         if (rc0) return BW_ENOMEM;
     }
+    // ---- the gear scan: counters zeroed, then the scan; it reads only the batch bytes and the
+    // tile buffers above
+    auto enqueue_scan = [&]() -> int {
+        HIPCHK(c, hipMemsetAsync(s.ctr.p, 0, C_COUNT * 8, c->stream));
+        if (c->prof) {
+            c->ev_set ^= 1;
+            prof_collect(c, c->ev_set);  // the set about to be reused belongs to batch k-2
+        }
+        prof_mark(c, BW_STAGE_SCAN);
+        if (!ncf_pre) return BW_OK;
+        bw_index* x = c->idx;
+        std::unique_lock<std::mutex> lk(x->mu, std::defer_lock);
+        if (c->order_hash || order_force) {
+            lk.lock();
+            if (x->scan_tail_set) HIPCHK(c, hipStreamWaitEvent(c->stream, x->scan_tail, 0));
+        }
+        if (!launch_scan(c->stream, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count),
+                         P<uint64_t>(c->tile_slots), P<uint32_t>(c->ovf), P<uint64_t>(s.ctr), c->scan_waves)) {
+            c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
+            return BW_EINVAL;
+        }
+        if (c->order_hash || order_force) {
+            HIPCHK(c, hipEventRecord(x->scan_tail, c->stream));
+            x->scan_tail_set = true;
+        }
+        return BW_OK;
+    };
+    // Small batches enqueue it before the host tables, so the GPU starts while the host builds
+    // them (one batch in flight: the host's share of a 1 GiB batch sits on the critical path).
+    // Large ones keep it behind the upload: enqueued first, it made C3's two contexts fall into a
+    // slower phase in one run of two (1,647 vs 1,871 GB/s; profiles/r02/s31_reorder).
+    const bool scan_first = c->scan_first == 2 ? data_len < c->scan_small_bytes : c->scan_first == 1;
+    if (scan_first)
+        if (int r6 = enqueue_scan()) return r6;
+
     // ---- host metadata: CDC files, segments, canonical units
     const uint64_t L = seg_len_for(mk);
     // every chunk but a file's last is >= min(2*(min/2), max) bytes (max < min is legal in the crate)
@@ -993,34 +1051,10 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     s.meta_pending = true;
     phase(2);
 
-    // The gear scan is enqueued after the metadata upload, not before the host builds the tables:
-    // enqueued first, it made C3's two contexts fall into a slower phase in one run of two (1,647
-    // vs 1,871 GB/s; 1,859-1,864 this way) for no measurable gain elsewhere (profiles/r02/s31_reorder).
-    HIPCHK(c, hipMemsetAsync(s.ctr.p, 0, C_COUNT * 8, c->stream));
-    if (c->prof) {
-        c->ev_set ^= 1;
-        prof_collect(c, c->ev_set);  // the set about to be reused belongs to batch k-2
-    }
-    prof_mark(c, BW_STAGE_SCAN);
+    if (!scan_first)
+        if (int r6 = enqueue_scan()) return r6;
     uint64_t* ctr = P<uint64_t>(s.ctr);
     hipStream_t st = c->stream;
-    if (ncf_pre) {
-        bw_index* x = c->idx;
-        std::unique_lock<std::mutex> lk(x->mu, std::defer_lock);
-        if (c->order_hash || order_force) {
-            lk.lock();
-            if (x->scan_tail_set) HIPCHK(c, hipStreamWaitEvent(st, x->scan_tail, 0));
-        }
-        if (!launch_scan(st, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count), P<uint64_t>(c->tile_slots),
-                         P<uint32_t>(c->ovf), ctr, c->scan_waves)) {
-            c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
-            return BW_EINVAL;
-        }
-        if (c->order_hash || order_force) {
-            HIPCHK(c, hipEventRecord(x->scan_tail, st));
-            x->scan_tail_set = true;
-        }
-    }
 
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len};
@@ -1083,7 +1117,9 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         }
         HIPCHK(c, hipMemsetAsync(s.digests.p, 0, max_blobs * 32, lat));
     }
-    HIPCHK(c, hipEventRecord(s.input_free, st));  // no kernel of this batch reads d_data after here
+    // no kernel of this batch reads d_data after here; only the slot's own input buffer (host
+    // batches, stream_in) is ever refilled behind this event
+    if (d_data == P<uint8_t>(s.input)) HIPCHK(c, hipEventRecord(s.input_free, st));
     phase(3);
     prof_mark(c, BW_STAGE_DEDUP, lat);
     if (do_dedup) {
@@ -1193,7 +1229,7 @@ static int submit_split(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data
     // is free only after the tail's BLAKE3 read it too)
     HIPCHK(c, hipEventRecord(c->e_tail, h->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->e_tail, 0));
-    HIPCHK(c, hipEventRecord(s.input_free, c->stream));
+    if (d_data == P<uint8_t>(s.input)) HIPCHK(c, hipEventRecord(s.input_free, c->stream));
     s.tail_ticket = t2;
     s.tail_file0 = f0;
     return BW_OK;
@@ -1654,6 +1690,64 @@ extern "C" int bw_profile_read(bw_ctx* c, double* stage_ms, uint64_t* n_batches)
     if (stage_ms)
         for (int i = 0; i < BW_N_STAGES; i++) stage_ms[i] = c->stage_ms[i] + (c->helper ? c->helper->stage_ms[i] : 0);
     if (n_batches) *n_batches = c->prof_batches;
+    return BW_OK;
+}
+
+extern "C" int bw_calibrate_b3(bw_ctx* c, double ms, double out[4]) {
+    if (!c || !out || !(ms > 0) || ms > 10000) return BW_EINVAL;
+    hipSetDevice(c->device);
+    int n_cu = 0;
+    HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    if (n_cu <= 0) return BW_ESTATE;
+    const uint32_t nblk = (uint32_t)n_cu * b3_calib_blocks_per_cu();
+    DevBuf stamps, sink;
+    auto release = [&] {
+        free_dev(stamps);
+        free_dev(sink);
+    };
+    if (ensure(c, stamps, (size_t)nblk * 16) || ensure(c, sink, 64)) {
+        release();
+        return BW_ENOMEM;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto fail = [&](hipError_t e) {
+        c->err = std::string("calibration: ") + hipGetErrorString(e);
+        if (e0) hipEventDestroy(e0);
+        if (e1) hipEventDestroy(e1);
+        release();
+        return BW_EHIP;
+    };
+    hipError_t e;
+    if ((e = hipEventCreate(&e0)) || (e = hipEventCreate(&e1))) return fail(e);
+    // a short probe sizes the run: blocks per lane so that one launch lasts about `ms`
+    uint32_t bpl = 256;
+    float t = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        hipEventRecord(e0, c->stream);
+        launch_b3_calib(c->stream, nblk, bpl, P<uint32_t>(sink), P<uint64_t>(stamps));
+        hipEventRecord(e1, c->stream);
+        if ((e = hipEventSynchronize(e1)) || (e = hipEventElapsedTime(&t, e0, e1))) return fail(e);
+        if (pass == 0) {
+            const double scale = ms / std::max(1e-3, (double)t);
+            bpl = (uint32_t)std::min(1e8, std::max(256.0, bpl * scale));
+        }
+    }
+    std::vector<uint64_t> h((size_t)nblk * 2);
+    if ((e = hipMemcpy(h.data(), stamps.p, h.size() * 8, hipMemcpyDeviceToHost))) return fail(e);
+    double cyc = 0, ticks = 0;
+    for (uint32_t i = 0; i < nblk; i++) {
+        cyc += (double)h[2 * i];
+        ticks += (double)h[2 * i + 1];
+    }
+    const double bytes = (double)nblk * 256 * bpl * 64;
+    const double ghz = ticks > 0 ? cyc / ticks * 0.1 : 0;  // s_memrealtime counts at 100 MHz
+    out[0] = t > 0 ? bytes / (t * 1e-3) / 1e9 : 0;
+    out[1] = ghz;
+    out[2] = ghz > 0 && t > 0 ? out[0] / ghz / n_cu : 0;  // bytes per shader clock per CU
+    out[3] = t;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    release();
     return BW_OK;
 }
 

@@ -137,6 +137,10 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
                    hipEvent_t between /* may be null */, int loads,
                    hipStream_t upper /* stream of the upper tree levels; `between` must order it */,
                    hipEvent_t leaf_done = nullptr /* recorded on st right after the leaf pass */);
+// The leaf pass's compression from registers (roofline calibration): n_blocks blocks of 256,
+// stamps[2 * block] = shader cycles, stamps[2 * block + 1] = 100 MHz ticks of wave 0.
+void launch_b3_calib(hipStream_t st, uint32_t n_blocks, uint32_t blocks_per_lane, uint32_t* sink, uint64_t* stamps);
+uint32_t b3_calib_blocks_per_cu();  // the leaf pass's occupancy (blocks of 256 per CU)
 
 // ------------------------------------------------------------------ launchers (bw_dedup.hip)
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),

@@ -31,10 +31,13 @@ sys.path.insert(0, ROOT)
 METRIC = "GB/s chunked+hashed+deduped (whole node, 1/2/4/8 GPU), bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: PCIe Gen5 x16, 63 GB/s (spec)
-# k_b3_groups' own ceiling: 0.1845 wave-instructions per input byte (SQ_INSTS_VALU)
-# at the measured issue costs of its mix (tools/op_rate.hip: ~3.55 cycles per instruction per
-# SIMD) on 1024 SIMDs at the 1.94 GHz top of the clock the chip holds under this load
-B3_VALU_CEILING_GBS = 3000.0
+# The BLAKE3 leaf pass's own ceiling is integer VALU issue.  It is measured in the
+# run: bw_calibrate_b3 runs the pass's compression from registers at its occupancy, giving bytes
+# per shader clock per CU, which the line scales to the GFX clock the chip held over the timed steps.
+CALIBRATE_MS = 150.0
+# stage marks kept in the timed region (BW_OPT_PROFILE_MASK): the scan and the leaf pass, the two
+# kernels the roofline is about; a mark costs the stream ~5 us, so the full split is taken after
+PROFILE_MASK_TIMED = (1 << 0) | (1 << 1) | (1 << 4) | (1 << 5)  # scan, compact, b3_leaf, b3_tree
 
 
 def log(*a):
@@ -154,6 +157,10 @@ def main():
     ap.add_argument("--order-hash", type=int, default=None, choices=[0, 1], help="BW_OPT_ORDER_HASH")
     ap.add_argument("--split", type=int, default=None, choices=[1, 2],
                     help="BW_OPT_SPLIT: 2 = multi-file batches of 64 MiB-4 GiB as a head and a tail part on two streams")
+    ap.add_argument("--scan-first", type=int, default=None, choices=[0, 1, 2], help="BW_OPT_SCAN_FIRST")
+    ap.add_argument("--all-stage-marks", action="store_true",
+                    help="mark every stage in the timed region (each mark costs the stream ~5 us)")
+    ap.add_argument("--no-calibrate", action="store_true", help="skip the in-run VALU-issue calibration")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
     args = ap.parse_args()
@@ -182,7 +189,7 @@ def main():
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
     from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
-                                   BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
+                                   BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -232,6 +239,8 @@ def main():
             c.set_option(BW_OPT_ORDER_HASH, args.order_hash)
         if args.split is not None:
             c.set_option(BW_OPT_SPLIT, args.split)
+        if args.scan_first is not None:
+            c.set_option(BW_OPT_SCAN_FIRST, args.scan_first)
         if args.host_stream and nctx > 1:
             c.set_option(BW_OPT_DEPTH, 1)  # contexts alternate: one HBM input buffer each is enough
         ctxs.append(c)
@@ -306,7 +315,9 @@ def main():
         if not check["bit_exact"]:
             raise SystemExit("parity check failed")
 
+    full_mask = (1 << len(STAGES)) - 1
     for c in ctxs:
+        c.set_option(BW_OPT_PROFILE_MASK, full_mask if args.all_stage_marks else PROFILE_MASK_TIMED)
         c.profile_enable(True)
     if multi:
         dist.barrier()
@@ -330,9 +341,11 @@ def main():
     stage_ms, nbatch = ctx.profile_read()
     per = {s: stage_ms[s] / max(nbatch, 1) for s in STAGES}
     iso = None
-    if len(ctxs) > 1 and not multi and host is None:
-        # the same batch with nothing beside it (one context, synchronized): each kernel's own
-        # duration, reported next to the live one, which shares the GPU with the other batch
+    if not multi and host is None:
+        # the same batch with nothing beside it (one context, synchronized, every stage marked):
+        # each kernel's own duration, reported next to the live one, which shares the GPU with
+        # the other batches in flight (and has only the roofline's kernels marked)
+        ctx.set_option(BW_OPT_PROFILE_MASK, full_mask)
         ctx.profile_enable(True)
         for _ in range(3):
             with torch.cuda.stream(streams[0]):
@@ -362,10 +375,19 @@ def main():
                 "kernel": kernel,
                 "algorithmic_bytes_per_launch": algo,
                 "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
-    if kernel == leaf_kernel:
-        # the limit this kernel actually meets: integer VALU issue (B3_VALU_CEILING_GBS)
-        roofline["valu_issue"] = {"ceiling": B3_VALU_CEILING_GBS, "unit": "GB/s",
-                                  "frac": round(achieved / B3_VALU_CEILING_GBS, 4)}
+    valu = None
+    if kernel == leaf_kernel and not args.no_calibrate:
+        # the limit this kernel actually meets: integer VALU issue, measured now on this chip
+        cal = ctx.calibrate_b3(CALIBRATE_MS)
+        mhz = power["gfx_mhz_mean"] if power is not None else None
+        ceiling = cal["gbs"] * (mhz / 1e3) / cal["ghz"] if mhz and cal["ghz"] > 0 else cal["gbs"]
+        valu = {"ceiling": round(ceiling, 1), "unit": "GB/s", "frac": round(achieved / ceiling, 4),
+                "basis": ("bw_calibrate_b3: the leaf pass's compression from registers at its occupancy, "
+                          "%.3f B per shader clock per CU, scaled to the %s" %
+                          (cal["bytes_per_clk_cu"], "%d MHz GFX clock of the timed steps" % mhz if mhz
+                           else "calibration's own clock (no power samples)")),
+                "calibration": {k: round(v, 4) for k, v in cal.items()}}
+        roofline["valu_issue"] = valu
     if host is not None:
         roofline.update({"host_stream_pcie_frac": round(value / PCIE_PEAK_GBS, 4)})
     if power is not None:
@@ -379,10 +401,10 @@ def main():
     if iso is not None:
         # live durations above include the overlap with the other batch in flight
         a_iso = algo / (iso["b3_leaf" if kernel == leaf_kernel else "scan"] * 1e-3) / 1e9
-        roofline["live_shares_gpu_with"] = "the other batches in flight (%d contexts)" % len(ctxs)
+        if len(ctxs) > 1:
+            roofline["live_shares_gpu_with"] = "the other batches in flight (%d contexts)" % len(ctxs)
         roofline["isolated"] = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
-                                "valu_issue_frac": (round(a_iso / B3_VALU_CEILING_GBS, 4)
-                                                    if kernel == leaf_kernel else None),
+                                "valu_issue_frac": (round(a_iso / valu["ceiling"], 4) if valu else None),
                                 "stage_ms_per_step": {k: round(v, 3) for k, v in iso.items()}}
 
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None

@@ -167,13 +167,20 @@ enum {
                                     index run one at a time each, in submission order (a batch's scan
                                     then overlaps the previous batch's hashing); 0 (default): as soon
                                     as their inputs are ready */
-    BW_OPT_SPLIT = 11            /* 2: a batch of >= 2 files between 64 MiB and 4 GiB that gates
+    BW_OPT_SPLIT = 11,           /* 2: a batch of >= 2 files between 64 MiB and 4 GiB that gates
                                     through the index runs as two parts on two streams (head files
                                     here, tail files on a helper context), scans and BLAKE3 passes in
                                     order, meant to keep the scan beside the hashing with one batch
                                     in flight; 1 (default): off -- measured slower (the tail's scan
                                     waits for CUs held by the head's hashing).  bw_batch_views /
                                     bw_batch_device_views of a split batch return BW_ESTATE */
+    BW_OPT_PROFILE_MASK = 12,    /* bw_profile_*: bit i = mark the start of stage i (BW_STAGE_*); a
+                                    stage's time runs to the next marked one.  Default: every stage.
+                                    Each mark costs the stream ~5 us of idle time */
+    BW_OPT_SCAN_FIRST = 13       /* when a batch's gear scan is enqueued: 1 = before the host builds
+                                    and uploads the batch tables (the scan needs none of them), 0 =
+                                    after the upload, 2 (default) = first for batches under
+                                    BW_OPT_SCAN_SMALL_BYTES, where the host's share of a batch shows */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 
@@ -503,6 +510,14 @@ enum {
 int bw_profile_enable(bw_ctx* ctx, int on); /* also clears the accumulators */
 /* stage_ms[BW_N_STAGES] = summed milliseconds; *n_batches = batches accumulated.  Syncs. */
 int bw_profile_read(bw_ctx* ctx, double* stage_ms, uint64_t* n_batches);
+
+/* ---- roofline calibration (diagnostic; replaces no reference call, touches no batch state) ----
+ * The BLAKE3 leaf pass's compression run from registers (no memory traffic) on every CU at the
+ * leaf pass's occupancy, for about `ms` milliseconds on the context stream: the integer-issue
+ * ceiling of that pass measured on the running chip.  out[0] = GB/s of message compressed,
+ * out[1] = mean shader clock over the run in GHz, out[2] = bytes per shader clock per CU,
+ * out[3] = the measured launch's milliseconds.  Synchronous. */
+int bw_calibrate_b3(bw_ctx* ctx, double ms, double out[4]);
 
 #ifdef __cplusplus
 }

@@ -574,3 +574,56 @@ def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads):
         for c in cs:
             c.close()
         ix.close()
+
+
+@pytest.mark.parametrize("scan_first", [0, 1])
+def test_scan_first_and_profile_mask(oracle, scan_first):
+    """BW_OPT_SCAN_FIRST moves the gear scan ahead of the host's batch tables and
+    BW_OPT_PROFILE_MASK thins the stage marks: neither changes a result (two contexts sharing an
+    index, profiled, four batches), and only the marked stages accumulate time."""
+    import torch
+    from backuwup_amd._lib import BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, STAGES
+    data, offs, lens = tree_corpus(48 << 20, seed=23, max_file=12 << 20)
+    batches = _slices(data, offs, lens, [(0, len(lens) // 2), (len(lens) // 2, len(lens))]) * 2
+    want = oracle_session(oracle, batches)
+    devs = [torch.from_numpy(d).cuda() for d, _, _ in batches[:2]] * 2
+    torch.cuda.synchronize()
+    mask = (1 << 0) | (1 << 4) | (1 << 5)  # scan, b3_leaf, b3_tree
+    ix = Index(0)
+    cs = [Context(0), Context(0)]
+    try:
+        for c in cs:
+            c.set_stream(torch.cuda.Stream().cuda_stream)
+            c.attach_index(ix)
+            c.set_option(BW_OPT_SCAN_FIRST, scan_first)
+            c.set_option(BW_OPT_PROFILE_MASK, mask)
+            c.profile_enable(True)
+        with pytest.raises(BwError):
+            cs[0].set_option(BW_OPT_PROFILE_MASK, 0)
+        with pytest.raises(BwError):
+            cs[0].set_option(BW_OPT_SCAN_FIRST, 3)
+        cs[0].index_reset()
+        tickets = [cs[k % 2].submit_device(t.data_ptr(), d.size, o, l) for k, (t, (d, o, l)) in enumerate(zip(devs, batches))]
+        for k, t in enumerate(tickets):
+            blobs_equal(cs[k % 2].wait(t), want[k], k)
+        ms, n = cs[0].profile_read()
+        assert n == 2
+        for i, s in enumerate(STAGES):
+            assert (ms[s] > 0) == bool((mask >> i) & 1), (s, ms[s])
+    finally:
+        for c in cs:
+            c.close()
+        ix.close()
+
+
+def test_calibrate_b3():
+    """bw_calibrate_b3: the leaf pass's compression from registers, timed on the device."""
+    with Context(0) as c:
+        cal = c.calibrate_b3(20.0)
+        assert 100 < cal["gbs"] < 20000, cal
+        assert 0.3 < cal["ghz"] < 3.5, cal
+        assert cal["launch_ms"] > 2, cal
+        n_cu = cal["gbs"] / cal["ghz"] / cal["bytes_per_clk_cu"]
+        assert 200 < n_cu < 320, cal
+        with pytest.raises(BwError):
+            c.calibrate_b3(0.0)
