@@ -309,12 +309,30 @@ __device__ __forceinline__ void b3_line_block(uint32_t m[16], uint32_t blk, uint
     }
 }
 
-template <int MINW>
+constexpr uint64_t B3_SMALL_LEAVES = 64;
+__device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr, const BlobArrays& b,
+                                              uint32_t* __restrict__ cv_buf, uint8_t* __restrict__ digests);
+__device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
+                              uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests);
+
+// FUSED: the upper levels run inside the leaf pass.  Each wave adds the groups it finished to its
+// blobs' counters (b.gdone, one atomic per blob per wave); the wave that completes a blob builds its
+// upper levels at once -- the whole wave for a blob of > 64 leaves (b3_upper_wave), one lane per blob
+// of 5..64 leaves (b3_small_blob) -- and sets the counter back to zero for the next batch.  The
+// upper levels then fill the CUs the leaf pass's last round leaves idle instead of running as a
+// launch of their own after it.
+template <int MINW, bool FUSED>
 __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restrict__ data, const uint64_t* ctr,
                                                         BlobArrays b, uint32_t* __restrict__ cv_buf,
-                                                        uint8_t* __restrict__ digests) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= ctr[C_NGROUPS]) return;
+                                                        uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests) {
+    const uint64_t ng = ctr[C_NGROUPS];
+    const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // FUSED needs whole waves (the completing wave's shuffles and lane 63's digest store): lanes past
+    // the last group repeat the last group's work (identical values to identical addresses) and
+    // are not counted; only whole waves past it leave
+    const bool live = g0 < ng;
+    if (FUSED ? (ng == 0 || g0 - (threadIdx.x & 63) >= ng) : !live) return;
+    const uint64_t g = live ? g0 : ng - 1;
     const uint64_t nb = ctr[C_NBLOBS];
     uint64_t lo = 0, hi = nb;
     while (lo < hi) {
@@ -403,6 +421,38 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
 #pragma unroll
         for (int i = 0; i < 8; i++) o8[i] = acc[i];
     }
+    if constexpr (FUSED) {
+        const uint32_t lane = threadIdx.x & 63;
+        // the wave's lanes hold consecutive groups, so each blob is one run of lanes (live lanes
+        // are a prefix of the wave)
+        const bool upper = live && n > 4;
+        const uint64_t pb = bw_shfl_up64(blob, 1);
+        const bool head = upper && (lane == 0 || pb != blob);
+        const uint64_t H = __ballot(head), U = __ballot(upper);
+        if (H == 0) return;  // wave-uniform
+        __threadfence();     // release: this wave's level-2 nodes, before any counter moves
+        bool complete = false;
+        if (head) {
+            const uint64_t above = H & ~((2ull << lane) - 1);  // heads after this lane
+            const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : 64u;
+            const uint64_t run = (end == 64 ? ~0ull : ((1ull << end) - 1)) & ~((1ull << lane) - 1);
+            const uint32_t cnt = (uint32_t)__popcll(U & run);
+            const uint32_t total = (uint32_t)((n + 3) / 4);
+            const uint32_t old = atomicAdd(b.gdone + blob, cnt);
+            BW_ASSERT(old + cnt <= total);
+            complete = old + cnt == total;
+            if (complete) b.gdone[blob] = 0;  // nothing else touches it in this pass
+        }
+        const uint64_t C = __ballot(complete);
+        if (C == 0) return;
+        __threadfence();  // acquire: the other waves' level-2 nodes of the completed blobs
+        for (uint64_t m = C; m; m &= m - 1) {  // blobs of > 64 leaves: the whole wave, one by one
+            const int h = __builtin_ctzll(m);
+            const uint64_t cb = bw_shfl64(blob, h), cl = bw_shfl64(len, h);
+            if (cl > (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) b3_upper_wave(cb, cl, b, cv_buf, cv_tmp, digests);
+        }
+        if (complete) b3_small_blob(blob, ctr, b, cv_buf, digests);  // 5..64 leaves; returns otherwise
+    }
 }
 
 // Upper levels of a small blob (4 < n <= B3_SMALL_LEAVES leaves), one lane per blob: a batch of
@@ -411,7 +461,6 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
 // in the blob's own cv_buf slots (slot d < node i, so it only overwrites consumed nodes); the
 // stack is then folded from the right onto the ragged tail (bits 0..1 of n).  The merge that
 // completes a power-of-two blob, or the last fold, carries ROOT.
-constexpr uint64_t B3_SMALL_LEAVES = 64;
 
 __device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr, const BlobArrays& b,
                                               uint32_t* __restrict__ cv_buf, uint8_t* __restrict__ digests) {
@@ -476,7 +525,7 @@ __device__ __forceinline__ void b3_shfl8(const uint32_t x[8], int src, uint32_t 
     for (int w = 0; w < 8; w++) out[w] = __shfl(x[w], src, 64);
 }
 
-__device__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
+__device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
                               uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t n = (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;  // > B3_SMALL_LEAVES
@@ -632,9 +681,13 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
 #ifndef BW_B3_DYN_LDS
 #define BW_B3_DYN_LDS 0  // A/B: extra LDS per block caps the blocks per CU (occupancy experiments)
 #endif
-    if (loads == B3_LOADS_LINES)
-        hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st, data, ctr, b,
-                           cv_buf, digests);
+    const bool fused = loads == B3_LOADS_LINES && b.gdone;
+    if (fused)
+        hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
+                           data, ctr, b, cv_buf, cv_tmp, digests);
+    else if (loads == B3_LOADS_LINES)
+        hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
+                           data, ctr, b, cv_buf, cv_tmp, digests);
     else if (loads == B3_LOADS_PAIRS)
         hipLaunchKernelGGL((k_b3_groups<false, 1, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), BW_B3_DYN_LDS, st,
                            data, ctr, b, cv_buf, digests);
@@ -645,7 +698,7 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     if (between) hipEventRecord(between, st);
     if (upper != st) hipStreamWaitEvent(upper, between, 0);
     st = upper;
-    if (max_leaves > 4) {
+    if (max_leaves > 4 && !fused) {
         const uint64_t small = (max_blobs + 255) / 256;
         uint64_t big = max_leaves > (int)B3_SMALL_LEAVES ? (max_blobs + 3) / 4 : 0;  // 4 waves per block
         if (big > 4096) big = 4096;

@@ -49,7 +49,9 @@ constexpr int STAGE_RING = 4;
 
 // One batch's outputs (kept until the ring wraps) and its host-streamed input.
 struct Slot {
-    DevBuf ctr, digests, is_dup, packed, input;
+    // `res_dev`: the batch's device counters (C_COUNT u64) followed by its packed bw_blob records,
+    // one buffer so that the results come back to the host in one copy
+    DevBuf res_dev, digests, is_dup, input;
     PinBuf meta;                      // pinned metadata staging of this slot's batch
     hipEvent_t meta_done = nullptr;   // `meta` reusable once this fired
     hipEvent_t input_free = nullptr;  // the batch's last read of its input (BLAKE3) finished
@@ -104,6 +106,7 @@ struct bw_ctx {
     DevBuf tile_count, tile_slots, tile_off, tile_btot, cand, ovf;
     DevBuf meta, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
+    DevBuf b_gdone;  // per blob: BLAKE3 groups finished (fused upper levels); zero between passes
     DevBuf cv, cv2, data, scratch, ucnt, ubtot;
     DevBuf bk_blk, bk_pack, bk_v;  // multi-GPU exchange buckets (bw_partition_buckets, ...)
     // bw_exchange_dedup: my buckets and the ones received, their source positions, the counts
@@ -140,6 +143,7 @@ struct bw_ctx {
     uint64_t scan_small_bytes = SCAN_SMALL_BYTES;
     bool order_hash = false;  // BW_OPT_ORDER_HASH
     uint64_t cand_cap_forced = 0;
+    bool b3_fused = true;  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass
     int b3_loads = B3_LOADS_LINES;  // k_b3_lines: 1.07x fetch (pairs 1.42x), -6 % time isolated
     int scan_waves = 16;
     // latency stream: the small kernels between the two big passes (compaction, boundary
@@ -186,7 +190,7 @@ struct bw_ctx {
 
     // stage timing: two event sets, alternated per batch so recording never waits on the GPU
     bool prof = false;
-    uint32_t prof_mask = (1u << BW_N_STAGES) - 1;  // stages whose start is marked (BW_OPT_PROFILE_MASK)
+    uint32_t prof_mask = (2u << BW_N_STAGES) - 1;  // marks recorded (BW_OPT_PROFILE_MASK)
     int scan_first = 2;                             // BW_OPT_SCAN_FIRST
     hipEvent_t ev[2][BW_N_STAGES + 1] = {};
     bool ev_pending[2] = {false, false};
@@ -255,6 +259,10 @@ static void free_host(PinBuf& b) {
 template <typename T>
 static T* P(DevBuf& b) { return (T*)b.p; }
 
+constexpr size_t CTR_BYTES = C_COUNT * 8;
+static uint64_t* slot_ctr(Slot& s) { return (uint64_t*)s.res_dev.p; }
+static uint8_t* slot_records(Slot& s) { return (uint8_t*)s.res_dev.p + CTR_BYTES; }
+
 static int make_masks(uint32_t mn, uint32_t av, uint32_t mx, Masks* mk) {
     // FastCDC::with_level asserts (fastcdc 3.0.3 v2020) -> BW_EINVAL instead of a panic.
     if (mn < BW_MINIMUM_MIN || mn > BW_MINIMUM_MAX) return BW_EINVAL;
@@ -286,15 +294,17 @@ static uint64_t seg_len_for(const Masks& mk) {
 
 // ------------------------------------------------------------------ stage timing
 
-// Stage i's time runs from its mark to the next recorded one (prof_mask: the marks recorded; the
-// batch-end mark BW_N_STAGES always is).  Every event recorded between two kernels costs the
-// stream ~5.5 us of idle time (profiles/r03: k_scan -> k_tile_partial with a mark between them
-// 5.7 us, kernels without one 0), so the bench's timed region marks only its dominant kernels.
+// prof_mask bit i (i <= BW_N_STAGES, the batch end) = record mark i; stage i's time runs from its
+// mark to the next recorded one, and the last recorded mark closes the batch.  Every event
+// recorded between two kernels costs the stream ~5.5 us of idle time (profiles/r03: k_scan ->
+// k_tile_partial with a mark between them 5.7 us, kernels without one 0), so the bench's timed
+// region marks only the leaf pass.
 static void prof_collect(bw_ctx* c, int set) {
     if (!c->ev_pending[set]) return;
-    hipEventSynchronize(c->ev[set][BW_N_STAGES]);
-    const uint32_t mask = c->prof_mask | (1u << BW_N_STAGES);
-    for (int i = 0; i < BW_N_STAGES; i++) {
+    const uint32_t mask = c->prof_mask;
+    const int last = 31 - __builtin_clz(mask);
+    hipEventSynchronize(c->ev[set][last]);
+    for (int i = 0; i < last; i++) {
         if (!((mask >> i) & 1)) continue;
         int j = i + 1;
         while (!((mask >> j) & 1)) j++;
@@ -306,8 +316,7 @@ static void prof_collect(bw_ctx* c, int set) {
 }
 
 static void prof_mark(bw_ctx* c, int stage, hipStream_t st = nullptr) {
-    if (c->prof && (stage == BW_N_STAGES || ((c->prof_mask >> stage) & 1)))
-        hipEventRecord(c->ev[c->ev_set][stage], st ? st : c->stream);
+    if (c->prof && ((c->prof_mask >> stage) & 1)) hipEventRecord(c->ev[c->ev_set][stage], st ? st : c->stream);
 }
 
 // ------------------------------------------------------------------ the index object
@@ -549,7 +558,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
     DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->meta,
                      &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
-                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->cv, &c->cv2,
+                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->b_gdone, &c->cv, &c->cv2,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
                      &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage,
@@ -559,10 +568,9 @@ extern "C" void bw_destroy(bw_ctx* c) {
     c->zw = nullptr;
     for (int k = 0; k <= MAX_DEPTH; k++) {
         Slot& s = k < MAX_DEPTH ? c->slots[k] : c->sync_slot;
-        free_dev(s.ctr);
+        free_dev(s.res_dev);
         free_dev(s.digests);
         free_dev(s.is_dup);
-        free_dev(s.packed);
         free_dev(s.input);
         free_host(s.meta);
         free_host(s.res);
@@ -664,8 +672,12 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             c->b3_loads = (int)v;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_PROFILE_MASK:
-            if (v == 0 || v >= (1u << BW_N_STAGES)) return BW_EINVAL;
+            if (__builtin_popcountll(v) < 2 || v >= (2u << BW_N_STAGES)) return BW_EINVAL;
             c->prof_mask = (uint32_t)v;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
+        case BW_OPT_B3_UPPER:
+            if (v > 1) return BW_EINVAL;
+            c->b3_fused = v == 1;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_SCAN_FIRST:
             if (v > 2) return BW_EINVAL;
@@ -801,8 +813,9 @@ static int stage_results(bw_ctx* c, Slot& s) {
         if (int rc = ensure_host(c, s.res, C_COUNT * 8 + want * sizeof(bw_blob))) return rc;
     }
     uint8_t* h = (uint8_t*)s.res.p;
-    HIPCHK(c, hipMemcpyAsync(h, s.ctr.p, C_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
-    if (want) HIPCHK(c, hipMemcpyAsync(h + C_COUNT * 8, s.packed.p, want * sizeof(bw_blob), hipMemcpyDeviceToHost, c->stream));
+    // one copy: the counters and the first `want` records lie back to back on the device (two
+    // copies cost the stream a ~12 us gap between them with one batch in flight, profiles/r03)
+    HIPCHK(c, hipMemcpyAsync(h, s.res_dev.p, CTR_BYTES + want * sizeof(bw_blob), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(s.done, c->stream));
     s.res_n = want;
     return BW_OK;
@@ -832,8 +845,17 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     const bool do_dedup = do_hash && !(prm->flags & BW_F_NO_DEDUP);
 
     // ---- the scan's tiles and buffers
-    uint64_t ncf_pre = 0;
-    for (uint64_t f = 0; f < nf; f++) ncf_pre += flen[f] > prm->small_file_threshold && flen[f] > 0;
+    // CDC files and the blob bound (the same bound as the tables below give): the result buffer
+    // holds the counters the scan writes, so it is sized before the scan is enqueued
+    uint64_t ncf_pre = 0, mb_pre = 0;
+    {
+        const uint64_t mc = std::min<uint64_t>(mk.s0, mk.max);
+        for (uint64_t f = 0; f < nf; f++) {
+            const bool cdc = flen[f] > prm->small_file_threshold && flen[f] > 0;
+            ncf_pre += cdc;
+            mb_pre += cdc ? flen[f] / mc + 2 : 1;
+        }
+    }
     // small batches scan half-size tiles: with one 128 KiB tile per wave the per-tile start
     // costs dominate (C1: 0.50 -> 0.33 ms per GiB); large ones keep the longer strips
     // (BW_OPT_SCAN_SMALL_BYTES moves the threshold, so the tests can run either tile size on any input)
@@ -845,13 +867,13 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         rc0 |= ensure(c, c->tile_count, n_tiles * 4);
         rc0 |= ensure(c, c->tile_slots, n_tiles * SCAN_CAP * 8);
         rc0 |= ensure(c, c->ovf, n_tiles * 4);
-        rc0 |= ensure(c, s.ctr, C_COUNT * 8);
+        rc0 |= ensure(c, s.res_dev, CTR_BYTES + mb_pre * sizeof(bw_blob));
         if (rc0) return BW_ENOMEM;
     }
     // ---- the gear scan: counters zeroed, then the scan; it reads only the batch bytes and the
     // tile buffers above
     auto enqueue_scan = [&]() -> int {
-        HIPCHK(c, hipMemsetAsync(s.ctr.p, 0, C_COUNT * 8, c->stream));
+        HIPCHK(c, hipMemsetAsync(s.res_dev.p, 0, CTR_BYTES, c->stream));
         if (c->prof) {
             c->ev_set ^= 1;
             prof_collect(c, c->ev_set);  // the set about to be reused belongs to batch k-2
@@ -865,7 +887,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
             if (x->scan_tail_set) HIPCHK(c, hipStreamWaitEvent(c->stream, x->scan_tail, 0));
         }
         if (!launch_scan(c->stream, d_data, data_len, n_tiles, mk, P<uint32_t>(c->tile_count),
-                         P<uint64_t>(c->tile_slots), P<uint32_t>(c->ovf), P<uint64_t>(s.ctr), c->scan_waves)) {
+                         P<uint64_t>(c->tile_slots), P<uint32_t>(c->ovf), slot_ctr(s), c->scan_waves)) {
             c->err = "no scan kernel for tile size 2^" + std::to_string(mk.tile_shift);
             return BW_EINVAL;
         }
@@ -992,7 +1014,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
                    total_len = tot.total_len;
     const uint64_t max_groups = total_len / 4096 + max_blobs + 1;
     const int max_leaves = (int)std::min<uint64_t>((max_blob_len + 1023) / 1024, 1u << 30);
-    if (ncf != ncf_pre) return BW_ESTATE;  // the same test as the pre-count; cannot differ
+    if (ncf != ncf_pre || max_blobs != mb_pre) return BW_ESTATE;  // the same sums as the pre-count; cannot differ
 
     // ---- device buffers
     phase(0);
@@ -1016,11 +1038,14 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     rc |= ensure(c, c->b_kind, max_blobs * 4);
     rc |= ensure(c, c->b_fend, max_blobs * 8);
     rc |= ensure(c, c->b_ghash, max_blobs * 8);
+    if (c->b_gdone.cap < max_blobs * 4) {  // the passes leave it zeroed; a new buffer starts so
+        rc |= ensure(c, c->b_gdone, max_blobs * 4);
+        if (!rc) HIPCHK(c, hipMemsetAsync(c->b_gdone.p, 0, c->b_gdone.cap, c->stream));
+    }
     rc |= ensure(c, c->cv, max_groups * 32);
     rc |= ensure(c, c->cv2, max_leaves > 64 ? max_groups * 32 : 16);
     rc |= ensure(c, s.digests, max_blobs * 32);
     rc |= ensure(c, s.is_dup, max_blobs);
-    rc |= ensure(c, s.packed, max_blobs * sizeof(bw_blob));
     rc |= ensure(c, c->ucnt, 2 * nunits * 8);
     rc |= ensure(c, c->ubtot, 2 * (nunits / 256 + 2) * 8);
     if (rc) return BW_ENOMEM;
@@ -1053,11 +1078,12 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
 
     if (!scan_first)
         if (int r6 = enqueue_scan()) return r6;
-    uint64_t* ctr = P<uint64_t>(s.ctr);
+    uint64_t* ctr = slot_ctr(s);
     hipStream_t st = c->stream;
 
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
-                 P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len};
+                 P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len,
+                 c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr};
 
     // ---- chunking (the scan on the context stream, the latency-bound kernels after it on `lat`)
     const bool split = c->lat_split;
@@ -1130,7 +1156,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     phase(4);
     prof_mark(c, BW_STAGE_PACK, lat);
     launch_pack(lat, ctr, b, d_fstart, P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
-                P<uint8_t>(s.packed), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr);
+                slot_records(s), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr);
     if (split) {  // the batch ends on the context stream (the caller's order)
         prof_mark(c, BW_N_STAGES, lat);
         HIPCHK(c, hipEventRecord(c->e_end, lat));
@@ -1360,7 +1386,7 @@ static int slot_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t
         const uint64_t k = std::min(n, s.res_n);
         memcpy(out, (const uint8_t*)s.res.p + C_COUNT * 8, k * sizeof(bw_blob));
         if (n > k)  // more blobs than staged: the rest straight from the device
-            HIPCHK(c, hipMemcpy(out + k, P<uint8_t>(s.packed) + k * sizeof(bw_blob), (n - k) * sizeof(bw_blob),
+            HIPCHK(c, hipMemcpy(out + k, slot_records(s) + k * sizeof(bw_blob), (n - k) * sizeof(bw_blob),
                                 hipMemcpyDeviceToHost));
     }
     return BW_OK;
@@ -1418,7 +1444,7 @@ extern "C" int bw_batch_device_views(bw_ctx* c, uint64_t* n_blobs, const uint8_t
     }
     hipSetDevice(c->device);
     uint64_t n = 0;
-    HIPCHK(c, hipMemcpyAsync(&n, (uint64_t*)s->ctr.p + C_NBLOBS, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&n, slot_ctr(*s) + C_NBLOBS, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (n_blobs) *n_blobs = n;
     if (d_digests) *d_digests = P<uint8_t>(s->digests);
@@ -1551,7 +1577,7 @@ extern "C" int bw_batch_views(bw_ctx* c, uint64_t ticket, const uint64_t** d_n_b
         c->err = "the batch was split in two parts (BW_OPT_SPLIT): no single device view";
         return BW_ESTATE;
     }
-    if (d_n_blobs) *d_n_blobs = P<uint64_t>(s->ctr) + C_NBLOBS;
+    if (d_n_blobs) *d_n_blobs = slot_ctr(*s) + C_NBLOBS;
     if (d_digests) *d_digests = P<uint8_t>(s->digests);
     if (d_is_dup) *d_is_dup = P<uint8_t>(s->is_dup);
     if (max_blobs) *max_blobs = s->max_blobs;
@@ -1642,7 +1668,7 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     rc |= ensure(c, c->ex_v, slots);
     rc |= ensure(c, c->ex_rv, slots);
     if (rc) return BW_ENOMEM;
-    const uint64_t* d_n = P<uint64_t>(s->ctr) + C_NBLOBS;
+    const uint64_t* d_n = slot_ctr(*s) + C_NBLOBS;
     if (int r = bw_partition_buckets(c, P<uint8_t>(s->digests), d_n, s->max_blobs, cap, W, P<uint8_t>(c->ex_bk),
                                      P<uint64_t>(c->ex_perm), cnt))
         return r;
@@ -1652,8 +1678,8 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
         return r;
     if (int r = comm_all_to_all(comm, c->ex_v.p, c->ex_rv.p, cap, st, c->err)) return r;
     launch_bucket_scatter(st, P<uint8_t>(c->ex_rv), P<uint64_t>(c->ex_perm), cnt, W, cap, P<uint8_t>(s->is_dup),
-                          P<uint8_t>(s->packed));
-    launch_index_snapshot(st, P<uint64_t>(c->idx->dstate), P<uint64_t>(s->ctr));
+                          slot_records(*s));
+    launch_index_snapshot(st, P<uint64_t>(c->idx->dstate), slot_ctr(*s));
     HIPCHK(c, hipGetLastError());
     s->dedup = true;  // bw_wait now reports the index's sticky errors for this batch
     s->mark = c->idx_mark;

@@ -97,6 +97,8 @@ struct BlobArrays {
     uint64_t* ghash;  // Chunk.hash
     uint64_t cap;       // entries the arrays hold (BW_DEBUG checks)
     uint64_t data_len;  // bytes of the batch buffer (BW_DEBUG checks)
+    uint32_t* gdone = nullptr;  // per blob: BLAKE3 groups finished (zero between passes); null = the
+                                // upper levels run as a launch of their own (k_b3_upper)
 };
 
 // ------------------------------------------------------------------ launchers (bw_cdc.hip)

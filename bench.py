@@ -35,9 +35,10 @@ PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: PCIe Gen5 x16, 63 GB/s (spec)
 # run: bw_calibrate_b3 runs the pass's compression from registers at its occupancy, giving bytes
 # per shader clock per CU, which the line scales to the GFX clock the chip held over the timed steps.
 CALIBRATE_MS = 150.0
-# stage marks kept in the timed region (BW_OPT_PROFILE_MASK): the scan and the leaf pass, the two
-# kernels the roofline is about; a mark costs the stream ~5 us, so the full split is taken after
-PROFILE_MASK_TIMED = (1 << 0) | (1 << 1) | (1 << 4) | (1 << 5)  # scan, compact, b3_leaf, b3_tree
+# stage marks kept in the timed region (BW_OPT_PROFILE_MASK): the two around the BLAKE3 leaf pass,
+# the dominant kernel; each mark costs the stream ~5 us, so the full stage split is taken after,
+# on the same batch with nothing beside it
+PROFILE_MASK_TIMED = (1 << 4) | (1 << 5)  # b3_leaf start, b3_tree start
 
 
 def log(*a):
@@ -157,6 +158,8 @@ def main():
     ap.add_argument("--order-hash", type=int, default=None, choices=[0, 1], help="BW_OPT_ORDER_HASH")
     ap.add_argument("--split", type=int, default=None, choices=[1, 2],
                     help="BW_OPT_SPLIT: 2 = multi-file batches of 64 MiB-4 GiB as a head and a tail part on two streams")
+    ap.add_argument("--b3-upper", type=int, default=None, choices=[0, 1],
+                    help="BW_OPT_B3_UPPER: 1 = upper levels inside the leaf pass (default), 0 = own launch")
     ap.add_argument("--scan-first", type=int, default=None, choices=[0, 1, 2], help="BW_OPT_SCAN_FIRST")
     ap.add_argument("--all-stage-marks", action="store_true",
                     help="mark every stage in the timed region (each mark costs the stream ~5 us)")
@@ -189,7 +192,7 @@ def main():
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
     from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
-                                   BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
+                                   BW_OPT_B3_UPPER, BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -241,6 +244,8 @@ def main():
             c.set_option(BW_OPT_SPLIT, args.split)
         if args.scan_first is not None:
             c.set_option(BW_OPT_SCAN_FIRST, args.scan_first)
+        if args.b3_upper is not None:
+            c.set_option(BW_OPT_B3_UPPER, args.b3_upper)
         if args.host_stream and nctx > 1:
             c.set_option(BW_OPT_DEPTH, 1)  # contexts alternate: one HBM input buffer each is enough
         ctxs.append(c)
@@ -315,7 +320,7 @@ def main():
         if not check["bit_exact"]:
             raise SystemExit("parity check failed")
 
-    full_mask = (1 << len(STAGES)) - 1
+    full_mask = (2 << len(STAGES)) - 1  # every stage and the batch end
     for c in ctxs:
         c.set_option(BW_OPT_PROFILE_MASK, full_mask if args.all_stage_marks else PROFILE_MASK_TIMED)
         c.profile_enable(True)
@@ -363,7 +368,9 @@ def main():
 
     # roofline for the dominant kernel (largest stage time); algorithmic traffic = every input
     # byte read once per launch, so bytes per launch = the batch's file bytes
-    dom = max(["scan", "b3_leaf"], key=lambda s: per[s])
+    # the dominant kernel is the BLAKE3 leaf pass (the longer pass on a batch alone, `isolated`
+    # below, in every configuration); the timed region marks only it
+    dom = max(["scan", "b3_leaf"], key=lambda s: per[s]) if args.all_stage_marks else "b3_leaf"
     algo = processed if dom == "b3_leaf" else n
     achieved = algo / (per[dom] * 1e-3) / 1e9
     loads = args.b3_loads if args.b3_loads is not None else BW_B3_LOADS_DEFAULT

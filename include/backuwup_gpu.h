@@ -174,13 +174,18 @@ enum {
                                     in flight; 1 (default): off -- measured slower (the tail's scan
                                     waits for CUs held by the head's hashing).  bw_batch_views /
                                     bw_batch_device_views of a split batch return BW_ESTATE */
-    BW_OPT_PROFILE_MASK = 12,    /* bw_profile_*: bit i = mark the start of stage i (BW_STAGE_*); a
-                                    stage's time runs to the next marked one.  Default: every stage.
+    BW_OPT_PROFILE_MASK = 12,    /* bw_profile_*: bit i = mark the start of stage i (BW_STAGE_*), bit
+                                    BW_N_STAGES = the batch end; a stage's time runs to the next mark,
+                                    the last mark closes the batch (at least two bits).  Default: all.
                                     Each mark costs the stream ~5 us of idle time */
-    BW_OPT_SCAN_FIRST = 13       /* when a batch's gear scan is enqueued: 1 = before the host builds
+    BW_OPT_SCAN_FIRST = 13,      /* when a batch's gear scan is enqueued: 1 = before the host builds
                                     and uploads the batch tables (the scan needs none of them), 0 =
                                     after the upload, 2 (default) = first for batches under
                                     BW_OPT_SCAN_SMALL_BYTES, where the host's share of a batch shows */
+    BW_OPT_B3_UPPER = 14         /* BLAKE3 levels above the 4-leaf groups: 1 (default) = inside the leaf
+                                    pass (k_b3_lines; the wave that finishes a blob's last group builds
+                                    them), 0 = a launch of their own after it (k_b3_upper).  Only the
+                                    aligned-line leaf pass (BW_OPT_B3_LOADS 2) fuses them */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from backuwup_amd import make_params
-from backuwup_amd._lib import BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE, BW_OPT_B3_LOADS, BwError
+from backuwup_amd._lib import BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE, BW_OPT_B3_LOADS, BW_OPT_B3_UPPER, BwError
 from backuwup_amd.synth import splitmix_bytes
 
 pytestmark = pytest.mark.gpu
@@ -32,12 +32,15 @@ KAT = {
 
 
 # every BLAKE3 test runs with each leaf-pass loader: 0 = one block ahead, 1 = 132-byte block pairs
-# (k_b3_groups), 2 = aligned 128-byte lines through registers (k_b3_lines, the default)
-@pytest.fixture(params=[0, 1, 2], ids=["prefetch", "pairs", "lines"])
+# (k_b3_groups), 2 = aligned 128-byte lines through registers (k_b3_lines, the default) with the
+# upper levels inside the leaf pass (BW_OPT_B3_UPPER 1, the default) or as a launch of their own
+@pytest.fixture(params=[(0, 0), (1, 0), (2, 1), (2, 0)], ids=["prefetch", "pairs", "lines", "lines-unfused"])
 def b3ctx(ctx, request):
-    ctx.set_option(BW_OPT_B3_LOADS, request.param)
+    ctx.set_option(BW_OPT_B3_LOADS, request.param[0])
+    ctx.set_option(BW_OPT_B3_UPPER, request.param[1])
     yield ctx
-    ctx.set_option(BW_OPT_B3_LOADS, 2)  # the context default
+    ctx.set_option(BW_OPT_B3_LOADS, 2)  # the context defaults
+    ctx.set_option(BW_OPT_B3_UPPER, 1)
 
 
 def test_blake3_kat(b3ctx):

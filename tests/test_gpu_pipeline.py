@@ -544,14 +544,14 @@ def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
     assert got[0][2][3].all()  # batch 2 repeats batch 0 on rank 0
 
 
-@pytest.mark.parametrize("scan_waves,latency,loads", [(8, 0, 1), (16, 1, 1), (8, 1, 0), (16, 0, 0), (16, 0, 2),
-                                                     (8, 1, 2)])
-def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads):
+@pytest.mark.parametrize("scan_waves,latency,loads,upper", [(8, 0, 1, 0), (16, 1, 1, 0), (8, 1, 0, 0), (16, 0, 0, 0),
+                                                           (16, 0, 2, 1), (8, 1, 2, 1), (16, 0, 2, 0)])
+def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads, upper):
     """The scheduling variants (8-wave scan blocks, the high-priority latency stream, both BLAKE3
     load modes) change only where and when kernels run: results equal the oracle, including two
     batches in flight on two contexts that share an index."""
     import torch
-    from backuwup_amd._lib import BW_OPT_B3_LOADS, BW_OPT_LATENCY_STREAM, BW_OPT_SCAN_WAVES
+    from backuwup_amd._lib import BW_OPT_B3_LOADS, BW_OPT_B3_UPPER, BW_OPT_LATENCY_STREAM, BW_OPT_SCAN_WAVES
     data, offs, lens = tree_corpus(80 << 20, seed=21, max_file=20 << 20)
     batches = _slices(data, offs, lens, [(0, len(lens) // 2), (len(lens) // 2, len(lens))]) * 2
     want = oracle_session(oracle, batches)
@@ -566,6 +566,7 @@ def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads):
             c.set_option(BW_OPT_SCAN_WAVES, scan_waves)
             c.set_option(BW_OPT_LATENCY_STREAM, latency)
             c.set_option(BW_OPT_B3_LOADS, loads)
+            c.set_option(BW_OPT_B3_UPPER, upper)
         cs[0].index_reset()
         tickets = [cs[k % 2].submit_device(t.data_ptr(), d.size, o, l) for k, (t, (d, o, l)) in enumerate(zip(devs, batches))]
         for k, t in enumerate(tickets):
@@ -588,7 +589,7 @@ def test_scan_first_and_profile_mask(oracle, scan_first):
     want = oracle_session(oracle, batches)
     devs = [torch.from_numpy(d).cuda() for d, _, _ in batches[:2]] * 2
     torch.cuda.synchronize()
-    mask = (1 << 0) | (1 << 4) | (1 << 5)  # scan, b3_leaf, b3_tree
+    mask = (1 << 0) | (1 << 4) | (1 << 5) | (1 << len(STAGES))  # scan, b3_leaf, b3_tree, batch end
     ix = Index(0)
     cs = [Context(0), Context(0)]
     try:
@@ -598,8 +599,9 @@ def test_scan_first_and_profile_mask(oracle, scan_first):
             c.set_option(BW_OPT_SCAN_FIRST, scan_first)
             c.set_option(BW_OPT_PROFILE_MASK, mask)
             c.profile_enable(True)
-        with pytest.raises(BwError):
-            cs[0].set_option(BW_OPT_PROFILE_MASK, 0)
+        for bad in (0, 1 << 4, 2 << len(STAGES)):  # fewer than two marks, or past the batch end
+            with pytest.raises(BwError):
+                cs[0].set_option(BW_OPT_PROFILE_MASK, bad)
         with pytest.raises(BwError):
             cs[0].set_option(BW_OPT_SCAN_FIRST, 3)
         cs[0].index_reset()
@@ -610,6 +612,14 @@ def test_scan_first_and_profile_mask(oracle, scan_first):
         assert n == 2
         for i, s in enumerate(STAGES):
             assert (ms[s] > 0) == bool((mask >> i) & 1), (s, ms[s])
+        # the leaf pass alone, the batch closed by the b3_tree mark
+        for c in cs:
+            c.set_option(BW_OPT_PROFILE_MASK, (1 << 4) | (1 << 5))
+            c.profile_enable(True)
+        t = cs[0].submit_device(devs[0].data_ptr(), batches[0][0].size, batches[0][1], batches[0][2])
+        cs[0].wait(t)
+        ms, n = cs[0].profile_read()
+        assert n == 1 and ms["b3_leaf"] > 0 and sum(ms.values()) == ms["b3_leaf"], ms
     finally:
         for c in cs:
             c.close()
