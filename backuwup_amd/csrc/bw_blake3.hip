@@ -310,8 +310,31 @@ __device__ __forceinline__ void b3_line_block(uint32_t m[16], uint32_t blk, uint
 }
 
 constexpr uint64_t B3_SMALL_LEAVES = 64;
+
+// Chaining values handed between waves inside one launch (the fused upper levels): agent-scope
+// relaxed atomics, i.e. stores written through past the XCD's L2 and loads that miss it, so no
+// L2-wide writeback/invalidate fence is needed (a __threadfence per wave made the leaf pass 1.5x
+// slower: every wave wrote back and invalidated its XCD's L2, whose lines the neighbouring waves'
+// loads were still reusing).  COH = false: plain accesses (the separate k_b3_upper launch, ordered
+// by the kernel boundary).
+template <bool COH>
+__device__ __forceinline__ uint32_t cv_ld(const uint32_t* p) {
+    if constexpr (COH) return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void cv_st(uint32_t* p, uint32_t v) {
+    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+// every memory operation this wave issued has completed (coherent stores: at the agent's
+// coherence point)
+__device__ __forceinline__ void wave_mem_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <bool COH>
 __device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr, const BlobArrays& b,
                                               uint32_t* __restrict__ cv_buf, uint8_t* __restrict__ digests);
+template <bool COH>
 __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
                               uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests);
 
@@ -320,7 +343,10 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
 // upper levels at once -- the whole wave for a blob of > 64 leaves (b3_upper_wave), one lane per blob
 // of 5..64 leaves (b3_small_blob) -- and sets the counter back to zero for the next batch.  The
 // upper levels then fill the CUs the leaf pass's last round leaves idle instead of running as a
-// launch of their own after it.
+// launch of their own after it.  Measured (profiles/r03/s04_fused): the leaf pass gets 15-21 %
+// slower on C1, C2 and C4 (C2 5.71 -> 6.92 ms with the upper levels, against 5.71 + 0.25 ms
+// apart), so it is an option (BW_OPT_B3_UPPER), off by default.  With a __threadfence per wave
+// instead of the coherent accessors it was 1.5x slower (profiles/r03/s03_fused_fence).
 template <int MINW, bool FUSED>
 __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restrict__ data, const uint64_t* ctr,
                                                         BlobArrays b, uint32_t* __restrict__ cv_buf,
@@ -419,7 +445,7 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
     else {
         uint32_t* o8 = cv_buf + g * 8;
 #pragma unroll
-        for (int i = 0; i < 8; i++) o8[i] = acc[i];
+        for (int i = 0; i < 8; i++) cv_st<FUSED>(o8 + i, acc[i]);
     }
     if constexpr (FUSED) {
         const uint32_t lane = threadIdx.x & 63;
@@ -430,7 +456,7 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
         const bool head = upper && (lane == 0 || pb != blob);
         const uint64_t H = __ballot(head), U = __ballot(upper);
         if (H == 0) return;  // wave-uniform
-        __threadfence();     // release: this wave's level-2 nodes, before any counter moves
+        wave_mem_drain();    // this wave's level-2 nodes are written through before any counter moves
         bool complete = false;
         if (head) {
             const uint64_t above = H & ~((2ull << lane) - 1);  // heads after this lane
@@ -438,20 +464,20 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
             const uint64_t run = (end == 64 ? ~0ull : ((1ull << end) - 1)) & ~((1ull << lane) - 1);
             const uint32_t cnt = (uint32_t)__popcll(U & run);
             const uint32_t total = (uint32_t)((n + 3) / 4);
-            const uint32_t old = atomicAdd(b.gdone + blob, cnt);
+            const uint32_t old = __hip_atomic_fetch_add(b.gdone + blob, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             BW_ASSERT(old + cnt <= total);
             complete = old + cnt == total;
             if (complete) b.gdone[blob] = 0;  // nothing else touches it in this pass
         }
         const uint64_t C = __ballot(complete);
-        if (C == 0) return;
-        __threadfence();  // acquire: the other waves' level-2 nodes of the completed blobs
+        if (C == 0) return;  // (the completing counters were read above: every level-2 node they
+                             // count was written through before its counter moved)
         for (uint64_t m = C; m; m &= m - 1) {  // blobs of > 64 leaves: the whole wave, one by one
             const int h = __builtin_ctzll(m);
             const uint64_t cb = bw_shfl64(blob, h), cl = bw_shfl64(len, h);
-            if (cl > (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) b3_upper_wave(cb, cl, b, cv_buf, cv_tmp, digests);
+            if (cl > (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) b3_upper_wave<true>(cb, cl, b, cv_buf, cv_tmp, digests);
         }
-        if (complete) b3_small_blob(blob, ctr, b, cv_buf, digests);  // 5..64 leaves; returns otherwise
+        if (complete) b3_small_blob<true>(blob, ctr, b, cv_buf, digests);  // 5..64 leaves; returns otherwise
     }
 }
 
@@ -462,6 +488,7 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
 // stack is then folded from the right onto the ragged tail (bits 0..1 of n).  The merge that
 // completes a power-of-two blob, or the last fold, carries ROOT.
 
+template <bool COH>
 __device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr, const BlobArrays& b,
                                               uint32_t* __restrict__ cv_buf, uint8_t* __restrict__ digests) {
     if (blob >= ctr[C_NBLOBS]) return;
@@ -475,30 +502,30 @@ __device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr
     for (uint32_t i = 0; i < m2; i++) {
         uint32_t carry[8];
 #pragma unroll
-        for (int w = 0; w < 8; w++) carry[w] = g[i * 8 + w];
+        for (int w = 0; w < 8; w++) carry[w] = cv_ld<COH>(g + i * 8 + w);
         for (uint32_t c = i + 1; (c & 1) == 0; c >>= 1) {
             uint32_t l[8];
             depth--;
 #pragma unroll
-            for (int w = 0; w < 8; w++) l[w] = g[depth * 8 + w];
+            for (int w = 0; w < 8; w++) l[w] = cv_ld<COH>(g + depth * 8 + w);
             b3_parent(l, carry, (!tail && i + 1 == m2 && depth == 0) ? B3_ROOT : 0, carry);
         }
 #pragma unroll
-        for (int w = 0; w < 8; w++) g[depth * 8 + w] = carry[w];
+        for (int w = 0; w < 8; w++) cv_st<COH>(g + depth * 8 + w, carry[w]);
         depth++;
     }
     uint32_t acc[8];
     bool have = false;
     if (tail) {
 #pragma unroll
-        for (int w = 0; w < 8; w++) acc[w] = g[m2 * 8 + w];
+        for (int w = 0; w < 8; w++) acc[w] = cv_ld<COH>(g + m2 * 8 + w);
         have = true;
     }
     while (depth > 0) {
         depth--;
         uint32_t t[8];
 #pragma unroll
-        for (int w = 0; w < 8; w++) t[w] = g[depth * 8 + w];
+        for (int w = 0; w < 8; w++) t[w] = cv_ld<COH>(g + depth * 8 + w);
         if (!have) {
 #pragma unroll
             for (int w = 0; w < 8; w++) acc[w] = t[w];
@@ -525,6 +552,7 @@ __device__ __forceinline__ void b3_shfl8(const uint32_t x[8], int src, uint32_t 
     for (int w = 0; w < 8; w++) out[w] = __shfl(x[w], src, 64);
 }
 
+template <bool COH>
 __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
                               uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests) {
     const uint32_t lane = threadIdx.x & 63;
@@ -538,7 +566,7 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
     for (int w = 0; w < 8; w++) acc[w] = 0;
     if (have && lane == 63) {
 #pragma unroll
-        for (int w = 0; w < 8; w++) acc[w] = src[cnt * 8 + w];
+        for (int w = 0; w < 8; w++) acc[w] = cv_ld<COH>(src + cnt * 8 + w);
     }
     int l = 2;
     while (cnt > 64) {  // never a root here: at least 65 nodes remain
@@ -552,13 +580,13 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
                 uint32_t L[8], R[8], P[8];
                 const uint64_t li = pair ? 2 * i : cnt - 1;
 #pragma unroll
-                for (int w = 0; w < 8; w++) L[w] = src[li * 8 + w];
+                for (int w = 0; w < 8; w++) L[w] = cv_ld<COH>(src + li * 8 + w);
 #pragma unroll
-                for (int w = 0; w < 8; w++) R[w] = pair ? src[(li + 1) * 8 + w] : acc[w];
+                for (int w = 0; w < 8; w++) R[w] = pair ? cv_ld<COH>(src + (li + 1) * 8 + w) : acc[w];
                 b3_parent(L, R, 0, P);
                 if (pair) {
 #pragma unroll
-                    for (int w = 0; w < 8; w++) dst[i * 8 + w] = P[w];
+                    for (int w = 0; w < 8; w++) cv_st<COH>(dst + i * 8 + w, P[w]);
                 } else {
 #pragma unroll
                     for (int w = 0; w < 8; w++) acc[w] = P[w];
@@ -567,10 +595,11 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
         }
         if (spine && !have && lane == 63) {
 #pragma unroll
-            for (int w = 0; w < 8; w++) acc[w] = src[(cnt - 1) * 8 + w];
+            for (int w = 0; w < 8; w++) acc[w] = cv_ld<COH>(src + (cnt - 1) * 8 + w);
         }
         have |= spine;
         // the wave reads the level it just wrote (same wave, same CU)
+        if constexpr (COH) wave_mem_drain();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -582,7 +611,7 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
     }
     uint32_t x[8];
 #pragma unroll
-    for (int w = 0; w < 8; w++) x[w] = lane < cnt ? src[lane * 8 + w] : 0;
+    for (int w = 0; w < 8; w++) x[w] = lane < cnt ? cv_ld<COH>(src + lane * 8 + w) : 0;
     for (;;) {
         const bool spine = cnt & 1;
         const uint32_t next = (uint32_t)(cnt / 2);
@@ -622,7 +651,7 @@ __global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArray
                                                   uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests,
                                                   uint32_t small_blocks) {
     if (blockIdx.x < small_blocks) {
-        b3_small_blob((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ctr, b, cv_buf, digests);
+        b3_small_blob<false>((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ctr, b, cv_buf, digests);
         return;
     }
     const uint64_t nblobs = ctr[C_NBLOBS];
@@ -631,7 +660,7 @@ __global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArray
          blob += waves) {
         const uint64_t len = b.len[blob];
         if (len <= (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) continue;  // k_b3_groups / the small path
-        b3_upper_wave(blob, len, b, cv_buf, cv_tmp, digests);
+        b3_upper_wave<false>(blob, len, b, cv_buf, cv_tmp, digests);
     }
 }
 

@@ -143,7 +143,7 @@ struct bw_ctx {
     uint64_t scan_small_bytes = SCAN_SMALL_BYTES;
     bool order_hash = false;  // BW_OPT_ORDER_HASH
     uint64_t cand_cap_forced = 0;
-    bool b3_fused = true;  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass
+    bool b3_fused = false;  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass (measured slower)
     int b3_loads = B3_LOADS_LINES;  // k_b3_lines: 1.07x fetch (pairs 1.42x), -6 % time isolated
     int scan_waves = 16;
     // latency stream: the small kernels between the two big passes (compaction, boundary

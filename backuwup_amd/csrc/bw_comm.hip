@@ -26,6 +26,12 @@ struct bw_comm {
     uint64_t cap = 0;                      // bucket capacity of the session (0 = not agreed yet)
     void* pin_send = nullptr;              // host transport: pinned staging, 2 x pin_cap
     size_t pin_cap = 0;
+    // The communicator's collectives run in the order the host issued them, whatever streams they
+    // were issued on: every one waits for the previous one's `tail`.  Contexts with batches in
+    // flight issue their exchanges on their own streams, and two RCCL operations of one
+    // communicator running at once on one GPU can wait on each other forever.
+    hipEvent_t tail = nullptr;
+    hipStream_t tail_stream = nullptr;
     std::string err;
 };
 
@@ -55,6 +61,8 @@ int bw::comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t b
     if (!bytes) return BW_OK;
     const int W = c->world;
     if (c->nccl) {
+        if (c->tail_stream && c->tail_stream != st && hipStreamWaitEvent(st, c->tail, 0) != hipSuccess)
+            return comm_err(c, err, "hipStreamWaitEvent on the communicator's last collective failed");
         if (int rc = nccl_chk(c, err, ncclGroupStart(), "ncclGroupStart")) return rc;
         for (int r = 0; r < W; r++) {
             ncclResult_t a = ncclSend((const uint8_t*)d_send + r * bytes, bytes, ncclUint8, r, c->nccl, st);
@@ -64,7 +72,10 @@ int bw::comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t b
                 return nccl_chk(c, err, a != ncclSuccess ? a : b, "ncclSend/ncclRecv");
             }
         }
-        return nccl_chk(c, err, ncclGroupEnd(), "ncclGroupEnd");
+        if (int rc = nccl_chk(c, err, ncclGroupEnd(), "ncclGroupEnd")) return rc;
+        if (hipEventRecord(c->tail, st) != hipSuccess) return comm_err(c, err, "hipEventRecord failed");
+        c->tail_stream = st;
+        return BW_OK;
     }
     // host transport: device -> pinned -> caller -> pinned -> device, synchronous on st
     const size_t total = (size_t)bytes * W;
@@ -130,7 +141,12 @@ extern "C" int bw_comm_init(int device, int rank, int world, const uint8_t id[BW
     c->world = world;
     ncclUniqueId u;
     memcpy(u.internal, id, BW_COMM_ID_BYTES);
+    if (hipEventCreateWithFlags(&c->tail, hipEventDisableTiming) != hipSuccess) {
+        delete c;
+        return BW_EHIP;
+    }
     if (ncclCommInitRank(&c->nccl, world, u, rank) != ncclSuccess) {  // blocks until every rank joined
+        hipEventDestroy(c->tail);
         delete c;
         return BW_ECOMM;
     }
@@ -155,7 +171,9 @@ extern "C" int bw_comm_init_host(int device, int rank, int world, bw_host_all_to
 extern "C" void bw_comm_destroy(bw_comm* c) {
     if (!c) return;
     hipSetDevice(c->device);
+    if (c->tail_stream) hipEventSynchronize(c->tail);
     if (c->nccl) ncclCommDestroy(c->nccl);
+    if (c->tail) hipEventDestroy(c->tail);
     if (c->pin_send) hipHostFree(c->pin_send);
     delete c;
 }

@@ -182,10 +182,11 @@ enum {
                                     and uploads the batch tables (the scan needs none of them), 0 =
                                     after the upload, 2 (default) = first for batches under
                                     BW_OPT_SCAN_SMALL_BYTES, where the host's share of a batch shows */
-    BW_OPT_B3_UPPER = 14         /* BLAKE3 levels above the 4-leaf groups: 1 (default) = inside the leaf
-                                    pass (k_b3_lines; the wave that finishes a blob's last group builds
-                                    them), 0 = a launch of their own after it (k_b3_upper).  Only the
-                                    aligned-line leaf pass (BW_OPT_B3_LOADS 2) fuses them */
+    BW_OPT_B3_UPPER = 14         /* BLAKE3 levels above the 4-leaf groups: 0 (default) = a launch of
+                                    their own after the leaf pass (k_b3_upper), 1 = inside the leaf pass
+                                    (k_b3_lines; the wave that finishes a blob's last group builds them)
+                                    -- measured 15-21 % slower on C1/C2/C4.  Only the aligned-line leaf
+                                    pass (BW_OPT_B3_LOADS 2) fuses them */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 

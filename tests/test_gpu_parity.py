@@ -33,14 +33,14 @@ KAT = {
 
 # every BLAKE3 test runs with each leaf-pass loader: 0 = one block ahead, 1 = 132-byte block pairs
 # (k_b3_groups), 2 = aligned 128-byte lines through registers (k_b3_lines, the default) with the
-# upper levels inside the leaf pass (BW_OPT_B3_UPPER 1, the default) or as a launch of their own
-@pytest.fixture(params=[(0, 0), (1, 0), (2, 1), (2, 0)], ids=["prefetch", "pairs", "lines", "lines-unfused"])
+# upper levels as a launch of their own (the default) or inside the leaf pass (BW_OPT_B3_UPPER 1)
+@pytest.fixture(params=[(0, 0), (1, 0), (2, 0), (2, 1)], ids=["prefetch", "pairs", "lines", "lines-fused"])
 def b3ctx(ctx, request):
     ctx.set_option(BW_OPT_B3_LOADS, request.param[0])
     ctx.set_option(BW_OPT_B3_UPPER, request.param[1])
     yield ctx
     ctx.set_option(BW_OPT_B3_LOADS, 2)  # the context defaults
-    ctx.set_option(BW_OPT_B3_UPPER, 1)
+    ctx.set_option(BW_OPT_B3_UPPER, 0)
 
 
 def test_blake3_kat(b3ctx):
