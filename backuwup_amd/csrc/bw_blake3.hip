@@ -369,21 +369,22 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
     const uint64_t blob = lo - 1;
     BW_ASSERT(lo >= 1 && blob < b.cap);
     const uint64_t start = b.start[blob], len = b.len[blob], gi = g - b.goff[blob];
-    BW_ASSERT(start + len <= b.data_len && gi * 4 * B3_LEAF_BYTES <= (len ? len - 1 : 0));
+    const uint32_t gs = b.gshift, G = 1u << gs;  // leaves per group (1, 2 or 4)
+    BW_ASSERT(gs <= 2 && start + len <= b.data_len && (gi << gs) * B3_LEAF_BYTES <= (len ? len - 1 : 0));
     const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
-    const uint64_t first = gi * 4;
-    const uint32_t k = (uint32_t)(n - first < 4 ? n - first : 4);
+    const uint64_t first = gi << gs;
+    const uint32_t k = (uint32_t)(n - first < G ? n - first : G);
     __shared__ uint32_t s_leaf[4][8][256];  // the group's leaf chaining values, word-major
     const int me = threadIdx.x;
-    const uint8_t* gp = data + start + gi * 4 * B3_LEAF_BYTES;
+    const uint8_t* gp = data + start + first * B3_LEAF_BYTES;
     const uint32_t o = (uint32_t)((uintptr_t)gp & 127);
     const uint32_t q = o >> 2, sh = o & 3;
     const uint32_t uq = __builtin_amdgcn_readfirstlane(q);
     uint32_t cv[8];
     if (__builtin_amdgcn_ballot_w64(q != uq) == 0) {
         // the whole wave at one line offset: whole aligned lines, each loaded once
-        const uint64_t rest = len - gi * 4 * B3_LEAF_BYTES;
-        const uint32_t glen = len == 0 ? 0 : (uint32_t)(rest < 4 * B3_LEAF_BYTES ? rest : 4 * B3_LEAF_BYTES);
+        const uint64_t rest = len - first * B3_LEAF_BYTES;
+        const uint32_t glen = len == 0 ? 0 : (uint32_t)(rest < G * B3_LEAF_BYTES ? rest : G * B3_LEAF_BYTES);
         const uint32_t nblk = glen == 0 ? 1 : (glen + 63) / 64;
         const uint4* lp = (const uint4*)(gp - o);
         const uint32_t nlines = glen == 0 ? 0 : (o + glen + 127) / 128;
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
         for (int i = 0; i < 8; i++) r[i] = s_leaf[2][i][me];
         b3_parent(acc, r, n == 3 ? B3_ROOT : 0, acc);
     }
-    if (n <= 4) store_digest(digests + blob * 32, acc);
+    if (n <= G) store_digest(digests + blob * 32, acc);
     else {
         uint32_t* o8 = cv_buf + g * 8;
 #pragma unroll
@@ -451,7 +452,7 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
         const uint32_t lane = threadIdx.x & 63;
         // the wave's lanes hold consecutive groups, so each blob is one run of lanes (live lanes
         // are a prefix of the wave)
-        const bool upper = live && n > 4;
+        const bool upper = live && n > G;
         const uint64_t pb = bw_shfl_up64(blob, 1);
         const bool head = upper && (lane == 0 || pb != blob);
         const uint64_t H = __ballot(head), U = __ballot(upper);
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
             const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : 64u;
             const uint64_t run = (end == 64 ? ~0ull : ((1ull << end) - 1)) & ~((1ull << lane) - 1);
             const uint32_t cnt = (uint32_t)__popcll(U & run);
-            const uint32_t total = (uint32_t)((n + 3) / 4);
+            const uint32_t total = (uint32_t)((n + G - 1) >> gs);
             const uint32_t old = __hip_atomic_fetch_add(b.gdone + blob, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             BW_ASSERT(old + cnt <= total);
             complete = old + cnt == total;
@@ -494,10 +495,11 @@ __device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr
     if (blob >= ctr[C_NBLOBS]) return;
     const uint64_t len = b.len[blob];
     const uint64_t n = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
-    if (n <= 4 || n > B3_SMALL_LEAVES) return;
+    const uint32_t gs = b.gshift;
+    if (n <= (1u << gs) || n > B3_SMALL_LEAVES) return;
     uint32_t* g = cv_buf + b.goff[blob] * 8;
-    const uint32_t m2 = (uint32_t)(n / 4);
-    const bool tail = (n & 3) != 0;
+    const uint32_t m2 = (uint32_t)(n >> gs);                 // complete group nodes
+    const bool tail = (n & ((1u << gs) - 1)) != 0;           // the ragged last group's merged node
     uint32_t depth = 0;
     for (uint32_t i = 0; i < m2; i++) {
         uint32_t carry[8];
@@ -559,8 +561,9 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
     const uint64_t n = (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;  // > B3_SMALL_LEAVES
     uint32_t* src = cv_buf + b.goff[blob] * 8;
     uint32_t* dst = cv_tmp + b.goff[blob] * 8;
-    uint64_t cnt = n / 4;  // complete level-2 nodes; the ragged tail's merged node follows them
-    bool have = (n & 3) != 0;
+    const uint32_t gs = b.gshift;
+    uint64_t cnt = n >> gs;  // complete group nodes (level gs); the ragged tail's merged node follows them
+    bool have = (n & ((1u << gs) - 1)) != 0;
     uint32_t acc[8];
 #pragma unroll
     for (int w = 0; w < 8; w++) acc[w] = 0;
@@ -568,7 +571,7 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
 #pragma unroll
         for (int w = 0; w < 8; w++) acc[w] = cv_ld<COH>(src + cnt * 8 + w);
     }
-    int l = 2;
+    int l = (int)gs;
     while (cnt > 64) {  // never a root here: at least 65 nodes remain
         const bool spine = cnt & 1;
         const uint64_t next = cnt / 2;
@@ -727,7 +730,7 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     if (between) hipEventRecord(between, st);
     if (upper != st) hipStreamWaitEvent(upper, between, 0);
     st = upper;
-    if (max_leaves > 4 && !fused) {
+    if (max_leaves > (1 << b.gshift) && !fused) {
         const uint64_t small = (max_blobs + 255) / 256;
         uint64_t big = max_leaves > (int)B3_SMALL_LEAVES ? (max_blobs + 3) / 4 : 0;  // 4 waves per block
         if (big > 4096) big = 4096;

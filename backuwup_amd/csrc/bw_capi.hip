@@ -143,6 +143,7 @@ struct bw_ctx {
     uint64_t scan_small_bytes = SCAN_SMALL_BYTES;
     bool order_hash = false;  // BW_OPT_ORDER_HASH
     uint64_t cand_cap_forced = 0;
+    int b3_group = 4;   // BW_OPT_B3_GROUP: leaves per BLAKE3 group of the aligned-line leaf pass (0 = auto)
     bool b3_fused = false;  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass (measured slower)
     int b3_loads = B3_LOADS_LINES;  // k_b3_lines: 1.07x fetch (pairs 1.42x), -6 % time isolated
     int scan_waves = 16;
@@ -675,6 +676,10 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             if (__builtin_popcountll(v) < 2 || v >= (2u << BW_N_STAGES)) return BW_EINVAL;
             c->prof_mask = (uint32_t)v;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
+        case BW_OPT_B3_GROUP:
+            if (v != 1 && v != 2 && v != 4) return BW_EINVAL;
+            c->b3_group = (int)v;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_B3_UPPER:
             if (v > 1) return BW_EINVAL;
             c->b3_fused = v == 1;
@@ -1012,7 +1017,9 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     }, nf);
     const uint64_t max_blobs = tot.max_blobs, fb_total = tot.fb, max_blob_len = tot.max_blob_len,
                    total_len = tot.total_len;
-    const uint64_t max_groups = total_len / 4096 + max_blobs + 1;
+    // leaves per BLAKE3 group (one lane each): 4, or fewer for the aligned-line pass on request
+    const uint32_t gshift = c->b3_loads != B3_LOADS_LINES ? 2 : (c->b3_group == 1 ? 0 : c->b3_group == 2 ? 1 : 2);
+    const uint64_t max_groups = total_len / (1024ull << gshift) + max_blobs + 1;  // 1 KiB BLAKE3 leaves
     const int max_leaves = (int)std::min<uint64_t>((max_blob_len + 1023) / 1024, 1u << 30);
     if (ncf != ncf_pre || max_blobs != mb_pre) return BW_ESTATE;  // the same sums as the pre-count; cannot differ
 
@@ -1083,7 +1090,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
 
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len,
-                 c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr};
+                 c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr, gshift};
 
     // ---- chunking (the scan on the context stream, the latency-bound kernels after it on `lat`)
     const bool split = c->lat_split;

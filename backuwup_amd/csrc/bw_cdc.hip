@@ -805,9 +805,9 @@ void launch_resolve(hipStream_t st, const uint8_t* data, uint64_t data_len, cons
 
 // ======================================================================== assembly
 
-__device__ __forceinline__ uint64_t groups_of(uint64_t len) {
+__device__ __forceinline__ uint64_t groups_of(uint64_t len, uint32_t gshift) {
     const uint64_t leaves = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;
-    return (leaves + 3) / 4;
+    return (leaves + (1u << gshift) - 1) >> gshift;
 }
 
 // Emit (or just count) the blobs of unit u.  Returns blob and group counts.
@@ -832,7 +832,7 @@ __device__ void unit_blobs(const UnitDesc& u, const SegDesc* segs, const CFileDe
             b.fend[k] = fend;
         }
         nb++;
-        ng += groups_of(len);
+        ng += groups_of(len, b.gshift);
     };
     if (u.kind == 0) { emit(u.start, u.start + u.len, 0, u.start + u.len); return; }
     const SegDesc sd = segs[u.seg];

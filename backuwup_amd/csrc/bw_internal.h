@@ -99,6 +99,7 @@ struct BlobArrays {
     uint64_t data_len;  // bytes of the batch buffer (BW_DEBUG checks)
     uint32_t* gdone = nullptr;  // per blob: BLAKE3 groups finished (zero between passes); null = the
                                 // upper levels run as a launch of their own (k_b3_upper)
+    uint32_t gshift = 2;        // log2 of the leaves per BLAKE3 group (k_b3_lines: 0..2; others: 2)
 };
 
 // ------------------------------------------------------------------ launchers (bw_cdc.hip)

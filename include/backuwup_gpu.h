@@ -182,11 +182,14 @@ enum {
                                     and uploads the batch tables (the scan needs none of them), 0 =
                                     after the upload, 2 (default) = first for batches under
                                     BW_OPT_SCAN_SMALL_BYTES, where the host's share of a batch shows */
-    BW_OPT_B3_UPPER = 14         /* BLAKE3 levels above the 4-leaf groups: 0 (default) = a launch of
+    BW_OPT_B3_UPPER = 14,        /* BLAKE3 levels above the 4-leaf groups: 0 (default) = a launch of
                                     their own after the leaf pass (k_b3_upper), 1 = inside the leaf pass
                                     (k_b3_lines; the wave that finishes a blob's last group builds them)
                                     -- measured 15-21 % slower on C1/C2/C4.  Only the aligned-line leaf
                                     pass (BW_OPT_B3_LOADS 2) fuses them */
+    BW_OPT_B3_GROUP = 15         /* BLAKE3 leaves per lane of the aligned-line leaf pass: 4 (default),
+                                    2 or 1.  Smaller groups cut the pass's last partial round of
+                                    waves on small batches (the levels above move to the upper pass) */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 

@@ -544,14 +544,15 @@ def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
     assert got[0][2][3].all()  # batch 2 repeats batch 0 on rank 0
 
 
-@pytest.mark.parametrize("scan_waves,latency,loads,upper", [(8, 0, 1, 0), (16, 1, 1, 0), (8, 1, 0, 0), (16, 0, 0, 0),
-                                                           (16, 0, 2, 1), (8, 1, 2, 1), (16, 0, 2, 0)])
-def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads, upper):
+@pytest.mark.parametrize("scan_waves,latency,loads,upper,group",
+                         [(8, 0, 1, 0, 4), (16, 1, 1, 0, 4), (8, 1, 0, 0, 4), (16, 0, 0, 0, 4), (16, 0, 2, 1, 4),
+                          (8, 1, 2, 1, 2), (16, 0, 2, 0, 4), (16, 0, 2, 0, 2), (8, 0, 2, 0, 1)])
+def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads, upper, group):
     """The scheduling variants (8-wave scan blocks, the high-priority latency stream, both BLAKE3
     load modes) change only where and when kernels run: results equal the oracle, including two
     batches in flight on two contexts that share an index."""
     import torch
-    from backuwup_amd._lib import BW_OPT_B3_LOADS, BW_OPT_B3_UPPER, BW_OPT_LATENCY_STREAM, BW_OPT_SCAN_WAVES
+    from backuwup_amd._lib import BW_OPT_B3_GROUP, BW_OPT_B3_LOADS, BW_OPT_B3_UPPER, BW_OPT_LATENCY_STREAM, BW_OPT_SCAN_WAVES
     data, offs, lens = tree_corpus(80 << 20, seed=21, max_file=20 << 20)
     batches = _slices(data, offs, lens, [(0, len(lens) // 2), (len(lens) // 2, len(lens))]) * 2
     want = oracle_session(oracle, batches)
@@ -567,6 +568,7 @@ def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads, upper):
             c.set_option(BW_OPT_LATENCY_STREAM, latency)
             c.set_option(BW_OPT_B3_LOADS, loads)
             c.set_option(BW_OPT_B3_UPPER, upper)
+            c.set_option(BW_OPT_B3_GROUP, group)
         cs[0].index_reset()
         tickets = [cs[k % 2].submit_device(t.data_ptr(), d.size, o, l) for k, (t, (d, o, l)) in enumerate(zip(devs, batches))]
         for k, t in enumerate(tickets):
