@@ -143,7 +143,7 @@ struct bw_ctx {
     uint64_t scan_small_bytes = SCAN_SMALL_BYTES;
     bool order_hash = false;  // BW_OPT_ORDER_HASH
     uint64_t cand_cap_forced = 0;
-    int b3_group = 4;   // BW_OPT_B3_GROUP: leaves per BLAKE3 group of the aligned-line leaf pass (0 = auto)
+    int b3_group = 0;   // BW_OPT_B3_GROUP: leaves per BLAKE3 group of the aligned-line leaf pass (0 = auto)
     bool b3_fused = false;  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass (measured slower)
     int b3_loads = B3_LOADS_LINES;  // k_b3_lines: 1.07x fetch (pairs 1.42x), -6 % time isolated
     int scan_waves = 16;
@@ -677,7 +677,7 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             c->prof_mask = (uint32_t)v;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_B3_GROUP:
-            if (v != 1 && v != 2 && v != 4) return BW_EINVAL;
+            if (v != 0 && v != 1 && v != 2 && v != 4) return BW_EINVAL;
             c->b3_group = (int)v;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_B3_UPPER:
@@ -1017,8 +1017,15 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     }, nf);
     const uint64_t max_blobs = tot.max_blobs, fb_total = tot.fb, max_blob_len = tot.max_blob_len,
                    total_len = tot.total_len;
-    // leaves per BLAKE3 group (one lane each): 4, or fewer for the aligned-line pass on request
-    const uint32_t gshift = c->b3_loads != B3_LOADS_LINES ? 2 : (c->b3_group == 1 ? 0 : c->b3_group == 2 ? 1 : 2);
+    // Leaves per BLAKE3 group (one lane each) of the aligned-line leaf pass.  Auto: 2 for small
+    // batches (under BW_OPT_SCAN_SMALL_BYTES: the pass's last partial round of waves is a large share
+    // of it) and for batches of small blobs (mean blob bound under 128 KiB: fewer lanes idle in a
+    // blob's ragged last group); 4 otherwise (the upper levels' extra work is not paid back).
+    // Measured (profiles/r03/s05_group): C1 one batch in flight +3 %, C1 three +1.7 %, C4 +9.5 %,
+    // C2 -1.3 % with 2.
+    const bool small_groups = data_len < c->scan_small_bytes || total_len < max_blobs * (128ull << 10);
+    const int grp = c->b3_group ? c->b3_group : (small_groups ? 2 : 4);
+    const uint32_t gshift = c->b3_loads != B3_LOADS_LINES ? 2 : (grp == 1 ? 0 : grp == 2 ? 1 : 2);
     const uint64_t max_groups = total_len / (1024ull << gshift) + max_blobs + 1;  // 1 KiB BLAKE3 leaves
     const int max_leaves = (int)std::min<uint64_t>((max_blob_len + 1023) / 1024, 1u << 30);
     if (ncf != ncf_pre || max_blobs != mb_pre) return BW_ESTATE;  // the same sums as the pre-count; cannot differ

@@ -35,8 +35,8 @@ KAT = {
 # (k_b3_groups), 2 = aligned 128-byte lines through registers (k_b3_lines, the default) with the
 # upper levels as a launch of their own (the default) or inside the leaf pass (BW_OPT_B3_UPPER 1)
 # and 4, 2 or 1 leaves per lane (BW_OPT_B3_GROUP)
-@pytest.fixture(params=[(0, 0, 4), (1, 0, 4), (2, 0, 4), (2, 1, 4), (2, 0, 2), (2, 0, 1), (2, 1, 1)],
-                ids=["prefetch", "pairs", "lines", "lines-fused", "lines-g2", "lines-g1", "lines-fused-g1"])
+@pytest.fixture(params=[(0, 0, 4), (1, 0, 4), (2, 0, 0), (2, 0, 4), (2, 1, 4), (2, 0, 2), (2, 0, 1), (2, 1, 1)],
+                ids=["prefetch", "pairs", "lines", "lines-g4", "lines-fused", "lines-g2", "lines-g1", "lines-fused-g1"])
 def b3ctx(ctx, request):
     ctx.set_option(BW_OPT_B3_LOADS, request.param[0])
     ctx.set_option(BW_OPT_B3_UPPER, request.param[1])
@@ -44,7 +44,7 @@ def b3ctx(ctx, request):
     yield ctx
     ctx.set_option(BW_OPT_B3_LOADS, 2)  # the context defaults
     ctx.set_option(BW_OPT_B3_UPPER, 0)
-    ctx.set_option(BW_OPT_B3_GROUP, 4)
+    ctx.set_option(BW_OPT_B3_GROUP, 0)
 
 
 def test_blake3_kat(b3ctx):
