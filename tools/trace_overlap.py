@@ -49,7 +49,8 @@ def main():
     path, warm, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     rows = list(csv.DictReader(open(path)))
     rows = [r for r in rows if "bw::" in r["Kernel_Name"]]
-    scans, b3 = intervals(rows, "k_scan"), intervals(rows, "k_b3_groups")
+    leaf = "k_b3_lines" if any("k_b3_lines" in r["Kernel_Name"] for r in rows) else "k_b3_groups"
+    scans, b3 = intervals(rows, "k_scan"), intervals(rows, leaf)
     lo, hi = scans[warm][0], b3[warm + steps - 1][1]
     span = hi - lo
     us = union(clip(scans, lo, hi))
