@@ -334,7 +334,7 @@ __device__ __forceinline__ void wave_mem_drain() { asm volatile("s_waitcnt vmcnt
 template <bool COH>
 __device__ __forceinline__ void b3_small_blob(uint64_t blob, const uint64_t* ctr, const BlobArrays& b,
                                               uint32_t* __restrict__ cv_buf, uint8_t* __restrict__ digests);
-template <bool COH>
+template <bool COH, int NT = 64>
 __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
                               uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests);
 
@@ -554,10 +554,14 @@ __device__ __forceinline__ void b3_shfl8(const uint32_t x[8], int src, uint32_t 
     for (int w = 0; w < 8; w++) out[w] = __shfl(x[w], src, 64);
 }
 
-template <bool COH>
+// NT = 256: the whole workgroup builds the levels that pass through global memory (255 parents per
+// round instead of 63, synchronized by the workgroup barrier), and its last wave takes the levels
+// from 64 nodes down.  Every thread of the workgroup calls it for the same blobs in the same order.
+template <bool COH, int NT>
 __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const BlobArrays& b, uint32_t* __restrict__ cv_buf,
                               uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests) {
-    const uint32_t lane = threadIdx.x & 63;
+    static_assert(NT == 64 || NT == 256, "a wave or a 4-wave workgroup per blob");
+    const uint32_t lane = threadIdx.x & 63, t = threadIdx.x & (NT - 1);
     const uint64_t n = (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;  // > B3_SMALL_LEAVES
     uint32_t* src = cv_buf + b.goff[blob] * 8;
     uint32_t* dst = cv_tmp + b.goff[blob] * 8;
@@ -567,7 +571,7 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
     uint32_t acc[8];
 #pragma unroll
     for (int w = 0; w < 8; w++) acc[w] = 0;
-    if (have && lane == 63) {
+    if (have && t == NT - 1) {
 #pragma unroll
         for (int w = 0; w < 8; w++) acc[w] = cv_ld<COH>(src + cnt * 8 + w);
     }
@@ -575,10 +579,10 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
     while (cnt > 64) {  // never a root here: at least 65 nodes remain
         const bool spine = cnt & 1;
         const uint64_t next = cnt / 2;
-        for (uint64_t base = 0; base < next; base += 63) {
-            const uint64_t i = base + lane;
-            const bool pair = lane < 63 && i < next;
-            const bool fold = lane == 63 && base == 0 && spine && have;
+        for (uint64_t base = 0; base < next; base += NT - 1) {
+            const uint64_t i = base + t;
+            const bool pair = t < NT - 1 && i < next;
+            const bool fold = t == NT - 1 && base == 0 && spine && have;
             if (pair || fold) {
                 uint32_t L[8], R[8], P[8];
                 const uint64_t li = pair ? 2 * i : cnt - 1;
@@ -596,22 +600,28 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
                 }
             }
         }
-        if (spine && !have && lane == 63) {
+        if (spine && !have && t == NT - 1) {
 #pragma unroll
             for (int w = 0; w < 8; w++) acc[w] = cv_ld<COH>(src + (cnt - 1) * 8 + w);
         }
         have |= spine;
-        // the wave reads the level it just wrote (same wave, same CU)
+        // the wave (workgroup) reads the level it just wrote (same CU)
         if constexpr (COH) wave_mem_drain();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if constexpr (NT == 64) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        } else {
+            __syncthreads();
+        }
         uint32_t* t = src;
         src = dst;
         dst = t;
         cnt = next;
         l++;
     }
+    // from 64 nodes down: the wave that holds the spine (thread NT - 1 = its lane 63)
+    if (NT > 64 && t / 64 != (NT - 1) / 64) return;
     uint32_t x[8];
 #pragma unroll
     for (int w = 0; w < 8; w++) x[w] = lane < cnt ? cv_ld<COH>(src + lane * 8 + w) : 0;
@@ -650,25 +660,41 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
 // The upper levels of every blob with more than 4 leaves in one launch: blocks [0, small_blocks)
 // run k_b3_small's lane-per-blob stacks, the rest run b3_upper_wave over the blobs with more than
 // B3_SMALL_LEAVES leaves, so the two latency-bound passes overlap instead of running back to back.
+//
+// Blobs of > 64 leaves get a wave each, or with `per_block` (batches of few blobs, where the upper
+// levels are latency on the critical path rather than throughput) a 4-wave workgroup each: a 3 MiB
+// chunk at 2 leaves per group is 1,536 nodes, 26 rounds of 63 parents through global memory for a
+// wave and 9 of 255 for the workgroup.
 __global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArrays b, uint32_t* __restrict__ cv_buf,
                                                   uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests,
-                                                  uint32_t small_blocks) {
+                                                  uint32_t small_blocks, uint32_t per_block) {
     if (blockIdx.x < small_blocks) {
         b3_small_blob<false>((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ctr, b, cv_buf, digests);
         return;
     }
     const uint64_t nblobs = ctr[C_NBLOBS];
+    if (per_block) {
+        for (uint64_t blob = blockIdx.x - small_blocks; blob < nblobs; blob += gridDim.x - small_blocks) {
+            const uint64_t len = b.len[blob];  // workgroup-uniform
+            if (len <= (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) continue;
+            b3_upper_wave<false, 256>(blob, len, b, cv_buf, cv_tmp, digests);
+        }
+        return;
+    }
     const uint64_t waves = (uint64_t)(gridDim.x - small_blocks) * (blockDim.x / 64);
     for (uint64_t blob = (uint64_t)(blockIdx.x - small_blocks) * (blockDim.x / 64) + threadIdx.x / 64; blob < nblobs;
          blob += waves) {
         const uint64_t len = b.len[blob];
         if (len <= (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) continue;  // k_b3_groups / the small path
-        b3_upper_wave<false>(blob, len, b, cv_buf, cv_tmp, digests);
+        b3_upper_wave<false, 64>(blob, len, b, cv_buf, cv_tmp, digests);
     }
 }
 
 #ifndef BW_B3_LINES_MINW
 #define BW_B3_LINES_MINW 3  // blocks of 256 per CU: 3 = 3 waves per SIMD (168 VGPRs; at 4 the ring spills)
+#endif
+#ifndef B3_UPPER_BLOCK_BLOBS
+#define B3_UPPER_BLOCK_BLOBS 8192  // k_b3_upper: a workgroup per large blob up to this many blobs (bound)
 #endif
 
 // Roofline calibration: the leaf pass's compression (b3_compress, the same instruction forms)
@@ -732,10 +758,12 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     st = upper;
     if (max_leaves > (1 << b.gshift) && !fused) {
         const uint64_t small = (max_blobs + 255) / 256;
-        uint64_t big = max_leaves > (int)B3_SMALL_LEAVES ? (max_blobs + 3) / 4 : 0;  // 4 waves per block
+        // few blobs (bound <= B3_UPPER_BLOCK_BLOBS): a workgroup per blob; many: a wave per blob
+        const bool per_block = max_blobs <= B3_UPPER_BLOCK_BLOBS;
+        uint64_t big = max_leaves > (int)B3_SMALL_LEAVES ? (per_block ? max_blobs : (max_blobs + 3) / 4) : 0;
         if (big > 4096) big = 4096;
         hipLaunchKernelGGL(k_b3_upper, dim3((unsigned)(small + big)), dim3(256), 0, st, ctr, b, cv_buf, cv_tmp, digests,
-                           (uint32_t)small);
+                           (uint32_t)small, (uint32_t)per_block);
     }
 }
 
