@@ -662,9 +662,11 @@ __device__ __forceinline__ void b3_upper_wave(uint64_t blob, uint64_t len, const
 // B3_SMALL_LEAVES leaves, so the two latency-bound passes overlap instead of running back to back.
 //
 // Blobs of > 64 leaves get a wave each, or with `per_block` (batches of few blobs, where the upper
-// levels are latency on the critical path rather than throughput) a 4-wave workgroup each: a 3 MiB
-// chunk at 2 leaves per group is 1,536 nodes, 26 rounds of 63 parents through global memory for a
-// wave and 9 of 255 for the workgroup.
+// levels are latency on the critical path rather than throughput) every blob above one group gets a
+// 4-wave workgroup: a 3 MiB chunk at 2 leaves per group is 1,536 nodes, 26 rounds of 63 parents
+// through global memory for a wave and 9 of 255 for the workgroup, and a 64-leaf blob's 32 nodes
+// take 5 register levels instead of a lane's 31 serial merges (C1: the longest chain of the pass,
+// ~75 us of 2.3 us compressions).
 __global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArrays b, uint32_t* __restrict__ cv_buf,
                                                   uint32_t* __restrict__ cv_tmp, uint8_t* __restrict__ digests,
                                                   uint32_t small_blocks, uint32_t per_block) {
@@ -673,10 +675,11 @@ __global__ __launch_bounds__(256) void k_b3_upper(const uint64_t* ctr, BlobArray
         return;
     }
     const uint64_t nblobs = ctr[C_NBLOBS];
-    if (per_block) {
+    if (per_block) {  // every blob above one group, small ones included (no lane-per-blob stacks)
+        const uint64_t one_group = (uint64_t)B3_LEAF_BYTES << b.gshift;
         for (uint64_t blob = blockIdx.x - small_blocks; blob < nblobs; blob += gridDim.x - small_blocks) {
             const uint64_t len = b.len[blob];  // workgroup-uniform
-            if (len <= (uint64_t)B3_SMALL_LEAVES * B3_LEAF_BYTES) continue;
+            if (len <= one_group) continue;   // rooted in the leaf pass
             b3_upper_wave<false, 256>(blob, len, b, cv_buf, cv_tmp, digests);
         }
         return;
@@ -757,10 +760,11 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
     if (upper != st) hipStreamWaitEvent(upper, between, 0);
     st = upper;
     if (max_leaves > (1 << b.gshift) && !fused) {
-        const uint64_t small = (max_blobs + 255) / 256;
-        // few blobs (bound <= B3_UPPER_BLOCK_BLOBS): a workgroup per blob; many: a wave per blob
+        // few blobs (bound <= B3_UPPER_BLOCK_BLOBS): a workgroup per blob; many: a lane per small
+        // blob and a wave per large one
         const bool per_block = max_blobs <= B3_UPPER_BLOCK_BLOBS;
-        uint64_t big = max_leaves > (int)B3_SMALL_LEAVES ? (per_block ? max_blobs : (max_blobs + 3) / 4) : 0;
+        const uint64_t small = per_block ? 0 : (max_blobs + 255) / 256;
+        uint64_t big = per_block ? max_blobs : (max_leaves > (int)B3_SMALL_LEAVES ? (max_blobs + 3) / 4 : 0);
         if (big > 4096) big = 4096;
         hipLaunchKernelGGL(k_b3_upper, dim3((unsigned)(small + big)), dim3(256), 0, st, ctr, b, cv_buf, cv_tmp, digests,
                            (uint32_t)small, (uint32_t)per_block);
