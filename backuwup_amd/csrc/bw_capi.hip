@@ -811,16 +811,30 @@ static int validate_batch(bw_ctx* c, uint64_t data_len, const uint64_t* foff, co
 // Queue the host copies of a batch's results behind its kernels on the context stream: the
 // counters and the first res_n packed records (about twice the previous batch's blob count: a
 // guess, the rest is copied at the wait if the batch has more) into the slot's pinned buffer.
-static int stage_results(bw_ctx* c, Slot& s) {
-    const uint64_t want = std::min<uint64_t>(s.max_blobs, std::max<uint64_t>(1024, 2 * c->last_n + 1024));
+// The results a bw_wait returns without touching the device: the counters and the first `want`
+// records in the slot's pinned buffer.  stage_prepare sizes the buffer (before the batch's last
+// kernel, which may write it directly: `*zero_copy`); stage_results copies what that kernel did not
+// write and records `done`.
+constexpr uint64_t ZERO_COPY_MAX = 4ull << 20;  // larger result sets go by DMA copy
+static int stage_prepare(bw_ctx* c, Slot& s, uint64_t max_blobs, uint64_t* want_out, bool* zero_copy) {
+    const uint64_t want = std::min<uint64_t>(max_blobs, std::max<uint64_t>(1024, 2 * c->last_n + 1024));
     if (s.res.cap < C_COUNT * 8 + want * sizeof(bw_blob)) {
         HIPCHK(c, hipEventSynchronize(s.done));  // the buffer may still be the target of the slot's last copy
         if (int rc = ensure_host(c, s.res, C_COUNT * 8 + want * sizeof(bw_blob))) return rc;
     }
-    uint8_t* h = (uint8_t*)s.res.p;
-    // one copy: the counters and the first `want` records lie back to back on the device (two
-    // copies cost the stream a ~12 us gap between them with one batch in flight, profiles/r03)
-    HIPCHK(c, hipMemcpyAsync(h, s.res_dev.p, CTR_BYTES + want * sizeof(bw_blob), hipMemcpyDeviceToHost, c->stream));
+    *want_out = want;
+    if (zero_copy) *zero_copy = CTR_BYTES + want * sizeof(bw_blob) <= ZERO_COPY_MAX;
+    return BW_OK;
+}
+
+static int stage_results(bw_ctx* c, Slot& s, bool written = false, uint64_t want = 0) {
+    if (!written) {
+        if (int rc = stage_prepare(c, s, s.max_blobs, &want, nullptr)) return rc;
+        // one copy: the counters and the first `want` records lie back to back on the device (two
+        // copies cost the stream a ~12 us gap between them with one batch in flight, profiles/r03)
+        HIPCHK(c, hipMemcpyAsync(s.res.p, s.res_dev.p, CTR_BYTES + want * sizeof(bw_blob), hipMemcpyDeviceToHost,
+                                 c->stream));
+    }
     HIPCHK(c, hipEventRecord(s.done, c->stream));
     s.res_n = want;
     return BW_OK;
@@ -1169,8 +1183,15 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     }
     phase(4);
     prof_mark(c, BW_STAGE_PACK, lat);
+    // small result sets are written to the slot's pinned buffer by k_pack itself (no copy on the
+    // stream: pack -> copy cost a 12 us gap with one batch in flight, profiles/r03/s07_upper_block)
+    uint64_t want = 0;
+    bool zero_copy = false;
+    if (stage)
+        if (int r5 = stage_prepare(c, s, max_blobs, &want, &zero_copy)) return r5;
     launch_pack(lat, ctr, b, d_fstart, P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
-                slot_records(s), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr);
+                slot_records(s), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr,
+                zero_copy ? (uint8_t*)s.res.p : nullptr, want);
     if (split) {  // the batch ends on the context stream (the caller's order)
         prof_mark(c, BW_N_STAGES, lat);
         HIPCHK(c, hipEventRecord(c->e_end, lat));
@@ -1182,7 +1203,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     s.max_blobs = max_blobs;
     s.dedup = do_dedup;
     if (stage)
-        if (int r5 = stage_results(c, s)) return r5;
+        if (int r5 = stage_results(c, s, zero_copy, want)) return r5;
     phase(5);
     c->host_batches += c->host_timing;
     return BW_OK;

@@ -177,9 +177,10 @@ void launch_bucket_expand(hipStream_t st, const uint64_t* counts, uint32_t n_src
 void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, const uint64_t* counts,
                            uint32_t n_owners, uint64_t cap, uint8_t* is_dup, uint8_t* packed = nullptr);
 // dstate (may be null): the index state snapshot into ctr[C_COLLIDE, C_NUNIQUE, C_IX_*]
+// host (may be null): pinned memory that also receives ctr and the first host_n records
 void launch_pack(hipStream_t st, uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
                  const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs,
-                 const uint64_t* dstate);
+                 const uint64_t* dstate, uint8_t* host = nullptr, uint64_t host_n = 0);
 void launch_index_snapshot(hipStream_t st, const uint64_t* dstate, uint64_t* ctr);
 
 // ------------------------------------------------------------------ sealing (bw_seal.hip)
