@@ -359,15 +359,19 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
     const bool live = g0 < ng;
     if (FUSED ? (ng == 0 || g0 - (threadIdx.x & 63) >= ng) : !live) return;
     const uint64_t g = live ? g0 : ng - 1;
-    const uint64_t nb = ctr[C_NBLOBS];
-    uint64_t lo = 0, hi = nb;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (b.goff[mid] <= g) lo = mid + 1;
-        else hi = mid;
+    uint64_t blob;
+    if (b.gblob) {
+        blob = b.gblob[g];
+    } else {
+        uint64_t lo = 0, hi = ctr[C_NBLOBS];
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (b.goff[mid] <= g) lo = mid + 1;
+            else hi = mid;
+        }
+        blob = lo - 1;
     }
-    const uint64_t blob = lo - 1;
-    BW_ASSERT(lo >= 1 && blob < b.cap);
+    BW_ASSERT(blob < b.cap && b.goff[blob] <= g);
     const uint64_t start = b.start[blob], len = b.len[blob], gi = g - b.goff[blob];
     const uint32_t gs = b.gshift, G = 1u << gs;  // leaves per group (1, 2 or 4)
     BW_ASSERT(gs <= 2 && start + len <= b.data_len && (gi << gs) * B3_LEAF_BYTES <= (len ? len - 1 : 0));

@@ -107,6 +107,7 @@ struct bw_ctx {
     DevBuf meta, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
     DevBuf b_gdone;  // per blob: BLAKE3 groups finished (fused upper levels); zero between passes
+    DevBuf b_gblob;  // per BLAKE3 group: its blob (k_cut_hash -> the aligned-line leaf pass)
     DevBuf cv, cv2, data, scratch, ucnt, ubtot;
     DevBuf bk_blk, bk_pack, bk_v;  // multi-GPU exchange buckets (bw_partition_buckets, ...)
     // bw_exchange_dedup: my buckets and the ones received, their source positions, the counts
@@ -283,13 +284,15 @@ static int make_masks(uint32_t mn, uint32_t av, uint32_t mx, Masks* mk) {
     return BW_OK;
 }
 
-static uint64_t seg_len_for(const Masks& mk) {
+static uint64_t seg_len_for(const Masks& mk, bool small_batch) {
     // Segments are a multiple of max_size so that chains through data without candidates
     // (e.g. zeros: every chunk is exactly max) stay phase-aligned and merge immediately; the
-    // multiple keeps a segment's own cuts within CHAIN_CAP / 2.
+    // multiple keeps a segment's own cuts within CHAIN_CAP / 2.  Small batches take at most 2 x max:
+    // their chain walk is latency on the critical path (one wave walks a segment's cuts one after
+    // another, ~1.7 us each), and more, shorter segments walk in parallel.
     uint64_t k = (uint64_t)(CHAIN_CAP / 2) * std::min<uint64_t>(mk.s0, mk.max) / mk.max;
     if (k < 1) k = 1;
-    if (k > 8) k = 8;
+    if (k > (small_batch ? 2 : 8)) k = small_batch ? 2 : 8;
     return k * mk.max;
 }
 
@@ -559,7 +562,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
     DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->meta,
                      &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
-                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->b_gdone, &c->cv, &c->cv2,
+                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->b_gdone, &c->b_gblob, &c->cv, &c->cv2,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
                      &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage,
@@ -925,7 +928,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         if (int r6 = enqueue_scan()) return r6;
 
     // ---- host metadata: CDC files, segments, canonical units
-    const uint64_t L = seg_len_for(mk);
+    const uint64_t L = seg_len_for(mk, data_len < c->scan_small_bytes);
     // every chunk but a file's last is >= min(2*(min/2), max) bytes (max < min is legal in the crate)
     const uint64_t min_chunk = std::min<uint64_t>(mk.s0, mk.max);
     // Two passes over file ranges (in parallel for large batches: C4's million files took ~4 ms on
@@ -1071,6 +1074,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         if (!rc) HIPCHK(c, hipMemsetAsync(c->b_gdone.p, 0, c->b_gdone.cap, c->stream));
     }
     rc |= ensure(c, c->cv, max_groups * 32);
+    rc |= ensure(c, c->b_gblob, max_groups * 4);
     rc |= ensure(c, c->cv2, max_leaves > 64 ? max_groups * 32 : 16);
     rc |= ensure(c, s.digests, max_blobs * 32);
     rc |= ensure(c, s.is_dup, max_blobs);
@@ -1111,7 +1115,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
 
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len,
-                 c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr, gshift};
+                 c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr, gshift,
+                 c->b3_loads == B3_LOADS_LINES ? P<uint32_t>(c->b_gblob) : nullptr};
 
     // ---- chunking (the scan on the context stream, the latency-bound kernels after it on `lat`)
     const bool split = c->lat_split;
@@ -1142,8 +1147,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
                     P<uint64_t>(c->ubtot));
     // Chunk.hash: one wave per chunk (a thread-serial version inside k_unit_emit made C1's
     // assembly 0.03 -> 0.31 ms: 64 dependent byte loads per chunk)
-    if (ncf) launch_cut_hash(lat, d_data, mk, ctr, b, max_blobs);
-    else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, lat));
+    // Chunk.hash (0 for whole-file blobs) and the group -> blob map of the leaf pass
+    launch_cut_hash(lat, d_data, mk, ctr, b, max_blobs);
     if (split) {
         HIPCHK(c, hipEventRecord(c->e_lat, lat));
         HIPCHK(c, hipStreamWaitEvent(st, c->e_lat, 0));
