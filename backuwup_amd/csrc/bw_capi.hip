@@ -145,7 +145,8 @@ struct bw_ctx {
     bool order_hash = false;  // BW_OPT_ORDER_HASH
     uint64_t cand_cap_forced = 0;
     int b3_group = 0;   // BW_OPT_B3_GROUP: leaves per BLAKE3 group of the aligned-line leaf pass (0 = auto)
-    bool b3_fused = false;  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass (measured slower)
+    bool b3_fused = false;
+    bool b3_map = true;  // BW_OPT_B3_MAP: the leaf pass reads its blob from the group -> blob map  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass (measured slower)
     int b3_loads = B3_LOADS_LINES;  // k_b3_lines: 1.07x fetch (pairs 1.42x), -6 % time isolated
     int scan_waves = 16;
     // latency stream: the small kernels between the two big passes (compaction, boundary
@@ -679,6 +680,10 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
             if (__builtin_popcountll(v) < 2 || v >= (2u << BW_N_STAGES)) return BW_EINVAL;
             c->prof_mask = (uint32_t)v;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
+        case BW_OPT_B3_MAP:
+            if (v > 1) return BW_EINVAL;
+            c->b3_map = v == 1;
+            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_B3_GROUP:
             if (v != 0 && v != 1 && v != 2 && v != 4) return BW_EINVAL;
             c->b3_group = (int)v;
@@ -1098,8 +1103,11 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     auto up = [&](DevBuf& dst, const void* src, size_t bytes) -> hipError_t {
         return bytes ? hipMemcpyAsync(dst.p, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
     };
-    // one copy: the tables lie back to back in the staging and keep that layout on the device
-    HIPCHK(c, up(c->meta, segs, meta_bytes));
+    // one copy: the tables lie back to back in the staging and keep that layout on the device.
+    // Up to 1 MiB a kernel reads them over PCIe (no copy-engine round trip on the stream); more
+    // (C4's million units, ~40 MB) go by DMA.
+    if (meta_bytes <= (1u << 20)) launch_upload(c->stream, segs, c->meta.p, meta_bytes);
+    else HIPCHK(c, up(c->meta, segs, meta_bytes));
     SegDesc* d_segs = P<SegDesc>(c->meta);
     CFileDesc* d_cfs = (CFileDesc*)(d_segs + nseg);
     UnitDesc* d_units = (UnitDesc*)(d_cfs + ncf);
@@ -1116,7 +1124,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len,
                  c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr, gshift,
-                 c->b3_loads == B3_LOADS_LINES ? P<uint32_t>(c->b_gblob) : nullptr};
+                 c->b3_loads == B3_LOADS_LINES && c->b3_map ? P<uint32_t>(c->b_gblob) : nullptr};
 
     // ---- chunking (the scan on the context stream, the latency-bound kernels after it on `lat`)
     const bool split = c->lat_split;

@@ -945,6 +945,25 @@ void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint6
                        cfiles, chains, chain_n, seg_M, cf_invalid, fb_starts, fb_count, b, ucb, ucg, bt_b, bt_g);
 }
 
+// ======================================================================== batch tables upload
+
+// The batch's tables from the slot's pinned staging into HBM, read over PCIe by the kernel itself.
+// A hipMemcpyAsync of the same ~17 KB (C1) ran as a blit kernel below ~16 KB but as an SDMA copy
+// above, and the compute stream then waited ~22 us for the copy engine after the scan
+// (profiles/r03/s11_*); a kernel on the stream costs a few us and no cross-engine sync.
+__global__ __launch_bounds__(256) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+void launch_upload(hipStream_t st, const void* host_src, void* dst, uint64_t bytes) {
+    const uint64_t n16 = (bytes + 15) / 16;
+    if (!n16) return;
+    uint64_t grid = (n16 + 255) / 256;
+    if (grid > 1024) grid = 1024;
+    hipLaunchKernelGGL(k_upload, dim3((unsigned)grid), dim3(256), 0, st, (const uint4*)host_src, (uint4*)dst, n16);
+}
+
 // ======================================================================== Chunk.hash
 
 // The crate returns its running gear state with the cut: h_p (odd p) or h_p << 1 (even p, the
