@@ -16,7 +16,7 @@ BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
 BW_OPT_DEPTH, BW_OPT_SCAN_SMALL_BYTES, BW_OPT_CAND_CAP, BW_OPT_STAGE_CHUNK, BW_OPT_B3_LOADS = 1, 2, 3, 4, 5
 BW_OPT_SCAN_WAVES, BW_OPT_LATENCY_STREAM, BW_OPT_ZSTD_SLOTS, BW_OPT_ZSTD_BATCH_BYTES = 6, 7, 8, 9
 BW_OPT_ORDER_HASH, BW_OPT_SPLIT = 10, 11
-BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_B3_UPPER, BW_OPT_B3_GROUP, BW_OPT_B3_MAP = 12, 13, 14, 15, 16
+BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_B3_UPPER, BW_OPT_B3_GROUP = 12, 13, 14, 15
 BW_B3_LOADS_DEFAULT = 2  # the library's BW_OPT_B3_LOADS default (bw_capi.hip)
 
 u8p = ctypes.POINTER(ctypes.c_uint8)

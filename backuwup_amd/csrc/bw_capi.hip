@@ -107,7 +107,6 @@ struct bw_ctx {
     DevBuf meta, chains, chain_n, chain_cptr, merge, seg_M, seg_cnt, cf_invalid, fb_starts, fb_count;
     DevBuf b_start, b_len, b_goff, b_file, b_kind, b_fend, b_ghash;
     DevBuf b_gdone;  // per blob: BLAKE3 groups finished (fused upper levels); zero between passes
-    DevBuf b_gblob;  // per BLAKE3 group: its blob (k_cut_hash -> the aligned-line leaf pass)
     DevBuf cv, cv2, data, scratch, ucnt, ubtot;
     DevBuf bk_blk, bk_pack, bk_v;  // multi-GPU exchange buckets (bw_partition_buckets, ...)
     // bw_exchange_dedup: my buckets and the ones received, their source positions, the counts
@@ -145,8 +144,7 @@ struct bw_ctx {
     bool order_hash = false;  // BW_OPT_ORDER_HASH
     uint64_t cand_cap_forced = 0;
     int b3_group = 0;   // BW_OPT_B3_GROUP: leaves per BLAKE3 group of the aligned-line leaf pass (0 = auto)
-    bool b3_fused = false;
-    bool b3_map = true;  // BW_OPT_B3_MAP: the leaf pass reads its blob from the group -> blob map  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass (measured slower)
+    bool b3_fused = false;  // BW_OPT_B3_UPPER: the upper levels inside the leaf pass (measured slower)
     int b3_loads = B3_LOADS_LINES;  // k_b3_lines: 1.07x fetch (pairs 1.42x), -6 % time isolated
     int scan_waves = 16;
     // latency stream: the small kernels between the two big passes (compaction, boundary
@@ -563,7 +561,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
     DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->meta,
                      &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
-                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->b_gdone, &c->b_gblob, &c->cv, &c->cv2,
+                     &c->b_goff, &c->b_file, &c->b_kind, &c->b_fend, &c->b_ghash, &c->b_gdone, &c->cv, &c->cv2,
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
                      &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage,
@@ -679,10 +677,6 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
         case BW_OPT_PROFILE_MASK:
             if (__builtin_popcountll(v) < 2 || v >= (2u << BW_N_STAGES)) return BW_EINVAL;
             c->prof_mask = (uint32_t)v;
-            return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
-        case BW_OPT_B3_MAP:
-            if (v > 1) return BW_EINVAL;
-            c->b3_map = v == 1;
             return c->helper ? bw_set_option(c->helper, opt, v) : BW_OK;
         case BW_OPT_B3_GROUP:
             if (v != 0 && v != 1 && v != 2 && v != 4) return BW_EINVAL;
@@ -1079,7 +1073,6 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         if (!rc) HIPCHK(c, hipMemsetAsync(c->b_gdone.p, 0, c->b_gdone.cap, c->stream));
     }
     rc |= ensure(c, c->cv, max_groups * 32);
-    rc |= ensure(c, c->b_gblob, max_groups * 4);
     rc |= ensure(c, c->cv2, max_leaves > 64 ? max_groups * 32 : 16);
     rc |= ensure(c, s.digests, max_blobs * 32);
     rc |= ensure(c, s.is_dup, max_blobs);
@@ -1123,8 +1116,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
 
     BlobArrays b{P<uint64_t>(c->b_start), P<uint64_t>(c->b_len), P<uint64_t>(c->b_goff), P<uint32_t>(c->b_file),
                  P<uint32_t>(c->b_kind), P<uint64_t>(c->b_fend), P<uint64_t>(c->b_ghash), max_blobs, data_len,
-                 c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr, gshift,
-                 c->b3_loads == B3_LOADS_LINES && c->b3_map ? P<uint32_t>(c->b_gblob) : nullptr};
+                 c->b3_fused ? P<uint32_t>(c->b_gdone) : nullptr, gshift};
 
     // ---- chunking (the scan on the context stream, the latency-bound kernels after it on `lat`)
     const bool split = c->lat_split;
@@ -1155,8 +1147,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
                     P<uint64_t>(c->ubtot));
     // Chunk.hash: one wave per chunk (a thread-serial version inside k_unit_emit made C1's
     // assembly 0.03 -> 0.31 ms: 64 dependent byte loads per chunk)
-    // Chunk.hash (0 for whole-file blobs) and the group -> blob map of the leaf pass
-    launch_cut_hash(lat, d_data, mk, ctr, b, max_blobs);
+    if (ncf) launch_cut_hash(lat, d_data, mk, ctr, b, max_blobs);
+    else HIPCHK(c, hipMemsetAsync(c->b_ghash.p, 0, max_blobs * 8, lat));
     if (split) {
         HIPCHK(c, hipEventRecord(c->e_lat, lat));
         HIPCHK(c, hipStreamWaitEvent(st, c->e_lat, 0));

@@ -969,19 +969,11 @@ void launch_upload(hipStream_t st, const void* host_src, void* dst, uint64_t byt
 // The crate returns its running gear state with the cut: h_p (odd p) or h_p << 1 (even p, the
 // two-byte loop keeps the even half-step shifted), h of the last tested position when no
 // position cut, and 0 for a tail of <= min bytes.  One wave per CDC chunk, <= 64 terms.
-//
-// The same wave writes its blob's entries of the group -> blob map the leaf pass reads (b.gblob), so
-// no lane of that pass binary-searches the group offsets (~log2(blobs) dependent loads at every
-// wave's start).
 __global__ __launch_bounds__(256) void k_cut_hash(const uint8_t* __restrict__ data, Masks mk,
                                                   const uint64_t* ctr, BlobArrays b) {
     const uint64_t k = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
     if (k >= ctr[C_NBLOBS]) return;
     const int lane = bw_lane();
-    if (b.gblob) {
-        const uint64_t g0 = b.goff[k], ng = groups_of(b.len[k], b.gshift);
-        for (uint64_t i = (uint64_t)lane; i < ng; i += 64) b.gblob[g0 + i] = (uint32_t)k;
-    }
     if (b.kind[k] == 0) { if (lane == 0) b.ghash[k] = 0; return; }
     const uint64_t s = b.start[k], len = b.len[k], fe = b.fend[k];
     const uint64_t rem = fe - s;

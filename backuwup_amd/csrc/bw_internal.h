@@ -100,8 +100,6 @@ struct BlobArrays {
     uint32_t* gdone = nullptr;  // per blob: BLAKE3 groups finished (zero between passes); null = the
                                 // upper levels run as a launch of their own (k_b3_upper)
     uint32_t gshift = 2;        // log2 of the leaves per BLAKE3 group (k_b3_lines: 0..2; others: 2)
-    uint32_t* gblob = nullptr;  // per BLAKE3 group: its blob (filled by k_cut_hash); null = the leaf
-                                // pass finds it by binary search over goff
 };
 
 // ------------------------------------------------------------------ launchers (bw_cdc.hip)

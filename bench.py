@@ -162,7 +162,6 @@ def main():
                     help="BW_OPT_B3_UPPER: 1 = upper levels inside the leaf pass (default), 0 = own launch")
     ap.add_argument("--b3-group", type=int, default=None, choices=[1, 2, 4],
                     help="BW_OPT_B3_GROUP: BLAKE3 leaves per lane of the leaf pass")
-    ap.add_argument("--b3-map", type=int, default=None, choices=[0, 1], help="BW_OPT_B3_MAP")
     ap.add_argument("--scan-first", type=int, default=None, choices=[0, 1, 2], help="BW_OPT_SCAN_FIRST")
     ap.add_argument("--all-stage-marks", action="store_true",
                     help="mark every stage in the timed region (each mark costs the stream ~5 us)")
@@ -195,7 +194,7 @@ def main():
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
     from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
-                                   BW_OPT_B3_GROUP, BW_OPT_B3_MAP, BW_OPT_B3_UPPER, BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
+                                   BW_OPT_B3_GROUP, BW_OPT_B3_UPPER, BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -251,8 +250,6 @@ def main():
             c.set_option(BW_OPT_B3_UPPER, args.b3_upper)
         if args.b3_group is not None:
             c.set_option(BW_OPT_B3_GROUP, args.b3_group)
-        if args.b3_map is not None:
-            c.set_option(BW_OPT_B3_MAP, args.b3_map)
         if args.host_stream and nctx > 1:
             c.set_option(BW_OPT_DEPTH, 1)  # contexts alternate: one HBM input buffer each is enough
         ctxs.append(c)

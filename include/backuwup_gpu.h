@@ -187,14 +187,11 @@ enum {
                                     (k_b3_lines; the wave that finishes a blob's last group builds them)
                                     -- measured 15-21 % slower on C1/C2/C4.  Only the aligned-line leaf
                                     pass (BW_OPT_B3_LOADS 2) fuses them */
-    BW_OPT_B3_GROUP = 15,        /* BLAKE3 leaves per lane of the aligned-line leaf pass: 4, 2 or 1, or
+    BW_OPT_B3_GROUP = 15         /* BLAKE3 leaves per lane of the aligned-line leaf pass: 4, 2 or 1, or
                                     0 (default) = 2 for batches under BW_OPT_SCAN_SMALL_BYTES or of
                                     small blobs, else 4.  Smaller groups cut the pass's last partial
                                     round of waves and ragged lanes (the levels above them move to the
                                     upper pass) */
-    BW_OPT_B3_MAP = 16           /* 1 (default): the aligned-line leaf pass reads each lane's blob from a
-                                    group -> blob map written beside Chunk.hash; 0: binary search over
-                                    the blobs' group offsets */
 };
 int bw_set_option(bw_ctx* ctx, int option, uint64_t value);
 
