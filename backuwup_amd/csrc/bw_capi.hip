@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -439,8 +440,12 @@ static int index_reset_locked(bw_ctx* c, uint64_t hint, hipStream_t st) {
 }
 
 // Append + gate n digests (n read on the device from n_dev when given; max_n bounds it).
+// `then` (may be empty) is enqueued after the gate and before the index's tail event, i.e. inside
+// the index operation: a batch's k_pack snapshots the index state there, and its launch does not
+// sit behind an event record (each costs the stream ~5.5 us of idle time).
 static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
-                        uint8_t* d_is_dup, hipStream_t st = nullptr) {
+                        uint8_t* d_is_dup, hipStream_t st = nullptr,
+                        const std::function<void(hipStream_t)>& then = nullptr) {
     IndexOp op(c, st);
     st = op.st;
     bw_index* x = c->idx;
@@ -452,6 +457,7 @@ static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_d
     x->log_hi += max_n;
     x->enq_total += max_n;
     c->idx_mark = x->enq_total;
+    if (then) then(st);
     HIPCHK(c, hipGetLastError());
     return BW_OK;
 }
@@ -1181,22 +1187,27 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     if (d_data == P<uint8_t>(s.input)) HIPCHK(c, hipEventRecord(s.input_free, st));
     phase(3);
     prof_mark(c, BW_STAGE_DEDUP, lat);
-    if (do_dedup) {
-        if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup), lat))
-            return r4;
-        s.mark = c->idx_mark;
-    }
-    phase(4);
-    prof_mark(c, BW_STAGE_PACK, lat);
     // small result sets are written to the slot's pinned buffer by k_pack itself (no copy on the
     // stream: pack -> copy cost a 12 us gap with one batch in flight, profiles/r03/s07_upper_block)
     uint64_t want = 0;
     bool zero_copy = false;
     if (stage)
         if (int r5 = stage_prepare(c, s, max_blobs, &want, &zero_copy)) return r5;
-    launch_pack(lat, ctr, b, d_fstart, P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
-                slot_records(s), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr,
-                zero_copy ? (uint8_t*)s.res.p : nullptr, want);
+    auto pack = [&](hipStream_t ps) {
+        prof_mark(c, BW_STAGE_PACK, ps);
+        launch_pack(ps, ctr, b, d_fstart, P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
+                    slot_records(s), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr,
+                    zero_copy ? (uint8_t*)s.res.p : nullptr, want);
+    };
+    if (do_dedup) {  // the pack runs inside the index operation (before its tail event)
+        if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup), lat,
+                                  pack))
+            return r4;
+        s.mark = c->idx_mark;
+    } else {
+        pack(lat);
+    }
+    phase(4);
     if (split) {  // the batch ends on the context stream (the caller's order)
         prof_mark(c, BW_N_STAGES, lat);
         HIPCHK(c, hipEventRecord(c->e_end, lat));
