@@ -192,7 +192,9 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from backuwup_amd import BLOB_DTYPE, Context, Index, make_params
+    import ctypes
+
+    from backuwup_amd import BLOB_DTYPE, Context, Index, _lib, make_params
     from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
                                    BW_OPT_B3_GROUP, BW_OPT_B3_UPPER, BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
 
@@ -295,7 +297,30 @@ def main():
     def drain():
         while inflight:
             c, t = inflight.pop(0)
-            c.wait(t, out=out_buf)
+            wait(c, t)
+
+    # The timed loop calls the C ABI with ctypes arguments built once (the Context methods convert
+    # and wrap per call, ~10-20 us of Python per batch that a Rust caller does not have; with one
+    # batch in flight that time sits between two batches on the GPU)
+    L = _lib.load()
+    c_data, c_fo, c_fl = ctypes.c_void_p(data_ptr), file_off.ctypes.data_as(_lib.u64p), file_len.ctypes.data_as(_lib.u64p)
+    c_nf, c_params = len(file_off), ctypes.byref(params)
+    t_out, n_out = ctypes.c_uint64(), ctypes.c_uint64()
+    c_t, c_n = ctypes.byref(t_out), ctypes.byref(n_out)
+    c_out, c_cap = out_buf.ctypes.data_as(ctypes.POINTER(_lib.BwBlob)), out_buf.size
+
+    def submit(c):
+        if host is not None:
+            return c.submit_host(host_ptr, file_off, file_len, params, data_len=n)
+        rc = L.bw_submit_device(c.h, c_data, n, c_fo, c_fl, c_nf, c_params, c_t)
+        if rc:
+            _lib.check(rc, c.h)
+        return t_out.value
+
+    def wait(c, t):
+        rc = L.bw_wait(c.h, t, c_out, c_cap, c_n)
+        if rc:
+            _lib.check(rc, c.h)
 
     def step():
         k = step_no[0] % len(ctxs)
@@ -303,17 +328,14 @@ def main():
         c = ctxs[k]
         # (the context runs on the stream set_stream gave it: no torch stream switch per step)
         th = time.perf_counter()
-        if host is not None:
-            t = c.submit_host(host_ptr, file_off, file_len, params, data_len=n)
-        else:
-            t = c.submit_device(data_ptr, n, file_off, file_len, params)
+        t = submit(c)
         host_ms[0] += (time.perf_counter() - th) * 1e3
         if multi:
             c.exchange_dedup(comm, t)  # owner = digest[0] >> (8 - log2 N); verdicts back into the batch
         inflight.append((c, t))
         if len(inflight) >= len(ctxs):  # one batch per context in flight: read the oldest while the rest run
             c0, t0 = inflight.pop(0)
-            c0.wait(t0, out=out_buf)
+            wait(c0, t0)
 
     ctx.index_reset(index_hint)
     for _ in range(args.warmup):
