@@ -956,6 +956,14 @@ __global__ __launch_bounds__(256) void k_upload(const uint4* __restrict__ src, u
         dst[i] = src[i];
 }
 
+__global__ __launch_bounds__(64) void k_zero(uint64_t* __restrict__ p, uint32_t n) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
+}
+
+void launch_zero(hipStream_t st, uint64_t* p, uint32_t n) {
+    hipLaunchKernelGGL(k_zero, dim3(1), dim3(64), 0, st, p, n);
+}
+
 void launch_upload(hipStream_t st, const void* host_src, void* dst, uint64_t bytes) {
     const uint64_t n16 = (bytes + 15) / 16;
     if (!n16) return;

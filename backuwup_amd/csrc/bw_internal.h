@@ -128,6 +128,7 @@ void launch_assemble(hipStream_t st, uint64_t* ctr, const UnitDesc* units, uint6
                      uint64_t* ucnt /* 2 * nunits */, uint64_t* ubtot /* 2 * (nunits / 256 + 2) */);
 // bytes (rounded up to 16) from device-accessible pinned host memory into HBM, by a kernel on st
 void launch_upload(hipStream_t st, const void* host_src, void* dst, uint64_t bytes);
+void launch_zero(hipStream_t st, uint64_t* p, uint32_t n);  // n u64 (<= a few hundred) to 0
 void launch_cut_hash(hipStream_t st, const uint8_t* data, const Masks& mk, const uint64_t* ctr,
                      BlobArrays b, uint64_t max_blobs);
 
