@@ -16,6 +16,7 @@ fi
 run bench_c2 400 python bench.py || exit 1
 if [[ "${CONFIGS:-1}" == 1 ]]; then
   run bench_c1_s1 200 python bench.py --workload c1 --streams 1 --steps 1500 --no-cpu-baseline || exit 1
+  run bench_c1_s1_b 200 python bench.py --workload c1 --streams 1 --steps 1500 --no-cpu-baseline || exit 1
   run bench_c1 200 python bench.py --workload c1 --steps 1500 --no-cpu-baseline || exit 1
   run bench_c3 400 python bench.py --workload c3 --no-cpu-baseline || exit 1
   run bench_c4 400 python bench.py --workload c4 --no-cpu-baseline || exit 1
