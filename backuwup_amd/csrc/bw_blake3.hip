@@ -736,7 +736,7 @@ uint32_t b3_calib_blocks_per_cu() { return BW_B3_LINES_MINW; }
 
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
                    uint64_t max_groups, uint32_t* cv_buf, uint32_t* cv_tmp, uint8_t* digests, int max_leaves,
-                   hipEvent_t between, int loads, hipStream_t upper, hipEvent_t leaf_done) {
+                   hipEvent_t between, int loads, hipStream_t upper, hipEvent_t leaf_done, hipEvent_t mark) {
     if (!max_blobs) {
         if (leaf_done) hipEventRecord(leaf_done, st);
         return;
@@ -758,6 +758,7 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
         hipLaunchKernelGGL((k_b3_groups<true, 1, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
                            data, ctr, b, cv_buf, digests);
     if (leaf_done) hipEventRecord(leaf_done, st);
+    if (mark) hipEventRecord(mark, st);
     if (between) hipEventRecord(between, st);
     if (upper != st) hipStreamWaitEvent(upper, between, 0);
     st = upper;

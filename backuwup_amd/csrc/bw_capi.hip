@@ -263,6 +263,14 @@ template <typename T>
 static T* P(DevBuf& b) { return (T*)b.p; }
 
 constexpr size_t CTR_BYTES = C_COUNT * 8;
+
+// Event kinds.  An event recorded between two kernels costs the stream ~5.5 us of idle time with
+// the default system-scope fence (a cache writeback and invalidate); the events that only order GPU
+// work (or tell the host that the GPU finished reading something) release at device scope, and the
+// stage marks, which only time, take no system fence at all.  `done`, after which the host reads
+// results the GPU wrote into pinned memory, keeps the system scope.
+constexpr unsigned EV_ORDER = hipEventDisableTiming | hipEventReleaseToDevice;
+constexpr unsigned EV_TIMING = hipEventDisableSystemFence;
 static uint64_t* slot_ctr(Slot& s) { return (uint64_t*)s.res_dev.p; }
 static uint8_t* slot_records(Slot& s) { return (uint8_t*)s.res_dev.p + CTR_BYTES; }
 
@@ -329,9 +337,9 @@ static void prof_mark(bw_ctx* c, int stage, hipStream_t st = nullptr) {
 static int index_init(bw_index* x, int device) {
     x->device = device;
     if (hipSetDevice(device) != hipSuccess) return BW_EHIP;
-    if (hipEventCreateWithFlags(&x->tail, hipEventDisableTiming) != hipSuccess) return BW_EHIP;
-    if (hipEventCreateWithFlags(&x->hash_tail, hipEventDisableTiming) != hipSuccess) return BW_EHIP;
-    if (hipEventCreateWithFlags(&x->scan_tail, hipEventDisableTiming) != hipSuccess) return BW_EHIP;
+    if (hipEventCreateWithFlags(&x->tail, EV_ORDER) != hipSuccess) return BW_EHIP;
+    if (hipEventCreateWithFlags(&x->hash_tail, EV_ORDER) != hipSuccess) return BW_EHIP;
+    if (hipEventCreateWithFlags(&x->scan_tail, EV_ORDER) != hipSuccess) return BW_EHIP;
     if (hipMalloc(&x->dstate.p, D_COUNT * 8) != hipSuccess) return BW_ENOMEM;
     x->dstate.cap = D_COUNT * 8;
     if (hipMemset(x->dstate.p, 0, D_COUNT * 8) != hipSuccess) return BW_EHIP;
@@ -540,9 +548,9 @@ extern "C" int bw_create(int device, bw_ctx** out) {
     }
     for (int s = 0; s <= MAX_DEPTH; s++) {
         Slot& sl = s < MAX_DEPTH ? c->slots[s] : c->sync_slot;
-        if (hipEventCreateWithFlags(&sl.meta_done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&sl.input_free, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) != hipSuccess ||
+        if (hipEventCreateWithFlags(&sl.meta_done, EV_ORDER) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.input_free, EV_ORDER) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.copied, EV_ORDER) != hipSuccess ||
             hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
             bw_destroy(c);
             return BW_EHIP;
@@ -663,7 +671,7 @@ extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
                 HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
                 HIPCHK(c, hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest));
                 for (hipEvent_t* e : {&c->e_scan, &c->e_lat, &c->e_b3, &c->e_end})
-                    HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+                    HIPCHK(c, hipEventCreateWithFlags(e, EV_ORDER));
             }
             c->lat_split = v != 0;
             return BW_OK;
@@ -1169,7 +1177,10 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     // ---- hashing (the leaf pass on the context stream, the upper levels on lat) + dedup on lat
     prof_mark(c, BW_STAGE_B3LEAF, st);
     if (do_hash) {
-        hipEvent_t between = c->prof ? c->ev[c->ev_set][BW_STAGE_B3TREE] : (split ? c->e_b3 : nullptr);
+        // the B3TREE stage mark (timing only) and the event that orders the upper levels' stream
+        // after the leaf pass (split latency stream) are separate events
+        hipEvent_t mark = c->prof && ((c->prof_mask >> BW_STAGE_B3TREE) & 1) ? c->ev[c->ev_set][BW_STAGE_B3TREE] : nullptr;
+        hipEvent_t between = split ? c->e_b3 : nullptr;
         bw_index* x = c->idx;
         std::unique_lock<std::mutex> lk(x->mu, std::defer_lock);
         const bool order = c->order_hash || order_force;
@@ -1178,7 +1189,7 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
             if (x->hash_tail_set) HIPCHK(c, hipStreamWaitEvent(st, x->hash_tail, 0));
         }
         launch_blake3(st, d_data, ctr, b, max_blobs, max_groups, P<uint32_t>(c->cv), P<uint32_t>(c->cv2),
-                      P<uint8_t>(s.digests), max_leaves, between, c->b3_loads, lat, order ? x->hash_tail : nullptr);
+                      P<uint8_t>(s.digests), max_leaves, between, c->b3_loads, lat, order ? x->hash_tail : nullptr, mark);
         if (order) x->hash_tail_set = true;
     } else {
         prof_mark(c, BW_STAGE_B3TREE, st);
@@ -1263,8 +1274,8 @@ static int ensure_helper(bw_ctx* c) {
         return rc;
     }
     if (c->prof) bw_profile_enable(h, 1);
-    if (!c->e_split) HIPCHK(c, hipEventCreateWithFlags(&c->e_split, hipEventDisableTiming));
-    if (!c->e_tail) HIPCHK(c, hipEventCreateWithFlags(&c->e_tail, hipEventDisableTiming));
+    if (!c->e_split) HIPCHK(c, hipEventCreateWithFlags(&c->e_split, EV_ORDER));
+    if (!c->e_tail) HIPCHK(c, hipEventCreateWithFlags(&c->e_tail, EV_ORDER));
     c->helper = h;
     return BW_OK;
 }
@@ -1754,7 +1765,7 @@ extern "C" int bw_profile_enable(bw_ctx* c, int on) {
     for (int k = 0; k < 2; k++) {
         c->ev_pending[k] = false;
         for (int i = 0; i <= BW_N_STAGES; i++)
-            if (!c->ev[k][i]) HIPCHK(c, hipEventCreate(&c->ev[k][i]));
+            if (!c->ev[k][i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev[k][i], EV_TIMING));
     }
     c->prof = on != 0;
     for (int i = 0; i < BW_N_STAGES; i++) c->stage_ms[i] = 0;

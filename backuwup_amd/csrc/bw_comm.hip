@@ -141,7 +141,7 @@ extern "C" int bw_comm_init(int device, int rank, int world, const uint8_t id[BW
     c->world = world;
     ncclUniqueId u;
     memcpy(u.internal, id, BW_COMM_ID_BYTES);
-    if (hipEventCreateWithFlags(&c->tail, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c->tail, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
         delete c;
         return BW_EHIP;
     }

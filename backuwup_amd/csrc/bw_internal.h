@@ -142,7 +142,8 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
                    uint32_t* cv_tmp /* like cv_buf */, uint8_t* digests, int max_leaves,
                    hipEvent_t between /* may be null */, int loads,
                    hipStream_t upper /* stream of the upper tree levels; `between` must order it */,
-                   hipEvent_t leaf_done = nullptr /* recorded on st right after the leaf pass */);
+                   hipEvent_t leaf_done = nullptr /* recorded on st right after the leaf pass */,
+                   hipEvent_t mark = nullptr /* a timing mark, likewise */);
 // The leaf pass's compression from registers (roofline calibration): n_blocks blocks of 256,
 // stamps[2 * block] = shader cycles, stamps[2 * block + 1] = 100 MHz ticks of wave 0.
 void launch_b3_calib(hipStream_t st, uint32_t n_blocks, uint32_t blocks_per_lane, uint32_t* sink, uint64_t* stamps);
