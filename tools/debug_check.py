@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run the hot path once through the BW_DEBUG build (libbackuwup_amd_debug.so: device bounds asserts
-in walk_next, unit_blobs and k_b3_groups) over the inputs that stress those paths, checked against
+in walk_next, unit_blobs, k_b3_groups and k_b3_lines) over the inputs that stress those paths, checked against
 the oracle.  A failed device assert traps the kernel, so this runs as its own step of the GPU
 session (tools/gpu_r2.sh debug), never inside the pytest process."""
 import os
@@ -46,6 +46,18 @@ def main():
             c.index_reset()
             assert same(c.process_files(data, offs, lens), oracle.process_files(data, offs, lens, threads=8))
             checks += 1
+        # round 3: every BLAKE3 group size, and the upper levels fused into the leaf pass
+        from backuwup_amd._lib import BW_OPT_B3_GROUP, BW_OPT_B3_UPPER
+        data, offs, lens = tree_corpus(48 << 20, seed=5, max_file=9 << 20)
+        want = oracle.process_files(data, offs, lens, threads=8)
+        for grp, upper in ((1, 0), (2, 0), (4, 0), (2, 1)):
+            c.set_option(BW_OPT_B3_GROUP, grp)
+            c.set_option(BW_OPT_B3_UPPER, upper)
+            c.index_reset()
+            assert same(c.process_files(data, offs, lens), want), (grp, upper)
+            checks += 1
+        c.set_option(BW_OPT_B3_GROUP, 0)
+        c.set_option(BW_OPT_B3_UPPER, 0)
         data, offs, lens = small_files(20000, seed=4)
         c.index_reset()
         assert same(c.process_files(data, offs, lens), oracle.process_files(data, offs, lens, threads=8))
