@@ -449,10 +449,12 @@ static int index_reset_locked(bw_ctx* c, uint64_t hint, hipStream_t st) {
 }
 
 // Append + gate n digests (n read on the device from n_dev when given; max_n bounds it).
-// `pack` (may be null): the batch's result records are written by the gate's verdict pass itself
-// (inside the index operation, so the index snapshot in them is exact and no pack launch follows)
+// `then` (may be empty) is enqueued after the gate and before the index's tail event, i.e. inside
+// the index operation: a batch's k_pack snapshots the index state there, and its launch does not
+// sit behind an event record (each costs the stream ~5.5 us of idle time).
 static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
-                        uint8_t* d_is_dup, hipStream_t st = nullptr, const PackOut* pack = nullptr) {
+                        uint8_t* d_is_dup, hipStream_t st = nullptr,
+                        const std::function<void(hipStream_t)>& then = nullptr) {
     IndexOp op(c, st);
     st = op.st;
     bw_index* x = c->idx;
@@ -460,10 +462,11 @@ static int dedup_device(bw_ctx* c, const uint8_t* d_digests, const uint64_t* n_d
         if (int rc = index_reset_locked(c, 0, st)) return rc;
     if (int rc = index_capacity(c, max_n, st)) return rc;
     launch_dedup(st, P<uint64_t>(x->table), x->table_cap, P<uint8_t>(x->log), P<uint64_t>(x->dstate),
-                 d_digests, n_dev, n_host, max_n, d_is_dup, pack);
+                 d_digests, n_dev, n_host, max_n, d_is_dup);
     x->log_hi += max_n;
     x->enq_total += max_n;
     c->idx_mark = x->enq_total;
+    if (then) then(st);
     HIPCHK(c, hipGetLastError());
     return BW_OK;
 }
@@ -1207,17 +1210,19 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     bool zero_copy = false;
     if (stage)
         if (int r5 = stage_prepare(c, s, max_blobs, &want, &zero_copy)) return r5;
-    if (do_dedup) {  // the records are written by the gate's verdict pass (the PACK stage is empty)
-        PackOut po{ctr, b, d_fstart, slot_records(s), zero_copy ? (uint8_t*)s.res.p : nullptr, want};
+    auto pack = [&](hipStream_t ps) {
+        prof_mark(c, BW_STAGE_PACK, ps);
+        launch_pack(ps, ctr, b, d_fstart, P<uint8_t>(s.digests), do_dedup ? P<uint8_t>(s.is_dup) : nullptr,
+                    slot_records(s), max_blobs, do_dedup ? P<uint64_t>(c->idx->dstate) : nullptr,
+                    zero_copy ? (uint8_t*)s.res.p : nullptr, want);
+    };
+    if (do_dedup) {  // the pack runs inside the index operation (before its tail event)
         if (int r4 = dedup_device(c, P<uint8_t>(s.digests), ctr + C_DEDUPN, 0, max_blobs, P<uint8_t>(s.is_dup), lat,
-                                  &po))
+                                  pack))
             return r4;
         s.mark = c->idx_mark;
-        prof_mark(c, BW_STAGE_PACK, lat);
     } else {
-        prof_mark(c, BW_STAGE_PACK, lat);
-        launch_pack(lat, ctr, b, d_fstart, P<uint8_t>(s.digests), nullptr, slot_records(s), max_blobs, nullptr,
-                    zero_copy ? (uint8_t*)s.res.p : nullptr, want);
+        pack(lat);
     }
     phase(4);
     if (split) {  // the batch ends on the context stream (the caller's order)

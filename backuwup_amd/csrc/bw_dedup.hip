@@ -88,33 +88,8 @@ __global__ void k_append_claim(uint64_t* __restrict__ table, uint64_t cap, uint8
 
 // Verdicts of the batch (after every claim); the last block to finish advances the log length,
 // which every block read first (no separate launch).
-__device__ __forceinline__ void index_snapshot(const uint64_t* dstate, uint64_t* ctr);
-
-// One bw_blob record (72 B) of blob k, at out and (k < host_n) at host + C_COUNT * 8.
-__device__ __forceinline__ void pack_record(uint64_t k, uint8_t v, const BlobArrays& b, const uint64_t* file_start,
-                                            const uint8_t* digests, uint8_t* out, uint8_t* host, uint64_t host_n) {
-    uint64_t* o = (uint64_t*)(out + k * 72);
-    const uint32_t f = b.file[k];
-    o[0] = f;
-    o[1] = b.start[k] - file_start[f];
-    o[2] = b.len[k];
-    o[3] = b.ghash[k];
-    const uint64_t* d = (const uint64_t*)(digests + k * 32);
-    o[4] = d[0];
-    o[5] = d[1];
-    o[6] = d[2];
-    o[7] = d[3];
-    o[8] = v;
-    if (host && k < host_n) {
-        uint64_t* h = (uint64_t*)(host + C_COUNT * 8 + k * 72);
-#pragma unroll
-        for (int i = 0; i < 9; i++) h[i] = o[i];
-    }
-}
-
 __global__ void k_verdict(const uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
-                          uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host, uint8_t* __restrict__ is_dup,
-                          PackOut po) {
+                          uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host, uint8_t* __restrict__ is_dup) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t n = batch_n(n_dev, n_host);
     const uint64_t base = dstate[D_LOGLEN];
@@ -139,8 +114,6 @@ __global__ void k_verdict(const uint64_t* __restrict__ table, uint64_t cap, cons
             if (!same) atomicOr((unsigned long long*)&dstate[D_COLLIDE], 1ull);
         }
         if (is_dup) is_dup[i] = v;
-        // (the batch's digests as the log now holds them: entry base + i is blob i's)
-        if (po.out) pack_record(i, v, po.b, po.file_start, log + base * 32, po.out, po.host, po.host_n);
     }
     __shared__ bool last;
     __syncthreads();  // every thread of the block has read D_LOGLEN
@@ -152,23 +125,15 @@ __global__ void k_verdict(const uint64_t* __restrict__ table, uint64_t cap, cons
     if (last && threadIdx.x == 0) {  // every block has read D_LOGLEN: advance it for the next gate
         dstate[D_LOGLEN] = base + n;
         dstate[D_DONE] = 0;
-        if (po.out) {  // every verdict of the batch is in: the index state after its gate
-            __threadfence();
-            index_snapshot(dstate, po.ctr);
-            if (po.host)
-                for (int c = 0; c < C_COUNT; c++) ((uint64_t*)po.host)[c] = po.ctr[c];
-        }
     }
 }
 
 void launch_dedup(hipStream_t st, uint64_t* table, uint64_t cap, uint8_t* log, uint64_t* dstate,
-                  const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n, uint8_t* is_dup,
-                  const PackOut* pack) {
+                  const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n, uint8_t* is_dup) {
     if (!max_n) return;
     const dim3 g((unsigned)((max_n + 255) / 256)), b(256);
     hipLaunchKernelGGL(k_append_claim, g, b, 0, st, table, cap, log, dstate, digests, n_dev, n_host);
-    PackOut none{};
-    hipLaunchKernelGGL(k_verdict, g, b, 0, st, table, cap, log, dstate, n_dev, n_host, is_dup, pack ? *pack : none);
+    hipLaunchKernelGGL(k_verdict, g, b, 0, st, table, cap, log, dstate, n_dev, n_host, is_dup);
 }
 
 __global__ void k_rehash(uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
@@ -434,7 +399,23 @@ __global__ void k_pack(uint64_t* ctr, BlobArrays b, const uint64_t* __restrict__
             for (int i = 0; i < C_COUNT; i++) ((uint64_t*)host)[i] = ctr[i];
     }
     if (k >= ctr[C_NBLOBS]) return;
-    pack_record(k, is_dup ? is_dup[k] : 0, b, file_start, digests, out, host, host_n);
+    uint64_t* o = (uint64_t*)(out + k * 72);
+    const uint32_t f = b.file[k];
+    o[0] = f;
+    o[1] = b.start[k] - file_start[f];
+    o[2] = b.len[k];
+    o[3] = b.ghash[k];
+    const uint64_t* d = (const uint64_t*)(digests + k * 32);
+    o[4] = d[0];
+    o[5] = d[1];
+    o[6] = d[2];
+    o[7] = d[3];
+    o[8] = is_dup ? (uint64_t)is_dup[k] : 0;
+    if (host && k < host_n) {
+        uint64_t* h = (uint64_t*)(host + C_COUNT * 8 + k * 72);
+#pragma unroll
+        for (int i = 0; i < 9; i++) h[i] = o[i];
+    }
 }
 
 void launch_pack(hipStream_t st, uint64_t* ctr, BlobArrays b, const uint64_t* file_start, const uint8_t* digests,

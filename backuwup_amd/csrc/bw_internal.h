@@ -158,20 +158,9 @@ enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_COLLIDE = 2, D_BUCKET_OVF = 3
 void launch_table_clear(hipStream_t st, uint64_t* table, uint64_t cap);
 // Append n digests (n from *n_dev if non-null, else n_host) to the log and decide them in
 // order: is_dup[i] (may be null) = digest seen at an earlier log position.
-// A batch's result records written by its gate's verdict pass (record i = the batch's blob i, whose
-// verdict that thread just decided), so no pack launch follows the gate; the grid's last block
-// snapshots the index state into ctr and copies ctr to `host` (if set), as k_pack does.
-struct PackOut {
-    uint64_t* ctr;
-    BlobArrays b;
-    const uint64_t* file_start;
-    uint8_t* out;       // device records
-    uint8_t* host;      // pinned copy of ctr + the first host_n records (may be null)
-    uint64_t host_n;
-};
 void launch_dedup(hipStream_t st, uint64_t* table, uint64_t cap, uint8_t* log, uint64_t* dstate,
                   const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
-                  uint8_t* is_dup, const PackOut* pack = nullptr);
+                  uint8_t* is_dup);
 // Re-claim log[0 .. *len) into a fresh table (growth).
 void launch_rehash(hipStream_t st, uint64_t* table, uint64_t cap, const uint8_t* log,
                    const uint64_t* dstate, uint64_t max_n);
