@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("BW_LIB") or os.path.join(HERE, "libbackuwup_amd.so")
 BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -1, -2, -3, -4, -5, -6
 BW_ECRYPTO, BW_EFORMAT, BW_ECOMM = -7, -8, -9
 BW_COMM_ID_BYTES = 128
+BW_COMM_DEFAULT_TIMEOUT_MS = 120000
 BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
 BW_OPT_DEPTH, BW_OPT_SCAN_SMALL_BYTES, BW_OPT_CAND_CAP, BW_OPT_STAGE_CHUNK, BW_OPT_B3_LOADS = 1, 2, 3, 4, 5
 BW_OPT_SCAN_WAVES, BW_OPT_LATENCY_STREAM, BW_OPT_ZSTD_SLOTS, BW_OPT_ZSTD_BATCH_BYTES = 6, 7, 8, 9
@@ -117,6 +118,10 @@ SIGNATURES = [
     ("bw_scatter_buckets", ctypes.c_int, [vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]),
     ("bw_comm_unique_id", ctypes.c_int, [u8p]),
     ("bw_comm_init", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.POINTER(vp)]),
+    ("bw_comm_init_timeout", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_uint32,
+                                            ctypes.POINTER(vp)]),
+    ("bw_comm_set_timeout", ctypes.c_int, [vp, ctypes.c_uint32]),
+    ("bw_comm_status", ctypes.c_int, [vp]),
     ("bw_comm_init_host", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.POINTER(vp)]),
     ("bw_comm_destroy", None, [vp]),
     ("bw_comm_last_error", ctypes.c_char_p, [vp]),

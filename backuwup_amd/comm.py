@@ -35,12 +35,17 @@ class Comm:
         self._keep = keep  # the ctypes callback of a host transport must outlive the handle
 
     @classmethod
-    def rccl(cls, device, rank, world, uid):
+    def rccl(cls, device, rank, world, uid, timeout_ms=None):
+        """timeout_ms: the deadline of every wait on the peers (default BW_COMM_DEFAULT_TIMEOUT_MS);
+        a missed deadline aborts the communicator and returns BW_ECOMM."""
         L = _lib.load()
         assert len(uid) == _lib.BW_COMM_ID_BYTES
         h = ctypes.c_void_p()
         ub = (ctypes.c_uint8 * _lib.BW_COMM_ID_BYTES).from_buffer_copy(uid)
-        check(L.bw_comm_init(device, rank, world, ub, ctypes.byref(h)))
+        if timeout_ms is None:
+            check(L.bw_comm_init(device, rank, world, ub, ctypes.byref(h)))
+        else:
+            check(L.bw_comm_init_timeout(device, rank, world, ub, int(timeout_ms), ctypes.byref(h)))
         return cls(h)
 
     @classmethod
@@ -69,6 +74,13 @@ class Comm:
 
     def set_capacity(self, cap):
         check(self._L.bw_comm_set_capacity(self.h, int(cap)))
+
+    def set_timeout(self, timeout_ms):
+        check(self._L.bw_comm_set_timeout(self.h, int(timeout_ms)))
+
+    def status(self):
+        """0, or BW_ECOMM once the communicator was aborted (a peer failed or stalled)."""
+        return self._L.bw_comm_status(self.h)
 
     def last_error(self):
         m = self._L.bw_comm_last_error(self.h)

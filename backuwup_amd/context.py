@@ -269,7 +269,7 @@ class Context:
         return out
 
     def index_check(self):
-        """Raises BwError(BW_ECOLLISION) if the index ever saw a 64-bit key collision."""
+        """Raises BwError(BW_ENOSPC) if an exchange bucket overflowed since the last reset."""
         check(self._L.bw_index_check(self.h), self.h)
 
     def index_size(self):

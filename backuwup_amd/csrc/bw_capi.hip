@@ -62,6 +62,9 @@ struct Slot {
     uint64_t ticket = 0;  // 0: empty
     uint64_t max_blobs = 0;
     bool dedup = false;
+    bool hashed = false;          // digests computed (not BW_F_NO_HASH): the exchange may gate them
+    bw_comm* comm = nullptr;      // the batch went through this communicator's exchange: waits on it
+                                  // are deadline-bounded (bw::comm_wait_event)
     // Results staged for the host as the batch's last stream operations: the counters (with the
     // index's state after the batch's gate) and the first res_n packed records, in pinned memory,
     // so a wait is one event synchronization and a memcpy instead of three device round trips.
@@ -398,6 +401,10 @@ static int index_capacity(bw_ctx* c, uint64_t incoming, hipStream_t st) {
         x->log_hi = std::min(x->log_hi, len);
     }
     const uint64_t need_log = x->log_hi + incoming;
+    if (need_log >> 40) {  // table words hold a 40-bit log position
+        c->err = "index log beyond 2^40 entries";
+        return BW_ENOMEM;
+    }
     if (need_log > x->log_cap) {
         uint64_t cap = x->log_cap ? x->log_cap : 1 << 16;
         while (cap < need_log) cap *= 2;
@@ -424,11 +431,11 @@ static int index_capacity(bw_ctx* c, uint64_t incoming, hipStream_t st) {
             hipFree(x->table.p);
             x->table.p = nullptr;
         }
-        if (hipMalloc(&x->table.p, cap * 16) != hipSuccess) {
+        if (hipMalloc(&x->table.p, cap * 8) != hipSuccess) {
             c->err = "hipMalloc of the index table failed";
             return BW_ENOMEM;
         }
-        x->table.cap = cap * 16;
+        x->table.cap = cap * 8;
         const uint64_t old = x->table_cap;
         x->table_cap = cap;
         launch_table_clear(st, P<uint64_t>(x->table), cap);
@@ -493,9 +500,9 @@ static int read_index_state(bw_ctx* c, uint64_t st[D_COUNT], bool all) {
 static int check_collision(bw_ctx* c, bool all = false) {
     uint64_t st[D_COUNT];
     if (int rc = read_index_state(c, st, all)) return rc;
-    if (st[D_COLLIDE]) {
-        c->err = "64-bit key collision between distinct digests";
-        return BW_ECOLLISION;
+    if (st[D_LOST]) {
+        c->err = "index lookup found no slot (internal error)";
+        return BW_EHIP;
     }
     if (st[D_BUCKET_OVF]) {
         c->err = "a batch had more blobs than its exchange bucket capacity (verdicts incomplete)";
@@ -521,7 +528,7 @@ extern "C" const char* bw_strerror(int rc) {
         case BW_ENOSPC: return "output capacity too small";
         case BW_EHIP: return "HIP runtime error";
         case BW_ENOMEM: return "out of memory";
-        case BW_ECOLLISION: return "64-bit digest key collision in the index";
+        case BW_ECOLLISION: return "64-bit digest key collision in the index (no longer returned)";
         case BW_ESTATE: return "invalid call order";
         case BW_ECRYPTO: return "AES-GCM authentication failed";
         case BW_EFORMAT: return "malformed bincode data";
@@ -1235,6 +1242,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     HIPCHK(c, hipGetLastError());
     s.max_blobs = max_blobs;
     s.dedup = do_dedup;
+    s.hashed = do_hash;
+    s.comm = nullptr;
     if (stage)
         if (int r5 = stage_results(c, s, zero_copy, want)) return r5;
     phase(5);
@@ -1423,7 +1432,11 @@ extern "C" int bw_host_unregister(void* p) {
 // Results of the batch in slot s (waits for it).  Repeatable until the ring reuses the slot.
 static int slot_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t* n_out) {
     hipSetDevice(c->device);
-    HIPCHK(c, hipEventSynchronize(s.done));  // the staged counters and records have landed
+    if (s.comm) {  // an exchange in flight: a failed or stalled peer must not hang the wait
+        if (int rc = comm_wait_event(s.comm, s.done, c->err)) return rc;
+    } else {
+        HIPCHK(c, hipEventSynchronize(s.done));  // the staged counters and records have landed
+    }
     const uint64_t* ctr = (const uint64_t*)s.res.p;
     if (ctr[C_CANDTOTAL] > ctr[C_NCAND])  // exact anyway; give later batches the room they need
         c->cand_override = std::max(c->cand_override, ctr[C_CANDTOTAL] + 1024);
@@ -1437,9 +1450,9 @@ static int slot_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t
                 std::lock_guard<std::mutex> lk(x->mu);
                 x->log_hi = std::min(x->log_hi, ctr[C_IX_LOGLEN] + (x->enq_total - std::min(x->enq_total, s.mark)));
             }
-            if (ctr[C_COLLIDE]) {
-                c->err = "64-bit key collision between distinct digests";
-                return BW_ECOLLISION;
+            if (ctr[C_LOST]) {
+                c->err = "index lookup found no slot (internal error)";
+                return BW_EHIP;
             }
             if (ctr[C_IX_OVF]) {
                 c->err = "a batch had more blobs than its exchange bucket capacity (verdicts incomplete)";
@@ -1720,14 +1733,23 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
         c->err = "the batch was gated by the local index already (submit it with BW_F_NO_DEDUP)";
         return BW_ESTATE;
     }
+    if (!s->hashed) {  // BW_F_NO_HASH: its digest array holds no digests
+        c->err = "the batch was submitted with BW_F_NO_HASH: no digests to exchange";
+        return BW_ESTATE;
+    }
+    if (comm_failed(comm)) {
+        c->err = "the communicator was aborted by an earlier failure";
+        return BW_ECOMM;
+    }
     hipSetDevice(c->device);
     const uint32_t W = (uint32_t)comm_world(comm);
     hipStream_t st = c->stream;
     if (int rc = ensure(c, c->ex_cnt, 4 * W * 8)) return rc;
     uint64_t* cnt = P<uint64_t>(c->ex_cnt);  // [0, W): my counts, [W, 2W): received, [2W, 4W): scratch
-    uint64_t& cap = comm_cap(comm);
-    if (!cap)  // the session's bucket capacity: the largest per-batch bound over the ranks, once
-        if (int rc = comm_max(comm, s->max_blobs, &cap, cnt + 2 * W, st, c->err)) return rc;
+    // the bucket capacity: the largest per-batch bound over the ranks so far, agreed on every call
+    // (a later, larger batch on any rank grows it on all of them: ADVICE r3)
+    uint64_t cap = 0;
+    if (int rc = comm_agree_cap(comm, s->max_blobs, &cap, c->err)) return rc;
     const uint64_t slots = (uint64_t)W * cap;
     int rc = 0;
     rc |= ensure(c, c->ex_bk, slots * 32);
@@ -1750,6 +1772,7 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     launch_index_snapshot(st, P<uint64_t>(c->idx->dstate), slot_ctr(*s));
     HIPCHK(c, hipGetLastError());
     s->dedup = true;  // bw_wait now reports the index's sticky errors for this batch
+    s->comm = comm;
     s->mark = c->idx_mark;
     return stage_results(c, *s);  // the records staged at submit predate the verdicts
 }

@@ -8,9 +8,20 @@
 //   * a caller's host function (staged through pinned memory; synchronous) -- for a transport the
 //     caller already has, e.g. several processes on one GPU in tests, where RCCL refuses a
 //     communicator with two ranks on the same device.
+//
+// Failure path (round 4).  The reference never lets one peer stall the packer: its transport sends
+// with timeouts (net_p2p/transport.rs:127-128).  Here every wait on a peer has a deadline:
+//   * the RCCL communicators are non-blocking (ncclConfig_t.blocking = 0), so initialisation and
+//     every enqueue return at once and are polled with ncclCommGetAsyncError against the deadline;
+//   * a wait for a batch whose exchange is in flight polls its event and the async error state;
+//   * on an error or a missed deadline both communicators are aborted (ncclCommAbort stops the
+//     kernels that wait on a dead peer), the communicator is marked failed, and every later call
+//     returns BW_ECOMM at once.
 #include <string.h>
 
+#include <chrono>
 #include <string>
+#include <thread>
 
 #include <rccl/rccl.h>
 
@@ -20,10 +31,17 @@ static_assert(BW_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "the C ABI's id size is 
 
 struct bw_comm {
     int device = 0, rank = 0, world = 1;
-    ncclComm_t nccl = nullptr;            // RCCL transport
+    ncclComm_t nccl = nullptr;            // RCCL transport: the data path (counts, buckets, verdicts)
+    ncclComm_t ctl = nullptr;             // split of `nccl` at the first capacity agreement (none while
+                                          // the capacity is fixed): the per-batch agreement, own stream
+    hipStream_t ctl_st = nullptr;
+    uint64_t* ctl_buf = nullptr;          // device, 2 x world u64
     bw_host_all_to_all host_fn = nullptr;  // or the caller's host transport
     void* user = nullptr;
     uint64_t cap = 0;                      // bucket capacity of the session (0 = not agreed yet)
+    bool cap_fixed = false;                // set by bw_comm_set_capacity: no per-batch agreement
+    uint32_t timeout_ms = BW_COMM_DEFAULT_TIMEOUT_MS;
+    bool failed = false;                   // aborted: every call returns BW_ECOMM
     void* pin_send = nullptr;              // host transport: pinned staging, 2 x pin_cap
     size_t pin_cap = 0;
     // The communicator's collectives run in the order the host issued them, whatever streams they
@@ -37,15 +55,54 @@ struct bw_comm {
 
 namespace {
 
+using Clock = std::chrono::steady_clock;
+
 int comm_err(bw_comm* c, std::string& err, const std::string& what) {
     err = what;
     if (c) c->err = what;
     return BW_ECOMM;
 }
 
-int nccl_chk(bw_comm* c, std::string& err, ncclResult_t r, const char* what) {
-    if (r == ncclSuccess) return BW_OK;
-    return comm_err(c, err, std::string(what) + ": " + ncclGetErrorString(r));
+void abort_all(bw_comm* c) {
+    if (c->failed) return;
+    c->failed = true;
+    if (c->ctl) ncclCommAbort(c->ctl);
+    if (c->nccl) ncclCommAbort(c->nccl);
+    c->ctl = nullptr;
+    c->nccl = nullptr;
+}
+
+int fail(bw_comm* c, std::string& err, const std::string& what) {
+    abort_all(c);
+    return comm_err(c, err, what + " (communicator aborted)");
+}
+
+Clock::time_point deadline_of(const bw_comm* c) { return Clock::now() + std::chrono::milliseconds(c->timeout_ms); }
+
+// An error reported by either communicator (ncclInProgress = still enqueuing, not an error).
+ncclResult_t async_state(bw_comm* c) {
+    for (ncclComm_t k : {c->nccl, c->ctl}) {
+        if (!k) continue;
+        ncclResult_t r = ncclSuccess;
+        if (ncclCommGetAsyncError(k, &r) != ncclSuccess) return ncclInternalError;
+        if (r != ncclSuccess) return r;
+    }
+    return ncclSuccess;
+}
+
+// A non-blocking call returned r: wait (to the deadline) until communicator k has finished it.
+int settle(bw_comm* c, ncclComm_t k, ncclResult_t r, const char* what, std::string& err) {
+    if (r != ncclSuccess && r != ncclInProgress) return fail(c, err, std::string(what) + ": " + ncclGetErrorString(r));
+    const auto dl = deadline_of(c);
+    for (;;) {
+        ncclResult_t s = ncclSuccess;
+        if (ncclCommGetAsyncError(k, &s) != ncclSuccess) return fail(c, err, std::string(what) + ": async state");
+        if (s == ncclSuccess) return BW_OK;
+        if (s != ncclInProgress) return fail(c, err, std::string(what) + ": " + ncclGetErrorString(s));
+        if (Clock::now() > dl)
+            return fail(c, err, std::string(what) + ": no progress within " + std::to_string(c->timeout_ms) + " ms");
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
 }
 
 }  // namespace
@@ -54,25 +111,48 @@ int bw::comm_rank(const bw_comm* c) { return c->rank; }
 int bw::comm_world(const bw_comm* c) { return c->world; }
 int bw::comm_device(const bw_comm* c) { return c->device; }
 uint64_t& bw::comm_cap(bw_comm* c) { return c->cap; }
+bool bw::comm_failed(const bw_comm* c) { return c->failed; }
+
+// Wait for `ev` (recorded after work that includes this communicator's collectives): polls the
+// event and the communicators' async error state until the deadline; aborts on either.
+int bw::comm_wait_event(bw_comm* c, hipEvent_t ev, std::string& err) {
+    if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
+    const auto dl = deadline_of(c);
+    for (uint32_t spin = 0;; spin++) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return BW_OK;
+        if (q != hipErrorNotReady) return fail(c, err, std::string("hipEventQuery: ") + hipGetErrorString(q));
+        if (c->nccl) {
+            const ncclResult_t a = async_state(c);
+            if (a != ncclSuccess && a != ncclInProgress)
+                return fail(c, err, std::string("RCCL async error: ") + ncclGetErrorString(a));
+        }
+        if (Clock::now() > dl)
+            return fail(c, err, "a collective did not complete within " + std::to_string(c->timeout_ms) +
+                                    " ms (a peer failed or stalled)");
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
 
 // d_recv[r * bytes ..] = rank r's d_send[my_rank * bytes ..], for every rank r; ordered on st.
 int bw::comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t bytes, hipStream_t st,
                         std::string& err) {
+    if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
     if (!bytes) return BW_OK;
     const int W = c->world;
     if (c->nccl) {
         if (c->tail_stream && c->tail_stream != st && hipStreamWaitEvent(st, c->tail, 0) != hipSuccess)
             return comm_err(c, err, "hipStreamWaitEvent on the communicator's last collective failed");
-        if (int rc = nccl_chk(c, err, ncclGroupStart(), "ncclGroupStart")) return rc;
-        for (int r = 0; r < W; r++) {
-            ncclResult_t a = ncclSend((const uint8_t*)d_send + r * bytes, bytes, ncclUint8, r, c->nccl, st);
-            ncclResult_t b = ncclRecv((uint8_t*)d_recv + r * bytes, bytes, ncclUint8, r, c->nccl, st);
-            if (a != ncclSuccess || b != ncclSuccess) {
-                ncclGroupEnd();
-                return nccl_chk(c, err, a != ncclSuccess ? a : b, "ncclSend/ncclRecv");
-            }
+        ncclResult_t r = ncclGroupStart();
+        if (r != ncclSuccess) return fail(c, err, std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+        for (int k = 0; k < W && r == ncclSuccess; k++) {
+            r = ncclSend((const uint8_t*)d_send + k * bytes, bytes, ncclUint8, k, c->nccl, st);
+            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv((uint8_t*)d_recv + k * bytes, bytes, ncclUint8, k, c->nccl, st);
+            if (r == ncclInProgress) r = ncclSuccess;
         }
-        if (int rc = nccl_chk(c, err, ncclGroupEnd(), "ncclGroupEnd")) return rc;
+        const ncclResult_t e = ncclGroupEnd();
+        if (r != ncclSuccess) return fail(c, err, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+        if (int rc = settle(c, c->nccl, e, "ncclGroupEnd", err)) return rc;
         if (hipEventRecord(c->tail, st) != hipSuccess) return comm_err(c, err, "hipEventRecord failed");
         c->tail_stream = st;
         return BW_OK;
@@ -92,29 +172,73 @@ int bw::comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t b
     if (hipMemcpyAsync(hs, d_send, total, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return comm_err(c, err, "exchange staging copy (device to host) failed");
-    if (int rc = c->host_fn(c->user, hs, hr, bytes))
-        return comm_err(c, err, "the host all-to-all returned " + std::to_string(rc));
+    if (int rc = c->host_fn(c->user, hs, hr, bytes)) {
+        c->failed = true;  // the caller's transport lost a peer: the ranks no longer agree
+        return comm_err(c, err, "the host all-to-all returned " + std::to_string(rc) + " (communicator failed)");
+    }
     if (hipMemcpyAsync(d_recv, hr, total, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return comm_err(c, err, "exchange staging copy (host to device) failed");
     return BW_OK;
 }
 
-// max of v over the ranks (synchronous): one all-to-all of world x 8 bytes through `scratch`
-// (device, >= 2 * world * 8 bytes)
-int bw::comm_max(bw_comm* c, uint64_t v, uint64_t* out, void* scratch, hipStream_t st, std::string& err) {
+// max of v over the ranks, now (host-synchronous, deadline-bounded).  RCCL: an all-to-all of
+// world x 8 bytes on the control communicator and its own stream, so it never waits for the
+// batches in flight on the data path; host transport: the caller's function on host buffers.
+int bw::comm_max(bw_comm* c, uint64_t v, uint64_t* out, std::string& err) {
+    if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
     const int W = c->world;
-    std::vector<uint64_t> h(W, v);
-    uint64_t* d = (uint64_t*)scratch;
-    if (hipMemcpyAsync(d, h.data(), W * 8, hipMemcpyHostToDevice, st) != hipSuccess)
-        return comm_err(c, err, "hipMemcpyAsync failed");
-    if (int rc = comm_all_to_all(c, d, d + W, 8, st, err)) return rc;
-    if (hipMemcpyAsync(h.data(), d + W, W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return comm_err(c, err, "hipMemcpyAsync failed");
+    std::vector<uint64_t> h(2 * W, v);
+    if (c->nccl) {
+        if (!c->ctl) {  // first agreement: split the control communicator off (every rank gets here
+                        // at its first exchange with an unfixed capacity, in the same call order)
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            const ncclResult_t r1 = ncclCommSplit(c->nccl, 0, c->rank, &c->ctl, &cfg);
+            if (int rc = settle(c, c->ctl ? c->ctl : c->nccl, r1, "ncclCommSplit", err)) return rc;
+        }
+        uint64_t* d = c->ctl_buf;
+        hipStream_t st = c->ctl_st;
+        if (hipMemcpyAsync(d, h.data(), W * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+            return comm_err(c, err, "hipMemcpyAsync failed");
+        ncclResult_t r = ncclGroupStart();
+        for (int k = 0; k < W && (r == ncclSuccess || r == ncclInProgress); k++) {
+            r = ncclSend(d + k, 8, ncclUint8, k, c->ctl, st);
+            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv(d + W + k, 8, ncclUint8, k, c->ctl, st);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r != ncclSuccess && r != ncclInProgress)
+            return fail(c, err, std::string("capacity agreement: ") + ncclGetErrorString(r));
+        if (int rc = settle(c, c->ctl, e, "capacity agreement", err)) return rc;
+        hipEvent_t ev;
+        if (hipMemcpyAsync(h.data() + W, d + W, W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+            return comm_err(c, err, "hipMemcpyAsync failed");
+        hipEventRecord(ev, st);
+        const int rc = comm_wait_event(c, ev, err);
+        hipEventDestroy(ev);
+        if (rc) return rc;
+    } else if (int rc = c->host_fn(c->user, h.data(), h.data() + W, 8)) {
+        c->failed = true;
+        return comm_err(c, err, "the host all-to-all returned " + std::to_string(rc) + " (communicator failed)");
+    }
     uint64_t m = 0;
-    for (uint64_t x : h) m = std::max(m, x);
+    for (int k = 0; k < W; k++) m = std::max(m, h[W + k]);
     *out = m;
+    return BW_OK;
+}
+
+// The bucket capacity for a batch with max_blobs blobs at most: agreed over the ranks on every
+// exchange (it only grows), unless the caller fixed it.
+int bw::comm_agree_cap(bw_comm* c, uint64_t max_blobs, uint64_t* cap, std::string& err) {
+    if (c->cap_fixed) {
+        *cap = c->cap;
+        return BW_OK;
+    }
+    uint64_t m = 0;
+    if (int rc = comm_max(c, max_blobs, &m, err)) return rc;
+    c->cap = std::max(c->cap, m);
+    *cap = c->cap;
     return BW_OK;
 }
 
@@ -130,28 +254,39 @@ extern "C" int bw_comm_unique_id(uint8_t id[BW_COMM_ID_BYTES]) {
     return BW_OK;
 }
 
-extern "C" int bw_comm_init(int device, int rank, int world, const uint8_t id[BW_COMM_ID_BYTES], bw_comm** out) {
+extern "C" int bw_comm_init_timeout(int device, int rank, int world, const uint8_t id[BW_COMM_ID_BYTES],
+                                    uint32_t timeout_ms, bw_comm** out) {
     if (!out) return BW_EINVAL;
     *out = nullptr;
-    if (!id || !world_ok(rank, world)) return BW_EINVAL;
+    if (!id || !world_ok(rank, world) || !timeout_ms) return BW_EINVAL;
     if (hipSetDevice(device) != hipSuccess) return BW_EHIP;
     bw_comm* c = new bw_comm();
     c->device = device;
     c->rank = rank;
     c->world = world;
+    c->timeout_ms = timeout_ms;
     ncclUniqueId u;
     memcpy(u.internal, id, BW_COMM_ID_BYTES);
-    if (hipEventCreateWithFlags(&c->tail, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
-        delete c;
-        return BW_EHIP;
-    }
-    if (ncclCommInitRank(&c->nccl, world, u, rank) != ncclSuccess) {  // blocks until every rank joined
-        hipEventDestroy(c->tail);
-        delete c;
-        return BW_ECOMM;
-    }
+    std::string err;
+    auto bail = [&](int rc) {
+        bw_comm_destroy(c);
+        return rc;
+    };
+    if (hipEventCreateWithFlags(&c->tail, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->ctl_st, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->ctl_buf, 2 * world * 8) != hipSuccess)
+        return bail(BW_EHIP);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;  // every wait below is ours, with a deadline
+    const ncclResult_t r0 = ncclCommInitRankConfig(&c->nccl, world, u, rank, &cfg);
+    if (!c->nccl && r0 == ncclSuccess) return bail(BW_ECOMM);
+    if (settle(c, c->nccl, r0, "ncclCommInitRankConfig", err)) return bail(BW_ECOMM);
     *out = c;
     return BW_OK;
+}
+
+extern "C" int bw_comm_init(int device, int rank, int world, const uint8_t id[BW_COMM_ID_BYTES], bw_comm** out) {
+    return bw_comm_init_timeout(device, rank, world, id, BW_COMM_DEFAULT_TIMEOUT_MS, out);
 }
 
 extern "C" int bw_comm_init_host(int device, int rank, int world, bw_host_all_to_all fn, void* user, bw_comm** out) {
@@ -171,9 +306,23 @@ extern "C" int bw_comm_init_host(int device, int rank, int world, bw_host_all_to
 extern "C" void bw_comm_destroy(bw_comm* c) {
     if (!c) return;
     hipSetDevice(c->device);
-    if (c->tail_stream) hipEventSynchronize(c->tail);
-    if (c->nccl) ncclCommDestroy(c->nccl);
+    if (!c->failed && c->tail_stream) {
+        std::string err;
+        bw::comm_wait_event(c, c->tail, err);  // aborts on a missed deadline instead of hanging
+    }
+    std::string err;
+    for (ncclComm_t* k : {&c->ctl, &c->nccl}) {
+        if (!*k) continue;
+        if (c->failed) {
+            ncclCommAbort(*k);
+        } else if (settle(c, *k, ncclCommFinalize(*k), "ncclCommFinalize", err) == BW_OK) {
+            ncclCommDestroy(*k);
+        }  // else: settle aborted both
+        *k = nullptr;
+    }
     if (c->tail) hipEventDestroy(c->tail);
+    if (c->ctl_st) hipStreamDestroy(c->ctl_st);
+    if (c->ctl_buf) hipFree(c->ctl_buf);
     if (c->pin_send) hipHostFree(c->pin_send);
     delete c;
 }
@@ -181,7 +330,16 @@ extern "C" void bw_comm_destroy(bw_comm* c) {
 extern "C" int bw_comm_set_capacity(bw_comm* c, uint64_t cap) {
     if (!c) return BW_EINVAL;
     c->cap = cap;
+    c->cap_fixed = cap != 0;
     return BW_OK;
 }
+
+extern "C" int bw_comm_set_timeout(bw_comm* c, uint32_t timeout_ms) {
+    if (!c || !timeout_ms) return BW_EINVAL;
+    c->timeout_ms = timeout_ms;
+    return BW_OK;
+}
+
+extern "C" int bw_comm_status(const bw_comm* c) { return !c ? BW_EINVAL : c->failed ? BW_ECOMM : BW_OK; }
 
 extern "C" const char* bw_comm_last_error(const bw_comm* c) { return c ? c->err.c_str() : "null communicator"; }

@@ -9,16 +9,27 @@
 // digest was seeded (prior backups) or appeared at an earlier canonical position.
 //
 // Layout: a digest log (32 B per blob ever submitted, position = canonical sequence number)
-// and an open-addressing table of {key = first 8 digest bytes, seq = min position}.
-//   k_append_claim  copy the batch digests to the log tail; CAS each key into a slot and
-//                   atomicMin the sequence number (first occurrence wins)
-//   k_verdict       dup iff the slot's winner is an earlier position holding the same 32 bytes; a
-//                   different digest behind the same 64-bit key is reported (BW_ECOLLISION),
-//                   never silently merged; the last block advances the log length.
+// and an open-addressing table with one 64-bit word per distinct digest: tag << 40 | seq, where
+// seq is the first (minimum) log position holding that digest and tag is 24 bits of the slot hash
+// (the slot index takes the low bits).  Slots are compared by the FULL 32-byte digest (the
+// reference's HashSet<BlobHash> and binary search compare whole digests, blob_index.rs:109,
+// 130-148): two distinct digests that share their first 8 bytes, or the whole slot hash, simply
+// occupy two slots.  A slot never changes its digest once claimed, so every word of one slot
+// carries the same tag and atomicMin on the word is atomicMin on the position.
+//   k_append   copy the batch digests to the log tail
+//   k_claim    per digest: probe; an empty slot is CAS'd with this position, a slot whose tag
+//              matches is compared with the log entry it points at (written by an earlier launch,
+//              so visible), equal -> atomicMin, different -> keep probing
+//   k_verdict  dup iff the slot holding this digest names an earlier position; the last block
+//              advances the log length.
 #include "bw_device.h"
 #include "bw_internal.h"
 
 namespace bw {
+
+constexpr uint64_t SLOT_EMPTY = ~0ull;
+constexpr int SEQ_BITS = 40;
+constexpr uint64_t SEQ_MASK = (1ull << SEQ_BITS) - 1;
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
     k ^= k >> 33;
@@ -29,14 +40,27 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
     return k;
 }
 
-__device__ __forceinline__ uint64_t digest_key(const uint8_t* d) {
-    const uint64_t k = *(const uint64_t*)d;
-    return k ? k : 1;  // 0 marks an empty slot
+struct Dig {
+    uint4 a, b;
+};
+
+__device__ __forceinline__ Dig load_dig(const uint8_t* p) {
+    const uint4* q = (const uint4*)p;
+    return Dig{q[0], q[1]};
 }
+
+__device__ __forceinline__ bool dig_eq(const Dig& x, const Dig& y) {
+    return ((x.a.x ^ y.a.x) | (x.a.y ^ y.a.y) | (x.a.z ^ y.a.z) | (x.a.w ^ y.a.w) | (x.b.x ^ y.b.x) |
+            (x.b.y ^ y.b.y) | (x.b.z ^ y.b.z) | (x.b.w ^ y.b.w)) == 0;
+}
+
+// slot hash of a digest: fmix64 of its first 8 bytes (the digest is uniformly random already;
+// the mix keeps crafted keys that differ in a few bits apart)
+__device__ __forceinline__ uint64_t dig_hash(const Dig& d) { return fmix64(((uint64_t)d.a.y << 32) | d.a.x); }
 
 __global__ void k_table_clear(uint64_t* __restrict__ table, uint64_t cap) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < cap) { table[2 * i] = 0; table[2 * i + 1] = ~0ull; }
+    if (i < cap) table[i] = SLOT_EMPTY;
 }
 
 void launch_table_clear(hipStream_t st, uint64_t* table, uint64_t cap) {
@@ -47,43 +71,45 @@ __device__ __forceinline__ uint64_t batch_n(const uint64_t* n_dev, uint64_t n_ho
     return n_dev ? *n_dev : n_host;
 }
 
-// Claim position seq, whose digest's key is `key`, into the table: the first occurrence wins.
-__device__ __forceinline__ void claim_key(uint64_t* table, uint64_t cap, uint64_t key, uint64_t seq) {
-    const uint64_t mask = cap - 1;
-    uint64_t s = fmix64(key) & mask;
-    for (;;) {
-        unsigned long long* kp = (unsigned long long*)&table[2 * s];
-        uint64_t k = *kp;
-        if (k == 0) {
-            const uint64_t prev = atomicCAS(kp, 0ull, (unsigned long long)key);
-            k = prev == 0 ? key : prev;
+// Claim log position seq (digest d) into the table: the first occurrence of each distinct digest
+// wins.  Every log entry a slot can point at was written by an earlier launch.
+__device__ __forceinline__ void claim(uint64_t* table, uint64_t cap, const uint8_t* __restrict__ log, const Dig& d,
+                                      uint64_t seq) {
+    const uint64_t mask = cap - 1, h = dig_hash(d), tag = h >> SEQ_BITS;
+    const uint64_t mine = (tag << SEQ_BITS) | seq;
+    uint64_t s = h & mask;
+    for (uint64_t probes = 0; probes <= mask; probes++, s = (s + 1) & mask) {
+        unsigned long long* p = (unsigned long long*)&table[s];
+        uint64_t v = *p;  // possibly stale: an empty read is settled by the CAS, a slot never changes digest
+        if (v == SLOT_EMPTY) {
+            v = atomicCAS(p, (unsigned long long)SLOT_EMPTY, (unsigned long long)mine);
+            if (v == SLOT_EMPTY) return;
         }
-        if (k == key) {
-            atomicMin((unsigned long long*)&table[2 * s + 1], (unsigned long long)seq);
+        if ((v >> SEQ_BITS) == tag && dig_eq(load_dig(log + (v & SEQ_MASK) * 32), d)) {
+            atomicMin(p, (unsigned long long)mine);
             return;
         }
-        s = (s + 1) & mask;
     }
 }
 
-__device__ __forceinline__ void claim(uint64_t* table, uint64_t cap, const uint8_t* log, uint64_t seq) {
-    claim_key(table, cap, digest_key(log + seq * 32), seq);
+// The batch's digests to the log tail.
+__global__ void k_append(uint8_t* __restrict__ log, const uint64_t* dstate, const uint8_t* __restrict__ digests,
+                         const uint64_t* n_dev, uint64_t n_host) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= batch_n(n_dev, n_host)) return;
+    const uint4* s = (const uint4*)(digests + i * 32);
+    uint4* d = (uint4*)(log + (dstate[D_LOGLEN] + i) * 32);
+    d[0] = s[0];
+    d[1] = s[1];
 }
 
-// The batch's digests to the log tail, each claimed at its position as it is written.
-__global__ void k_append_claim(uint64_t* __restrict__ table, uint64_t cap, uint8_t* __restrict__ log,
-                               const uint64_t* dstate, const uint8_t* __restrict__ digests, const uint64_t* n_dev,
-                               uint64_t n_host) {
+// Each appended digest claimed at its position (the log entries are all in place).
+__global__ void k_claim(uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
+                        const uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= batch_n(n_dev, n_host)) return;
     const uint64_t seq = dstate[D_LOGLEN] + i;
-    const uint4* s = (const uint4*)(digests + i * 32);
-    const uint4 s0 = s[0], s1 = s[1];
-    uint4* d = (uint4*)(log + seq * 32);
-    d[0] = s0;
-    d[1] = s1;
-    const uint64_t key = ((uint64_t)s0.y << 32) | s0.x;
-    claim_key(table, cap, key ? key : 1, seq);
+    claim(table, cap, log, load_dig(log + seq * 32), seq);
 }
 
 // Verdicts of the batch (after every claim); the last block to finish advances the log length,
@@ -95,23 +121,24 @@ __global__ void k_verdict(const uint64_t* __restrict__ table, uint64_t cap, cons
     const uint64_t base = dstate[D_LOGLEN];
     if (i < n) {
         const uint64_t seq = base + i;
-        const uint8_t* d = log + seq * 32;
-        const uint64_t key = digest_key(d), mask = cap - 1;
-        uint64_t s = fmix64(key) & mask;
-        while (table[2 * s] != key) s = (s + 1) & mask;
-        const uint64_t w = table[2 * s + 1];
+        const Dig d = load_dig(log + seq * 32);
+        const uint64_t mask = cap - 1, h = dig_hash(d), tag = h >> SEQ_BITS;
+        uint64_t s = h & mask, w = SLOT_EMPTY;
+        for (uint64_t probes = 0; probes <= mask; probes++, s = (s + 1) & mask) {
+            const uint64_t v = table[s];
+            if (v == SLOT_EMPTY) break;  // unreachable: this position's own claim is in the table
+            if ((v >> SEQ_BITS) == tag && ((v & SEQ_MASK) == seq || dig_eq(load_dig(log + (v & SEQ_MASK) * 32), d))) {
+                w = v & SEQ_MASK;
+                break;
+            }
+        }
         uint8_t v;
         if (w == seq) {
             v = 0;
             atomicAdd((unsigned long long*)&dstate[D_NUNIQUE], 1ull);
         } else {
-            const uint4* a = (const uint4*)(log + w * 32);
-            const uint4* b = (const uint4*)d;
-            const uint4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
-            const bool same = a0.x == b0.x && a0.y == b0.y && a0.z == b0.z && a0.w == b0.w && a1.x == b1.x &&
-                              a1.y == b1.y && a1.z == b1.z && a1.w == b1.w;
-            v = same ? 1 : 2;
-            if (!same) atomicOr((unsigned long long*)&dstate[D_COLLIDE], 1ull);
+            v = 1;
+            if (w == SLOT_EMPTY) atomicOr((unsigned long long*)&dstate[D_LOST], 1ull);
         }
         if (is_dup) is_dup[i] = v;
     }
@@ -132,7 +159,8 @@ void launch_dedup(hipStream_t st, uint64_t* table, uint64_t cap, uint8_t* log, u
                   const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n, uint8_t* is_dup) {
     if (!max_n) return;
     const dim3 g((unsigned)((max_n + 255) / 256)), b(256);
-    hipLaunchKernelGGL(k_append_claim, g, b, 0, st, table, cap, log, dstate, digests, n_dev, n_host);
+    hipLaunchKernelGGL(k_append, g, b, 0, st, log, dstate, digests, n_dev, n_host);
+    hipLaunchKernelGGL(k_claim, g, b, 0, st, table, cap, log, dstate, n_dev, n_host);
     hipLaunchKernelGGL(k_verdict, g, b, 0, st, table, cap, log, dstate, n_dev, n_host, is_dup);
 }
 
@@ -140,7 +168,7 @@ __global__ void k_rehash(uint64_t* __restrict__ table, uint64_t cap, const uint8
                          const uint64_t* dstate) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= dstate[D_LOGLEN]) return;
-    claim(table, cap, log, i);
+    claim(table, cap, log, load_dig(log + i * 32), i);
 }
 
 void launch_rehash(hipStream_t st, uint64_t* table, uint64_t cap, const uint8_t* log, const uint64_t* dstate,
@@ -373,7 +401,7 @@ void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_
 // ------------------------------------------------------------------ result records
 
 __device__ __forceinline__ void index_snapshot(const uint64_t* dstate, uint64_t* ctr) {
-    ctr[C_COLLIDE] = dstate[D_COLLIDE];
+    ctr[C_LOST] = dstate[D_LOST];
     ctr[C_NUNIQUE] = dstate[D_NUNIQUE];
     ctr[C_IX_OVF] = dstate[D_BUCKET_OVF];
     ctr[C_IX_LOGLEN] = dstate[D_LOGLEN];

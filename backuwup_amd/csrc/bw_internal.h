@@ -37,7 +37,7 @@ enum Ctr : int {
     C_NBLOBS = 2,    // blobs produced by the batch
     C_NGROUPS = 3,   // BLAKE3 4-leaf groups
     C_SEQBASE = 4,   // dedup log position of the batch's first blob
-    C_COLLIDE = 5,   // 64-bit key collision seen by the index
+    C_LOST = 5,      // a gated digest found no table slot (internal error; the table is kept half empty)
     C_NINVALID = 6,  // files that needed the serial boundary walker
     C_NUNIQUE = 7,   // distinct digests in the index
     C_CANDTOTAL = 8, // gear candidates found (> C_NCAND: the array was too small, see C_TRUNC)
@@ -45,7 +45,7 @@ enum Ctr : int {
     C_TRUNC = 10,    // first byte position whose candidates did not fit the array (BW_NONE: all fit);
                      // the walkers scan the bytes themselves from there on
     // the index's state right after the batch's gate (snapshot by k_pack / k_index_snapshot), read
-    // back with the staged results: C_COLLIDE, C_NUNIQUE and these
+    // back with the staged results: C_LOST, C_NUNIQUE and these
     C_IX_OVF = 11,    // an exchange bucket overflowed (D_BUCKET_OVF)
     C_IX_LOGLEN = 12, // log length (D_LOGLEN)
     C_IX_VALID = 13,  // 1 = the snapshot was taken
@@ -151,17 +151,18 @@ uint32_t b3_calib_blocks_per_cu();  // the leaf pass's occupancy (blocks of 256 
 
 // ------------------------------------------------------------------ launchers (bw_dedup.hip)
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),
-// st[1] = distinct digests, st[2] = collision flag.
+// st[1] = distinct digests, st[2] = a digest found no slot (internal error; never set while the
+// table is kept at most half full).
 // st[3] = an exchange bucket overflowed (a batch had more blobs than the agreed capacity).
 // st[4] = blocks of the running gate's verdict pass that finished (its last block advances st[0]).
-enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_COLLIDE = 2, D_BUCKET_OVF = 3, D_DONE = 4, D_COUNT = 5 };
+enum DState : int { D_LOGLEN = 0, D_NUNIQUE = 1, D_LOST = 2, D_BUCKET_OVF = 3, D_DONE = 4, D_COUNT = 5 };
 void launch_table_clear(hipStream_t st, uint64_t* table, uint64_t cap);
 // Append n digests (n from *n_dev if non-null, else n_host) to the log and decide them in
 // order: is_dup[i] (may be null) = digest seen at an earlier log position.
 void launch_dedup(hipStream_t st, uint64_t* table, uint64_t cap, uint8_t* log, uint64_t* dstate,
                   const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n,
                   uint8_t* is_dup);
-// Re-claim log[0 .. *len) into a fresh table (growth).
+// Re-claim log[0 .. *len) into a fresh table (growth).  The table holds one u64 per slot.
 void launch_rehash(hipStream_t st, uint64_t* table, uint64_t cap, const uint8_t* log,
                    const uint64_t* dstate, uint64_t max_n);
 void launch_partition(hipStream_t st, const uint8_t* digests, uint64_t n, uint32_t n_owners,
@@ -180,7 +181,7 @@ void launch_bucket_expand(hipStream_t st, const uint64_t* counts, uint32_t n_src
 // packed (may be null): the batch's bw_blob records, whose is_dup byte is written as well
 void launch_bucket_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, const uint64_t* counts,
                            uint32_t n_owners, uint64_t cap, uint8_t* is_dup, uint8_t* packed = nullptr);
-// dstate (may be null): the index state snapshot into ctr[C_COLLIDE, C_NUNIQUE, C_IX_*]
+// dstate (may be null): the index state snapshot into ctr[C_LOST, C_NUNIQUE, C_IX_*]
 // host (may be null): pinned memory that also receives ctr and the first host_n records
 void launch_pack(hipStream_t st, uint64_t* ctr, BlobArrays b, const uint64_t* file_start,
                  const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs,
@@ -253,10 +254,17 @@ int comm_rank(const bw_comm* c);
 int comm_world(const bw_comm* c);
 int comm_device(const bw_comm* c);
 uint64_t& comm_cap(bw_comm* c);
+bool comm_failed(const bw_comm* c);
+// wait for ev (after work that includes the communicator's collectives) to the communicator's
+// deadline, polling RCCL's async errors; aborts the communicator on error or timeout (BW_ECOMM)
+int comm_wait_event(bw_comm* c, hipEvent_t ev, std::string& err);
 // all-to-all of equal splits: d_recv[r * bytes ..] = rank r's d_send[my_rank * bytes ..]; on st
 int comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t bytes, hipStream_t st, std::string& err);
-// *out = max of v over the ranks (synchronous); scratch = device, >= 2 * world * 8 bytes
-int comm_max(bw_comm* c, uint64_t v, uint64_t* out, void* scratch, hipStream_t st, std::string& err);
+// *out = max of v over the ranks (host-synchronous; RCCL: the control communicator on its own stream)
+int comm_max(bw_comm* c, uint64_t v, uint64_t* out, std::string& err);
+// the session's bucket capacity for a batch of at most max_blobs blobs: agreed on every call (grows
+// only), or the value fixed by bw_comm_set_capacity
+int comm_agree_cap(bw_comm* c, uint64_t max_blobs, uint64_t* cap, std::string& err);
 
 // ------------------------------------------------------------------ packfiles / index files (bw_pack.hip)
 constexpr uint32_t ZSTD_BLOCK = 131072;           // zstd ZSTD_BLOCKSIZE_MAX

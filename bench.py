@@ -3,7 +3,9 @@
 
 Default workload C2 = a single 16 GiB random stream per GPU, device-resident (BASELINE.json
 configs[1]).  One step = one pass of the hot path over the batch: FastCDC-v2020 (256 KiB / 1 MiB /
-3 MiB) -> BLAKE3 of every chunk -> seen-chunk index (fresh index per step: one backup session).
+3 MiB) -> BLAKE3 of every chunk -> seen-chunk index.  The whole run is one backup session: one
+index for every batch, so after the first step every timed blob is a re-submitted duplicate (the
+gate does the same work for a duplicate as for a new digest: append, claim, full-digest compare).
 Inputs are generated on the GPU (counter-based splitmix64, seed 42 + rank) before timing, so the
 timed region starts with the bytes resident in HBM.
 
@@ -118,6 +120,7 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: the ranks rendezvous over gloo, verify the world size and "
                          "time a CPU stand-in step (no hot path, value null)")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=None, help=argparse.SUPPRESS)  # failure-path test
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default: about 3 s of work for the workload)")
     ap.add_argument("--warmup", type=int, default=2)
@@ -159,7 +162,7 @@ def main():
     ap.add_argument("--split", type=int, default=None, choices=[1, 2],
                     help="BW_OPT_SPLIT: 2 = multi-file batches of 64 MiB-4 GiB as a head and a tail part on two streams")
     ap.add_argument("--b3-upper", type=int, default=None, choices=[0, 1],
-                    help="BW_OPT_B3_UPPER: 1 = upper levels inside the leaf pass (default), 0 = own launch")
+                    help="BW_OPT_B3_UPPER: 0 = upper levels in their own launch (default), 1 = inside the leaf pass")
     ap.add_argument("--b3-group", type=int, default=None, choices=[1, 2, 4],
                     help="BW_OPT_B3_GROUP: BLAKE3 leaves per lane of the leaf pass")
     ap.add_argument("--scan-first", type=int, default=None, choices=[0, 1, 2], help="BW_OPT_SCAN_FIRST")
@@ -208,7 +211,9 @@ def main():
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29511")
-            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+            import datetime  # a rank that never joins (or dies) ends the run instead of hanging it
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(minutes=5))
         if dist.get_world_size() != world:
             raise SystemExit("process group has %d ranks, WORLD_SIZE says %d" % (dist.get_world_size(), world))
 
@@ -276,6 +281,7 @@ def main():
         torch.cuda.synchronize()
 
     step_no = [0]
+    cap_fixed = [False]
     data_ptr = data.data_ptr()
     host_ptr = host.data_ptr() if host is not None else None
     file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
@@ -331,6 +337,9 @@ def main():
         t = submit(c)
         host_ms[0] += (time.perf_counter() - th) * 1e3
         if multi:
+            if not cap_fixed[0]:  # every batch has the same bound: fix the bucket capacity once (no
+                cap_fixed[0] = True  # per-batch agreement on the control communicator)
+                comm.set_capacity(c.batch_views(t)[3])
             c.exchange_dedup(comm, t)  # owner = digest[0] >> (8 - log2 N); verdicts back into the batch
         inflight.append((c, t))
         if len(inflight) >= len(ctxs):  # one batch per context in flight: read the oldest while the rest run
@@ -500,6 +509,9 @@ def dry_run(args):
     buf = np.random.default_rng(rank).integers(0, 256, 1 << 20, dtype=np.uint8)
     for _ in range(args.warmup):
         int(buf.sum())
+    if args.dry_run_fail_rank == rank:  # a rank that dies mid-run: the launcher must exit non-zero
+        log("bench: dry run: rank %d fails on purpose" % rank)
+        os._exit(3)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()

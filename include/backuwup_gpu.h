@@ -44,7 +44,7 @@ enum {
     BW_ENOSPC = -2,     /* caller's output array too small; *n_out = required count            */
     BW_EHIP = -3,       /* HIP runtime error (message in bw_last_error)                        */
     BW_ENOMEM = -4,     /* device or host allocation failed                                    */
-    BW_ECOLLISION = -5, /* two distinct digests share a 64-bit table key: verdicts withheld    */
+    BW_ECOLLISION = -5, /* not returned since round 4: the index compares whole digests        */
     BW_ESTATE = -6,     /* call order violated (e.g. bw_results before a batch was submitted)   */
     BW_ECRYPTO = -7,    /* an AES-GCM tag did not verify (PackfileError::CryptoError)           */
     BW_EFORMAT = -8,    /* bincode deserialization failed (PackfileError::SerializationError)   */
@@ -131,8 +131,10 @@ int bw_index_check_insert(bw_ctx* ctx, const uint8_t* digests, uint64_t n, uint8
 /* number of distinct digests currently in the index */
 int bw_index_size(bw_ctx* ctx, uint64_t* n);
 
-/* Any index error is sticky: BW_ECOLLISION if two distinct digests sharing a 64-bit key were
- * ever seen since the last reset (synchronizes; the device-side gate below does not check). */
+/* Any index error is sticky until the next reset: BW_ENOSPC if an exchange bucket overflowed
+ * (synchronizes; the device-side gate below does not check).  Distinct digests that share any
+ * prefix are distinct entries: slots are compared by all 32 bytes, as the reference's HashSet and
+ * binary search do (blob_index.rs:109,130-148). */
 int bw_index_check(bw_ctx* ctx);
 
 /* ---- one index shared by several contexts (one backup session, several batches in flight) ----
@@ -290,16 +292,30 @@ int bw_scatter_buckets(bw_ctx* ctx, const uint8_t* d_verdicts, const uint64_t* d
 typedef struct bw_comm bw_comm;
 typedef int (*bw_host_all_to_all)(void* user, const void* send, void* recv, uint64_t bytes_per_rank);
 int bw_comm_unique_id(uint8_t id[BW_COMM_ID_BYTES]);
-/* world: a power of two <= 256; device must be the device of the contexts it serves. */
+/* world: a power of two <= 256; device must be the device of the contexts it serves.
+ * Every wait on the peers has a deadline (the reference's transport sends with timeouts,
+ * net_p2p/transport.rs:127-128): initialisation, each collective's enqueue, the capacity
+ * agreement and bw_wait of an exchanged batch.  On an RCCL error or a missed deadline the
+ * communicator is aborted (ncclCommAbort), the call returns BW_ECOMM, and so does every later
+ * call on it; bw_comm_destroy then only releases it.  bw_comm_init uses the default deadline. */
+#define BW_COMM_DEFAULT_TIMEOUT_MS 120000u
 int bw_comm_init(int device, int rank, int world, const uint8_t id[BW_COMM_ID_BYTES], bw_comm** out);
+int bw_comm_init_timeout(int device, int rank, int world, const uint8_t id[BW_COMM_ID_BYTES], uint32_t timeout_ms,
+                         bw_comm** out);
+int bw_comm_set_timeout(bw_comm* comm, uint32_t timeout_ms);
+/* BW_OK, or BW_ECOMM once the communicator was aborted (a peer failed or stalled). */
+int bw_comm_status(const bw_comm* comm);
 int bw_comm_init_host(int device, int rank, int world, bw_host_all_to_all fn, void* user, bw_comm** out);
 void bw_comm_destroy(bw_comm* comm);
 const char* bw_comm_last_error(const bw_comm* comm);
-/* Digest slots per (source, owner) bucket for the session: 0 (default) = agreed at the first
- * exchange as the largest max_blobs over the ranks (one synchronous all-to-all).  A later batch
- * with more blobs for one owner than the capacity sets the sticky BW_ENOSPC of bw_index_check. */
+/* Digest slots per (source, owner) bucket.  0 (default): agreed on every exchange as the largest
+ * max_blobs over the ranks so far (8 bytes per rank over a second RCCL communicator on its own
+ * stream, so it never waits for the batches in flight; it only grows).  A fixed capacity skips
+ * the agreement; a batch with more blobs for one owner than it sets the sticky BW_ENOSPC of
+ * bw_index_check. */
 int bw_comm_set_capacity(bw_comm* comm, uint64_t cap);
-/* Batch `ticket` of ctx (0 = the most recent; submitted with BW_F_NO_DEDUP, else BW_ESTATE):
+/* Batch `ticket` of ctx (0 = the most recent; submitted with BW_F_NO_DEDUP and hashed, else
+ * BW_ESTATE):
  * partition its digests by owner = digest[0] >> (8 - log2 world), all-to-all of the counts and
  * the buckets, the owner's gate against ctx's index, all-to-all of the verdicts back, scattered
  * into the batch's is_dup (bw_wait / bw_batch_views see them).  Enqueued on ctx's stream with no

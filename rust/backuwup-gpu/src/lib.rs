@@ -47,6 +47,7 @@ pub mod ffi {
     pub const BW_F_NO_DEDUP: u32 = 2;
     pub const BW_F_SERIAL_RESOLVE: u32 = 4;
     pub const BW_COMM_ID_BYTES: usize = 128;
+    pub const BW_COMM_DEFAULT_TIMEOUT_MS: u32 = 120000;
     pub const BW_PACK_ZSTD_STORE: u32 = 1;
 
     #[repr(C)]
@@ -202,6 +203,10 @@ pub mod ffi {
 
         pub fn bw_comm_unique_id(id: *mut u8) -> c_int;
         pub fn bw_comm_init(device: c_int, rank: c_int, world: c_int, id: *const u8, out: *mut *mut bw_comm) -> c_int;
+        pub fn bw_comm_init_timeout(device: c_int, rank: c_int, world: c_int, id: *const u8, timeout_ms: u32,
+                                    out: *mut *mut bw_comm) -> c_int;
+        pub fn bw_comm_set_timeout(comm: *mut bw_comm, timeout_ms: u32) -> c_int;
+        pub fn bw_comm_status(comm: *const bw_comm) -> c_int;
         pub fn bw_comm_init_host(device: c_int, rank: c_int, world: c_int, fn_: bw_host_all_to_all, user: *mut c_void,
                                  out: *mut *mut bw_comm) -> c_int;
         pub fn bw_comm_destroy(comm: *mut bw_comm);
@@ -486,14 +491,31 @@ impl Comm {
         Ok(id)
     }
 
-    /// RCCL communicator of `world` ranks (blocks until every rank joined).
+    /// RCCL communicator of `world` ranks (waits until every rank joined, at most the default
+    /// deadline; a rank that never joins gives BW_ECOMM instead of a hang).
     pub fn rccl(device: i32, rank: i32, world: i32, id: &[u8; ffi::BW_COMM_ID_BYTES]) -> Result<Comm> {
+        Self::rccl_with_timeout(device, rank, world, id, ffi::BW_COMM_DEFAULT_TIMEOUT_MS)
+    }
+
+    /// As `rccl`, with the deadline of every wait on the peers (like the reference transport's
+    /// send timeouts, net_p2p/transport.rs:127-128).
+    pub fn rccl_with_timeout(device: i32, rank: i32, world: i32, id: &[u8; ffi::BW_COMM_ID_BYTES],
+                             timeout_ms: u32) -> Result<Comm> {
         let mut raw = std::ptr::null_mut();
-        let rc = unsafe { ffi::bw_comm_init(device, rank, world, id.as_ptr(), &mut raw) };
+        let rc = unsafe { ffi::bw_comm_init_timeout(device, rank, world, id.as_ptr(), timeout_ms, &mut raw) };
         if rc != ffi::BW_OK {
-            return Err(Error { rc, msg: "bw_comm_init".into() });
+            return Err(Error { rc, msg: "bw_comm_init_timeout".into() });
         }
         Ok(Comm { raw, _host: None })
+    }
+
+    /// Ok while usable; Err(BW_ECOMM) once a failed or stalled peer made the library abort it.
+    pub fn status(&self) -> Result<()> {
+        let rc = unsafe { ffi::bw_comm_status(self.raw) };
+        if rc != ffi::BW_OK {
+            return Err(Error { rc, msg: message(unsafe { ffi::bw_comm_last_error(self.raw) }) });
+        }
+        Ok(())
     }
 
     /// The caller's transport: `a2a(send, recv, bytes_per_rank)` delivers `send[r * b ..]` to rank

@@ -38,6 +38,19 @@ def test_bench_gpus_n_launches_n_ranks(n):
     assert rec["config"]["parallelism"] == "dp%d" % n
 
 
+def test_bench_rank_failure_exits_nonzero():
+    """one rank of `bench.py --gpus 2` dies after warmup while its peer waits in the
+    timing barrier; the launcher tears the survivor down and exits non-zero (no hang, no line)."""
+    import time
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--no-power",
+                          "--steps", "2", "--warmup", "1", "--dry-run-fail-rank", "1"], env=_env(),
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode != 0, out.stderr[-3000:]
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert time.time() - t0 < 200
+
+
 def test_bench_refuses_world_mismatch():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--no-power"],
                          env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from backuwup_amd import Context, Index, make_params, make_tree
-from backuwup_amd._lib import (BW_ECOLLISION, BW_ESTATE, BW_F_NO_DEDUP, BW_OPT_CAND_CAP, BW_OPT_DEPTH,
+from backuwup_amd._lib import (BW_ESTATE, BW_F_NO_DEDUP, BW_OPT_CAND_CAP, BW_OPT_DEPTH,
                                BW_OPT_STAGE_CHUNK, BwError)
 from backuwup_amd.synth import small_files, splitmix_bytes, tree_corpus, vm_image_variants
 
@@ -278,25 +278,96 @@ def test_candidate_array_truncation(oracle, cap):
                     oracle.process_files(data, offs, lens, *MID, threads=8))
 
 
-def test_device_gate_reports_collisions():
-    """Two distinct digests sharing the 64-bit table key: the device-side gate (the sharded
-    owner's path) writes verdict 2 and bw_index_check raises BW_ECOLLISION afterwards."""
+def _colliding_digests(seed):
+    """Digests built to collide in the index's 64-bit key: 40 groups of 2-12 distinct digests
+    that share their first 8 bytes (one group with key 0, one with key 1 -- the old table mapped
+    key 0 onto key 1), some sharing 16, 24 or 31 bytes, plus random singletons."""
+    rng = np.random.default_rng(seed)
+    groups = []
+    for g in range(40):
+        k = int(rng.integers(2, 13))
+        a = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+        a[:, :8] = a[0, :8]
+        if g == 0:
+            a[:, :8] = 0
+        elif g == 1:
+            a[:, :8] = 0
+            a[:, 0] = 1
+        elif g % 5 == 2:
+            n = int(rng.choice([16, 24, 31]))
+            a[:, :n] = a[0, :n]
+            a[:, 31] = np.arange(k, dtype=np.uint8) + a[0, 31]  # keep the rows distinct
+        groups.append(a)
+    a = np.concatenate(groups + [rng.integers(0, 256, (200, 32), dtype=np.uint8)])
+    # a group sharing 31 of 32 bytes
+    t = np.repeat(rng.integers(0, 256, (1, 32), dtype=np.uint8), 6, axis=0)
+    t[:, 31] = np.arange(6, dtype=np.uint8)
+    a = np.concatenate([a, t])
+    assert len({bytes(x) for x in a}) == len(a)
+    return a
+
+
+def _oracle_verdicts(oracle, seq, seed=b""):
+    ix = oracle.Index(seed)
+    out = []
+    for d in seq:
+        dup = ix.is_blob_duplicate(d.tobytes())
+        if not dup:
+            ix.insert(d.tobytes())
+        out.append(int(dup))
+    return out
+
+
+def test_index_key_collisions_bit_exact(oracle):
+    """distinct digests that share the table's 64-bit key (and longer prefixes)
+    are distinct entries, as in the reference's full-digest HashSet / binary search
+    (blob_index.rs:109,130-148).  Host gate, device gate, the exchange owner's bucket gate, a
+    seeded index and table growth (rehash) are all bit-exact against oracle.Index, and no call
+    reports an error."""
     import torch
-    a = np.random.default_rng(1).integers(0, 256, (3, 32), dtype=np.uint8)
-    a[1, :8] = a[0, :8]
+    pool = _colliding_digests(7)
+    rng = np.random.default_rng(8)
+    seed_rows = pool[rng.choice(len(pool), 60, replace=False)]
+    seed = np.array(sorted(seed_rows.tolist()), dtype=np.uint8)
+    batches = [pool[rng.integers(0, len(pool), n)] for n in (500, 1, 777, 3000)]
+    want = _oracle_verdicts(oracle, np.concatenate(batches), b"".join(bytes(x) for x in seed))
     with Context(0) as c:
+        # host path, seeded, tiny table hint so the batches force growth + rehash
+        c.index_reset(16)
+        c.index_seed(seed)
+        got = np.concatenate([c.index_check_insert(b) for b in batches])
+        assert got.tolist() == want
+        c.index_check()
+        distinct = {bytes(x) for x in np.concatenate(batches + [seed])}
+        assert c.index_size() == len(distinct)
+        # device path (the gate of a submitted batch and of bw_index_check_insert_device)
+        c.index_reset(16)
+        c.index_seed(seed)
+        got = []
+        for b in batches:
+            d = torch.from_numpy(np.ascontiguousarray(b).reshape(-1)).cuda()
+            v = torch.full((len(b),), 7, dtype=torch.uint8, device="cuda")
+            c.index_check_insert_device(d.data_ptr(), len(b), v.data_ptr())
+            torch.cuda.synchronize()
+            got.append(v.cpu().numpy())
+        assert np.concatenate(got).tolist() == want
+        c.index_check()
+        # the exchange owner's gate: two source buckets of cap slots, source-major order
         c.index_reset()
-        d = torch.from_numpy(a.reshape(-1)).cuda()
-        v = torch.zeros(3, dtype=torch.uint8, device="cuda")
+        cap = 2000
+        src = [pool[rng.integers(0, len(pool), 1500)], pool[rng.integers(0, len(pool), 900)]]
+        bk = np.zeros((2, cap, 32), np.uint8)
+        for j, s in enumerate(src):
+            bk[j, :len(s)] = s
+        d_bk = torch.from_numpy(bk.reshape(-1)).cuda()
+        d_cnt = torch.tensor([len(s) for s in src], dtype=torch.int64, device="cuda")
+        d_v = torch.full((2 * cap,), 7, dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()
-        c.index_check_insert_device(d.data_ptr(), 3, v.data_ptr())
-        with pytest.raises(BwError) as e:
-            c.index_check()
-        assert e.value.rc == BW_ECOLLISION
+        c.index_check_insert_buckets(d_bk.data_ptr(), d_cnt.data_ptr(), 2, cap, d_v.data_ptr())
         torch.cuda.synchronize()
-        assert v.cpu().tolist()[1] == 2
-        c.index_reset()
-        c.index_check()  # a reset clears it
+        v = d_v.cpu().numpy().reshape(2, cap)
+        assert np.concatenate([v[0, :1500], v[1, :900]]).tolist() == _oracle_verdicts(oracle, np.concatenate(src))
+        c.index_check()
 
 
 def test_tree_pack_tree_on_one_context(oracle):
@@ -465,11 +536,28 @@ def test_exchange_dedup_rccl_world1_c_abi(oracle):
         with pytest.raises(BwError) as e:
             cs[0].exchange_dedup(comm, tk)
         assert e.value.rc == BW_ESTATE
-        # capacity agreed at the first exchange (batch 0's 1000-blob bound): a later, larger batch
-        # overflows its bucket and says so instead of returning incomplete verdicts
-        from backuwup_amd._lib import BW_ENOSPC
+        # a batch hashed with BW_F_NO_HASH has no digests to exchange
+        from backuwup_amd._lib import BW_ENOSPC, BW_F_NO_HASH
+        tk = cs[0].submit_device(devs[0].data_ptr(), batches[0][0].size, batches[0][1], batches[0][2],
+                                 make_params(flags=BW_F_NO_DEDUP | BW_F_NO_HASH))
+        with pytest.raises(BwError) as e:
+            cs[0].exchange_dedup(comm, tk)
+        assert e.value.rc == BW_ESTATE
+        # the capacity is agreed on every exchange: a later batch with twice the first
+        # one's bound grows it on every rank and gets complete verdicts
         cs[0].index_reset(1 << 16)
         comm2 = Comm.rccl(0, 0, 1, unique_id())
+        want2 = oracle_session(oracle, [batches[0], batches[3]])
+        for j, k in enumerate((0, 3)):
+            d, o, l = batches[k]
+            tk = cs[0].submit_device(devs[k].data_ptr(), d.size, o, l, p)
+            cs[0].exchange_dedup(comm2, tk)
+            blobs_equal(cs[0].wait(tk), want2[j], ("grown", k))
+        cs[0].index_check()
+        # a capacity fixed by the caller is not agreed: a larger batch overflows its bucket and
+        # says so instead of returning incomplete verdicts
+        cs[0].index_reset(1 << 16)
+        comm2.set_capacity(1000)
         for k in (0, 3):
             d, o, l = batches[k]
             tk = cs[0].submit_device(devs[k].data_ptr(), d.size, o, l, p)
@@ -502,8 +590,10 @@ def _two_rank_c_worker(rank, world, port, q):
         with Context(0) as c, Comm.host(0, rank, world, gloo_all_to_all()) as comm:
             c.index_reset(1 << 16)
             for batch in range(3):  # batch-major, then rank-major canonical order
-                lo = ((batch % 2) * world + rank) * per // 2
-                hi = lo + per // 2 - 7 * rank * (batch == 2)  # ragged: the ranks' batch sizes differ
+                lo = ((batch % 2) * world + rank) * per // 4
+                hi = lo + per // 4 - 7 * rank * (batch == 1)  # ragged: the ranks' batch sizes differ
+                if batch == 2 and rank == 1:  # 4x the bound of its first batch: the capacity grows
+                    lo, hi = 2 * per // 2, 2 * per // 2 + per
                 b = _slices(data, offs, lens, [(lo, hi)])[0]
                 t_dev = torch.from_numpy(b[0]).cuda()
                 tk = c.submit_device(t_dev.data_ptr(), b[0].size, b[1], b[2], make_params(flags=BW_F_NO_DEDUP))
@@ -542,6 +632,104 @@ def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
             want = oracle.process_files(*_slices(data, offs, lens, [(lo, hi)])[0], index=ix)
             assert np.array_equal(dig, want["digest"]) and np.array_equal(dup, want["is_dup"]), (batch, r)
     assert got[0][2][3].all()  # batch 2 repeats batch 0 on rank 0
+
+
+def _dying_peer_worker(rank, world, port, q):
+    """Rank 1 leaves after the first exchange (os._exit, no goodbye); rank 0's next exchange must
+    fail with BW_ECOMM within the deadline instead of hanging (VERDICT r3 #4)."""
+    import datetime
+    import os
+    import time
+    import torch
+    import torch.distributed as dist
+    from backuwup_amd._lib import BW_ECOMM
+    from backuwup_amd.comm import Comm, gloo_all_to_all
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=20))
+    data, offs, lens = small_files(800, seed=57)
+    with Context(0) as c, Comm.host(0, rank, world, gloo_all_to_all()) as comm:
+        c.index_reset(1 << 14)
+        res = []
+        for batch in range(2):
+            b = _slices(data, offs, lens, [((2 * batch + rank) * 200, (2 * batch + rank + 1) * 200)])[0]
+            t_dev = torch.from_numpy(b[0]).cuda()
+            tk = c.submit_device(t_dev.data_ptr(), b[0].size, b[1], b[2], make_params(flags=BW_F_NO_DEDUP))
+            if batch == 1 and rank == 1:
+                q.put((rank, "left"))
+                q.close()
+                q.join_thread()  # flush the queue's feeder before leaving without teardown
+                os._exit(0)
+            t0 = time.time()
+            try:
+                c.exchange_dedup(comm, tk)
+                c.wait(tk)
+                res.append("ok")
+            except BwError as e:
+                res.append((e.rc, round(time.time() - t0, 1), comm.status()))
+                # every later call on the failed communicator fails at once
+                t1 = time.time()
+                with pytest.raises(BwError) as e2:
+                    c.exchange_dedup(comm, tk)
+                res.append((e2.value.rc, round(time.time() - t1, 1)))
+        q.put((rank, res))
+    q.close()
+    q.join_thread()
+    os._exit(0)  # the process group lost a member: skip its teardown
+
+
+def test_exchange_peer_failure_returns_ecomm():
+    """Host transport (gloo) with two ranks on the one GPU: the survivor of a peer that dies gets
+    BW_ECOMM from bw_exchange_dedup well within the transport's 20 s deadline, the communicator
+    reports itself failed, and later calls fail immediately."""
+    import socket
+    import torch.multiprocessing as mp
+    from backuwup_amd._lib import BW_ECOMM
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dying_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got[1] == "left"
+    first, (rc, dt, status), (rc2, dt2) = got[0]
+    assert first == "ok"
+    assert rc == BW_ECOMM and status == BW_ECOMM and dt < 30, got[0]
+    assert rc2 == BW_ECOMM and dt2 < 1, got[0]
+
+
+_NEVER_JOINED = """
+import sys, time
+sys.path.insert(0, %r)
+from backuwup_amd.comm import Comm, unique_id
+from backuwup_amd._lib import BwError
+t0 = time.time()
+try:
+    Comm.rccl(0, 0, 2, unique_id(), timeout_ms=4000)
+    print("JOINED")
+except BwError as e:
+    print("RC", e.rc, round(time.time() - t0, 1))
+"""
+
+
+def test_rccl_init_deadline_when_a_rank_never_joins():
+    """bw_comm_init_timeout with world 2 and no rank 1: the non-blocking RCCL initialisation is
+    aborted at the deadline and returns BW_ECOMM (it used to block forever).  Run in a child with
+    its own time limit so a regression cannot stall the suite."""
+    import subprocess
+    import sys
+    from backuwup_amd._lib import BW_ECOMM
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _NEVER_JOINED % root], capture_output=True, text=True, timeout=90)
+    line = [l for l in out.stdout.splitlines() if l.startswith(("RC", "JOINED"))]
+    assert line and line[0].startswith("RC"), (out.stdout[-2000:], out.stderr[-2000:])
+    _, rc, dt = line[0].split()
+    assert int(rc) == BW_ECOMM and 3.5 < float(dt) < 30, line
 
 
 @pytest.mark.parametrize("scan_waves,latency,loads,upper,group",

@@ -4,8 +4,15 @@
 # back-off it announces.  Never retries a command that actually ran on the GPU.
 cmd="$1"; tmo="${2:-1200}"
 for i in 1 2 3 4 5 6 7 8; do
-  # keep the previous call's results out of the way (not deleted: copy what matters to profiles/)
-  if [ -n "$(ls -A gpurun_out 2>/dev/null)" ]; then d=/tmp/gpurun_prev_$(date +%s); mkdir -p $d; mv gpurun_out/* $d/; fi
+  # archive the previous call's scratch where the judge can read it: every file (the verdict
+  # .last_call.json and any .graft_* marker included) goes to profiles/<round>/calls/<time>/; files
+  # over 8 MiB (raw traces) are listed there by size instead of copied
+  if [ -n "$(ls -A gpurun_out 2>/dev/null)" ]; then
+    d=profiles/${GPU_ROUND:-r04}/calls/$(date +%Y%m%d_%H%M%S); mkdir -p "$d"
+    (cd gpurun_out && find . -type f -size -8M -exec cp --parents {} "../$d" \;)
+    (cd gpurun_out && find . -type f -size +8M -printf '%s %p\n') > "$d/_large_files.txt"
+    rm -rf gpurun_out/* gpurun_out/.[!.]*
+  fi
   out=$(/usr/local/graft/bin/gpurun --timeout "$tmo" -- "$cmd" 2>&1); rc=$?
   echo "[$(date +%T) attempt $i rc=$rc]"; echo "$out" | tail -4
   if [ $rc = 3 ] || echo "$out" | grep -q "status=transient"; then
