@@ -159,6 +159,7 @@ SIGNATURES = [
                                            ctypes.c_uint64, u64p, u64p]),
     ("bw_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
+    ("bw_profile_intervals", ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, u64p]),
     ("bw_calibrate_b3", ctypes.c_int, [vp, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
 ]
 

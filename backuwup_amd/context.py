@@ -550,6 +550,18 @@ class Context:
         check(self._L.bw_profile_read(self.h, ms, ctypes.byref(n)), self.h)
         return {s: ms[i] for i, s in enumerate(_lib.STAGES)}, n.value
 
+    def profile_intervals(self, stage):
+        """[(start_ms, end_ms)] of one stage over the profiled batches, on the device's timeline
+        (shared by every context of the device)."""
+        k = _lib.STAGES.index(stage)
+        n = ctypes.c_uint64()
+        rc = self._L.bw_profile_intervals(self.h, k, None, 0, ctypes.byref(n))
+        if rc not in (0, _lib.BW_ENOSPC):
+            check(rc, self.h)
+        buf = (ctypes.c_double * max(2 * n.value, 1))()
+        check(self._L.bw_profile_intervals(self.h, k, buf, n.value, ctypes.byref(n)), self.h)
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(n.value)]
+
     def calibrate_b3(self, ms=100.0):
         """The BLAKE3 leaf pass's compression from registers on every CU for about `ms` ms:
         {gbs, ghz, bytes_per_clk_cu, launch_ms} -- the pass's integer-issue ceiling on this chip."""

@@ -202,6 +202,7 @@ struct bw_ctx {
     bool ev_pending[2] = {false, false};
     int ev_set = 0;
     double stage_ms[BW_N_STAGES] = {};
+    std::vector<double> intervals[BW_N_STAGES];  // [start, end) ms since the device's reference event
     uint64_t prof_batches = 0;
 };
 
@@ -315,17 +316,39 @@ static uint64_t seg_len_for(const Masks& mk, bool small_batch) {
 // recorded between two kernels costs the stream ~5.5 us of idle time (profiles/r03: k_scan ->
 // k_tile_partial with a mark between them 5.7 us, kernels without one 0), so the bench's timed
 // region marks only the leaf pass.
+// One timing event per device, recorded when a context of the device first enables profiling: the
+// stage intervals of every context of the device are placed on its timeline, so a caller can take
+// the union of one stage's launches across contexts (bw_profile_intervals).
+static std::mutex g_ref_mu;
+static hipEvent_t g_ref[64] = {};
+
+static hipEvent_t prof_reference(int device, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_ref_mu);
+    if (device < 0 || device >= 64) return nullptr;
+    if (!g_ref[device] && hipEventCreateWithFlags(&g_ref[device], EV_TIMING) == hipSuccess) {
+        hipEventRecord(g_ref[device], st);
+        hipEventSynchronize(g_ref[device]);
+    }
+    return g_ref[device];
+}
+
 static void prof_collect(bw_ctx* c, int set) {
     if (!c->ev_pending[set]) return;
     const uint32_t mask = c->prof_mask;
     const int last = 31 - __builtin_clz(mask);
     hipEventSynchronize(c->ev[set][last]);
+    hipEvent_t ref = prof_reference(c->device, c->stream);
     for (int i = 0; i < last; i++) {
         if (!((mask >> i) & 1)) continue;
         int j = i + 1;
         while (!((mask >> j) & 1)) j++;
         float ms = 0;
         if (hipEventElapsedTime(&ms, c->ev[set][i], c->ev[set][j]) == hipSuccess) c->stage_ms[i] += ms;
+        float t0 = 0;
+        if (ref && hipEventElapsedTime(&t0, ref, c->ev[set][i]) == hipSuccess) {
+            c->intervals[i].push_back(t0);
+            c->intervals[i].push_back((double)t0 + ms);
+        }
     }
     c->prof_batches++;
     c->ev_pending[set] = false;
@@ -1791,7 +1814,11 @@ extern "C" int bw_profile_enable(bw_ctx* c, int on) {
             if (!c->ev[k][i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev[k][i], EV_TIMING));
     }
     c->prof = on != 0;
-    for (int i = 0; i < BW_N_STAGES; i++) c->stage_ms[i] = 0;
+    if (c->prof) prof_reference(c->device, c->stream);
+    for (int i = 0; i < BW_N_STAGES; i++) {
+        c->stage_ms[i] = 0;
+        c->intervals[i].clear();
+    }
     c->prof_batches = 0;
     return BW_OK;
 }
@@ -1807,6 +1834,17 @@ extern "C" int bw_profile_read(bw_ctx* c, double* stage_ms, uint64_t* n_batches)
     if (stage_ms)
         for (int i = 0; i < BW_N_STAGES; i++) stage_ms[i] = c->stage_ms[i] + (c->helper ? c->helper->stage_ms[i] : 0);
     if (n_batches) *n_batches = c->prof_batches;
+    return BW_OK;
+}
+
+extern "C" int bw_profile_intervals(bw_ctx* c, int stage, double* out, uint64_t cap, uint64_t* n) {
+    if (!c || !n || stage < 0 || stage >= BW_N_STAGES || (cap && !out)) return BW_EINVAL;
+    prof_collect(c, 0);
+    prof_collect(c, 1);
+    const std::vector<double>& v = c->intervals[stage];
+    *n = v.size() / 2;
+    if (*n > cap) return BW_ENOSPC;
+    if (*n) memcpy(out, v.data(), v.size() * sizeof(double));
     return BW_OK;
 }
 

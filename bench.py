@@ -381,9 +381,24 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    ctx.index_check()  # no 64-bit key collision anywhere in the session
+    ctx.index_check()  # no sticky index error anywhere in the session
     stage_ms, nbatch = ctx.profile_read()
     per = {s: stage_ms[s] / max(nbatch, 1) for s in STAGES}
+    # the leaf pass's active time per step: the union of its launches' intervals over every context
+    # (two contexts' leaf passes overlap each other in time, so the mean launch duration can exceed
+    # the step time; the union cannot)
+    leaf_iv = sorted(iv for c in ctxs for iv in c.profile_intervals("b3_leaf"))
+    leaf_union, cur = 0.0, None
+    for a, z in leaf_iv:
+        if cur is None or a > cur[1]:
+            if cur is not None:
+                leaf_union += cur[1] - cur[0]
+            cur = [a, z]
+        else:
+            cur[1] = max(cur[1], z)
+    if cur is not None:
+        leaf_union += cur[1] - cur[0]
+    leaf_active_ms = leaf_union / args.steps if leaf_iv else None
     iso = None
     if not multi and host is None:
         # the same batch with nothing beside it (one context, synchronized, every stage marked):
@@ -411,15 +426,27 @@ def main():
     # below, in every configuration); the timed region marks only it
     dom = max(["scan", "b3_leaf"], key=lambda s: per[s]) if args.all_stage_marks else "b3_leaf"
     algo = processed if dom == "b3_leaf" else n
-    achieved = algo / (per[dom] * 1e-3) / 1e9
+    # achieved = the launch's bytes / the kernel's active time per step (the union above); the
+    # mean launch duration (live, overlapping) stays beside it
+    active_ms = leaf_active_ms if (dom == "b3_leaf" and leaf_active_ms) else per[dom]
+    achieved = algo / (active_ms * 1e-3) / 1e9
     loads = args.b3_loads if args.b3_loads is not None else BW_B3_LOADS_DEFAULT
     leaf_kernel = "k_b3_lines" if loads == 2 else "k_b3_groups"
     kernel = {"scan": "k_scan", "b3_leaf": leaf_kernel}[dom]
-    traffic, traffic_src = pmc_traffic(args, kernel)
+    traffic, traffic_src, path_bytes = pmc_traffic(args, kernel)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": kernel,
                 "algorithmic_bytes_per_launch": algo,
+                "kernel_active_ms_per_step": round(active_ms, 4),
+                "kernel_active_basis": ("union of the %s launches' intervals over the %d contexts, per timed step "
+                                        "(library events on the launches' own streams)" % (kernel, len(ctxs))
+                                        if active_ms is leaf_active_ms else "mean launch duration"),
+                "launch_ms_mean": round(per[dom], 4),
+                # the whole pipeline against HBM: this GPU's input bytes per second / 8 TB/s
+                "pipeline_frac": round(value / world / HBM_PEAK_GBS, 4),
+                # every kernel of a batch (PMC FETCH + WRITE), per input byte: 1.0 would be one pass
+                "path_bytes_per_input_byte": path_bytes,
                 "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
     valu = None
     if kernel == leaf_kernel and not args.no_calibrate:
@@ -904,21 +931,24 @@ def pmc_traffic(args, kernel):
     from backuwup_amd.build import source_digest
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if args.workload != "c2" or args.host_stream or not os.path.exists(path):
-        return None, None
+        return None, None, None
     try:
         pmc = json.load(open(path))
     except (OSError, ValueError):
-        return None, {"file": "profiles/pmc_traffic.json", "status": "unreadable"}
+        return None, {"file": "profiles/pmc_traffic.json", "status": "unreadable"}, None
     prov = {"file": "profiles/pmc_traffic.json", "commit": pmc.get("commit"),
             "source_digest": pmc.get("source_digest")}
     if pmc.get("source_digest") != source_digest():
         prov["status"] = "stale: measured on other kernel sources"
-        return None, prov
+        return None, prov, None
     if pmc.get("gib") != args.gib or kernel not in pmc.get("kernels", {}):
         prov["status"] = "no entry for this workload/kernel"
-        return None, prov
+        return None, prov, None
     prov["status"] = "measured on this tree's kernels"
-    return pmc["kernels"][kernel]["hbm_bytes_per_launch"], prov
+    # every kernel of the measured batch launches once per batch: their sum is the batch's traffic
+    path_bytes = sum(v["hbm_bytes_per_launch"] for k, v in pmc["kernels"].items()
+                     if k not in ("k_table_clear", "k_b3_calib"))  # session setup / calibration, not the batch
+    return pmc["kernels"][kernel]["hbm_bytes_per_launch"], prov, round(path_bytes / (args.gib * (1 << 30)), 3)
 
 
 def parity_spot_check(workload, ctx, data, file_off, file_len, rank):

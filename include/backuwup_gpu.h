@@ -537,6 +537,10 @@ enum {
 int bw_profile_enable(bw_ctx* ctx, int on); /* also clears the accumulators */
 /* stage_ms[BW_N_STAGES] = summed milliseconds; *n_batches = batches accumulated.  Syncs. */
 int bw_profile_read(bw_ctx* ctx, double* stage_ms, uint64_t* n_batches);
+/* The profiled batches' intervals of one stage, out[2k] = start, out[2k+1] = end, in ms on the
+ * device's timeline (every context of a device shares its origin, so a caller can take the union
+ * of a stage over contexts).  *n = intervals; BW_ENOSPC if cap < *n.  Syncs. */
+int bw_profile_intervals(bw_ctx* ctx, int stage, double* out, uint64_t cap, uint64_t* n);
 
 /* ---- roofline calibration (diagnostic; replaces no reference call, touches no batch state) ----
  * The BLAKE3 leaf pass's compression run from registers (no memory traffic) on every CU at the

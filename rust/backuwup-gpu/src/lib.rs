@@ -269,6 +269,7 @@ pub mod ffi {
 
         pub fn bw_profile_enable(ctx: *mut bw_ctx, on: c_int) -> c_int;
         pub fn bw_profile_read(ctx: *mut bw_ctx, stage_ms: *mut f64, n_batches: *mut u64) -> c_int;
+        pub fn bw_profile_intervals(ctx: *mut bw_ctx, stage: c_int, out: *mut f64, cap: u64, n: *mut u64) -> c_int;
         pub fn bw_calibrate_b3(ctx: *mut bw_ctx, ms: f64, out: *mut f64) -> c_int;
     }
 }
