@@ -64,7 +64,7 @@ def build(force=False, verbose=False, debug=False, jobs=8, variant=None, defines
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wno-unused-value", "-Wno-unused-result"]
     flags += list(defines)
     if debug:
-        flags += ["-DBW_DEBUG", "-g"]
+        flags += ["-DBW_DEBUG", "-DBW_DIAG=1", "-g"]  # asserts + the diagnostic kernel variants
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(HERE, "..", "include", "backuwup_gpu.h"))
     newest_hdr = max(os.path.getmtime(h) for h in headers)

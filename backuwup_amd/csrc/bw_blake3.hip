@@ -744,19 +744,25 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
 #ifndef BW_B3_DYN_LDS
 #define BW_B3_DYN_LDS 0  // A/B: extra LDS per block caps the blocks per CU (occupancy experiments)
 #endif
+#if BW_DIAG
     const bool fused = loads == B3_LOADS_LINES && b.gdone;
     if (fused)
         hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
                            data, ctr, b, cv_buf, cv_tmp, digests);
-    else if (loads == B3_LOADS_LINES)
-        hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
-                           data, ctr, b, cv_buf, cv_tmp, digests);
     else if (loads == B3_LOADS_PAIRS)
         hipLaunchKernelGGL((k_b3_groups<false, 1, true>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), BW_B3_DYN_LDS, st,
                            data, ctr, b, cv_buf, digests);
-    else
+    else if (loads == B3_LOADS_PREFETCH)
         hipLaunchKernelGGL((k_b3_groups<true, 1, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
                            data, ctr, b, cv_buf, digests);
+    else
+#else
+    // the product library: aligned 128-byte lines, upper levels in their own launch
+    const bool fused = false;
+    (void)loads;
+#endif
+        hipLaunchKernelGGL((k_b3_lines<BW_B3_LINES_MINW, false>), dim3((unsigned)((max_groups + 255) / 256)), dim3(256), 0, st,
+                           data, ctr, b, cv_buf, cv_tmp, digests);
     if (leaf_done) hipEventRecord(leaf_done, st);
     if (mark) hipEventRecord(mark, st);
     if (between) hipEventRecord(between, st);

@@ -663,8 +663,29 @@ extern "C" int bw_set_stream(bw_ctx* c, void* s) {
 
 extern "C" void* bw_get_stream(bw_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+// Variants measured slower than the shipped path are compiled only into the
+// diagnostic build (BW_DIAG: libbackuwup_amd_debug.so); the product library accepts their
+// options at the shipped value only.
+static int diag_only(bw_ctx* c, int opt, uint64_t v, uint64_t shipped) {
+    if (BW_DIAG || v == shipped) return 1;  // go on to the option's own case
+    c->err = "option " + std::to_string(opt) + " = " + std::to_string(v) +
+             " selects a diagnostic variant: load the BW_DIAG build (libbackuwup_amd_debug.so)";
+    return BW_EINVAL;
+}
+
 extern "C" int bw_set_option(bw_ctx* c, int opt, uint64_t v) {
     if (!c) return BW_EINVAL;
+    int d = 1;
+    switch (opt) {
+        case BW_OPT_SPLIT: d = v == 2 ? diag_only(c, opt, v, 1) : 1; break;
+        case BW_OPT_ORDER_HASH: d = diag_only(c, opt, v, 0); break;
+        case BW_OPT_SCAN_WAVES: d = diag_only(c, opt, v, 16); break;
+        case BW_OPT_LATENCY_STREAM: d = diag_only(c, opt, v, 0); break;
+        case BW_OPT_B3_LOADS: d = diag_only(c, opt, v, B3_LOADS_LINES); break;
+        case BW_OPT_B3_UPPER: d = diag_only(c, opt, v, 0); break;
+        default: break;
+    }
+    if (d != 1) return d;
     switch (opt) {
         case BW_OPT_DEPTH:
             if (v < 1 || v > MAX_DEPTH) return BW_EINVAL;
@@ -1299,8 +1320,17 @@ static int ensure_helper(bw_ctx* c) {
     h->depth = c->depth;
     h->scan_small_bytes = c->scan_small_bytes;
     h->cand_cap_forced = c->cand_cap_forced;
+    // every per-context kernel and profiling option (the tail parts ran with defaults)
     h->b3_loads = c->b3_loads;
     h->scan_waves = c->scan_waves;
+    h->b3_group = c->b3_group;
+    h->b3_fused = c->b3_fused;
+    h->prof_mask = c->prof_mask;
+    h->scan_first = c->scan_first;
+    if (c->lat_split && bw_set_option(h, BW_OPT_LATENCY_STREAM, 1) != BW_OK) {
+        bw_destroy(h);
+        return BW_EHIP;
+    }
     if (int rc = bw_attach_index(h, c->idx)) {
         bw_destroy(h);
         return rc;

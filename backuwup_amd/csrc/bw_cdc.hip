@@ -292,13 +292,16 @@ bool launch_scan(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint64_t
     if (!big && !small) return false;  // a tile size no kernel was built for: the caller reports BW_EINVAL
     // 16-wave blocks hold 148 KiB of LDS (one per CU); 8-wave blocks hold 106 KiB and leave room
     // for two k_b3_groups blocks of another batch on the same CU
+#if BW_DIAG
     if (waves == 8) {
         if (big) launch_scan_t<512, SCAN_STRIP>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
         else launch_scan_t<512, SCAN_STRIP_SMALL>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
-    } else {
-        if (big) launch_scan_t<SCAN_BLOCK, SCAN_STRIP>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
-        else launch_scan_t<SCAN_BLOCK, SCAN_STRIP_SMALL>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
+        return true;
     }
+#endif
+    (void)waves;
+    if (big) launch_scan_t<SCAN_BLOCK, SCAN_STRIP>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
+    else launch_scan_t<SCAN_BLOCK, SCAN_STRIP_SMALL>(st, data, n_bytes, n_tiles, mk, tile_count, tile_slots, ovf, ctr);
     return true;
 }
 

@@ -9,6 +9,15 @@
 
 #include "../../include/backuwup_gpu.h"
 
+// BW_DIAG: compile the variants measured slower than the shipped path (the 8-wave scan, the
+// prefetch / block-pair leaf loaders, the upper levels fused into the leaf pass, the split batch,
+// serialized passes, the latency stream).  Only the diagnostic build defines it
+// (libbackuwup_amd_debug.so, with BW_DEBUG); the product library holds one scan kernel per tile
+// size, one leaf kernel and one upper-level kernel.
+#ifndef BW_DIAG
+#define BW_DIAG 0
+#endif
+
 namespace bw {
 
 // ------------------------------------------------------------------ tunables

@@ -154,15 +154,15 @@ def main():
                     help="also time the full chain on the last batch's unique blobs: level-3 zstd on the GPU, "
                          "the packfile grouping over the frame sizes, sealing + layout (§8f rows 2-4)")
     ap.add_argument("--b3-loads", type=int, default=None, choices=[0, 1, 2],
-                    help="BLAKE3 leaf loads (BW_OPT_B3_LOADS): 0 = one block ahead, 1 = block pairs, "
+                    help="[BW_DIAG build only: BW_LIB=backuwup_amd/libbackuwup_amd_debug.so] BLAKE3 leaf loads (BW_OPT_B3_LOADS): 0 = one block ahead, 1 = block pairs, "
                          "2 = aligned lines (k_b3_lines)")
-    ap.add_argument("--scan-waves", type=int, default=None, choices=[8, 16], help="BW_OPT_SCAN_WAVES")
-    ap.add_argument("--latency-stream", type=int, default=None, choices=[0, 1], help="BW_OPT_LATENCY_STREAM")
-    ap.add_argument("--order-hash", type=int, default=None, choices=[0, 1], help="BW_OPT_ORDER_HASH")
+    ap.add_argument("--scan-waves", type=int, default=None, choices=[8, 16], help="[BW_DIAG build only: BW_LIB=backuwup_amd/libbackuwup_amd_debug.so] BW_OPT_SCAN_WAVES")
+    ap.add_argument("--latency-stream", type=int, default=None, choices=[0, 1], help="[BW_DIAG build only: BW_LIB=backuwup_amd/libbackuwup_amd_debug.so] BW_OPT_LATENCY_STREAM")
+    ap.add_argument("--order-hash", type=int, default=None, choices=[0, 1], help="[BW_DIAG build only: BW_LIB=backuwup_amd/libbackuwup_amd_debug.so] BW_OPT_ORDER_HASH")
     ap.add_argument("--split", type=int, default=None, choices=[1, 2],
-                    help="BW_OPT_SPLIT: 2 = multi-file batches of 64 MiB-4 GiB as a head and a tail part on two streams")
+                    help="[BW_DIAG build only: BW_LIB=backuwup_amd/libbackuwup_amd_debug.so] BW_OPT_SPLIT: 2 = multi-file batches of 64 MiB-4 GiB as a head and a tail part on two streams")
     ap.add_argument("--b3-upper", type=int, default=None, choices=[0, 1],
-                    help="BW_OPT_B3_UPPER: 0 = upper levels in their own launch (default), 1 = inside the leaf pass")
+                    help="[BW_DIAG build only: BW_LIB=backuwup_amd/libbackuwup_amd_debug.so] BW_OPT_B3_UPPER: 0 = upper levels in their own launch (default), 1 = inside the leaf pass")
     ap.add_argument("--b3-group", type=int, default=None, choices=[1, 2, 4],
                     help="BW_OPT_B3_GROUP: BLAKE3 leaves per lane of the leaf pass")
     ap.add_argument("--scan-first", type=int, default=None, choices=[0, 1, 2], help="BW_OPT_SCAN_FIRST")

@@ -155,6 +155,10 @@ int bw_attach_index(bw_ctx* ctx, bw_index* index);
 
 /* ---- context options ---- */
 enum {
+    /* Options 5, 6, 7, 10, 11 (value 2) and 14 (value 1) select variants measured slower than the
+     * shipped kernels.  They are compiled only into the diagnostic build (BW_DIAG,
+     * libbackuwup_amd_debug.so); the product library accepts them at the shipped value only and
+     * returns BW_EINVAL otherwise. */
     BW_OPT_DEPTH = 1,            /* batches a context keeps addressable (result slots), 1..8; default 2 */
     BW_OPT_SCAN_SMALL_BYTES = 2, /* batches below this many bytes scan half-size tiles (default 4 GiB) */
     BW_OPT_CAND_CAP = 3,         /* test hook: fixed candidate array capacity (0 = sized per batch)  */

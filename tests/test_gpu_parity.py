@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from backuwup_amd import make_params
-from backuwup_amd._lib import BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE, BW_OPT_B3_GROUP, BW_OPT_B3_LOADS, BW_OPT_B3_UPPER, BwError
+from backuwup_amd._lib import BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE, BW_OPT_B3_GROUP, BwError
 from backuwup_amd.synth import splitmix_bytes
 
 pytestmark = pytest.mark.gpu
@@ -31,20 +31,15 @@ KAT = {
 }
 
 
-# every BLAKE3 test runs with each leaf-pass loader: 0 = one block ahead, 1 = 132-byte block pairs
-# (k_b3_groups), 2 = aligned 128-byte lines through registers (k_b3_lines, the default) with the
-# upper levels as a launch of their own (the default) or inside the leaf pass (BW_OPT_B3_UPPER 1)
-# and 4, 2 or 1 leaves per lane (BW_OPT_B3_GROUP)
-@pytest.fixture(params=[(0, 0, 4), (1, 0, 4), (2, 0, 0), (2, 0, 4), (2, 1, 4), (2, 0, 2), (2, 0, 1), (2, 1, 1)],
-                ids=["prefetch", "pairs", "lines", "lines-g4", "lines-fused", "lines-g2", "lines-g1", "lines-fused-g1"])
+# every BLAKE3 test runs with each shipped leaf-pass grouping: the leaf kernel k_b3_lines (aligned
+# 128-byte lines through registers) with 4, 2 or 1 leaves per lane (BW_OPT_B3_GROUP; 0 = the
+# automatic choice).  The loaders and the fused upper levels measured slower live in the diagnostic
+# build only (BW_DIAG, tools/debug_check.py).
+@pytest.fixture(params=[0, 4, 2, 1], ids=["lines", "lines-g4", "lines-g2", "lines-g1"])
 def b3ctx(ctx, request):
-    ctx.set_option(BW_OPT_B3_LOADS, request.param[0])
-    ctx.set_option(BW_OPT_B3_UPPER, request.param[1])
-    ctx.set_option(BW_OPT_B3_GROUP, request.param[2])
+    ctx.set_option(BW_OPT_B3_GROUP, request.param)
     yield ctx
-    ctx.set_option(BW_OPT_B3_LOADS, 2)  # the context defaults
-    ctx.set_option(BW_OPT_B3_UPPER, 0)
-    ctx.set_option(BW_OPT_B3_GROUP, 0)
+    ctx.set_option(BW_OPT_B3_GROUP, 0)  # the context default
 
 
 def test_blake3_kat(b3ctx):

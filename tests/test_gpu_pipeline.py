@@ -71,12 +71,18 @@ def test_tickets_ring(oracle):
             c.wait(tickets[3] + 1)
 
 
+def _diag_lib():
+    """True when the loaded library is the diagnostic build (BW_DIAG variants compiled in)."""
+    from backuwup_amd import _lib
+    return _lib.LIB_PATH.endswith("_debug.so")
+
+
 def test_split_batches_match_unsplit(oracle):
-    """BW_OPT_SPLIT: multi-file batches of 64 MiB - 4 GiB run as a head (this context) and a tail
-    (a helper context) with their scans and BLAKE3 passes in order.  Four batches of a tree corpus
-    over two contexts sharing an index, with the split on and off: the blobs (file indices in the
-    batch's numbering), digests and verdicts equal the oracle either way, also from pinned host
-    memory, with depth 3 rings; a split batch has no single device view."""
+    """Four batches of a tree corpus over two contexts sharing an index, depth 3 rings: the blobs
+    (file indices in the batch's numbering), digests and verdicts equal the oracle, also from pinned
+    host memory.  With the diagnostic build (BW_LIB = the BW_DIAG library) also with BW_OPT_SPLIT 2:
+    multi-file batches of 64 MiB - 4 GiB as a head and a tail part (helper context), whose batches
+    have no single device view; the product library refuses that variant (measured slower)."""
     import torch
     from backuwup_amd._lib import BW_OPT_SPLIT
     data, offs, lens = tree_corpus(320 << 20, seed=91, max_file=40 << 20)
@@ -89,7 +95,10 @@ def test_split_batches_match_unsplit(oracle):
     want = oracle_session(oracle, batches)
     devs = [torch.from_numpy(d).cuda() for d, _, _ in batches]
     torch.cuda.synchronize()
-    for split in (2, 1):
+    if not _diag_lib():
+        with Context(0) as c, pytest.raises(BwError):
+            c.set_option(BW_OPT_SPLIT, 2)
+    for split in ((2, 1) if _diag_lib() else (1,)):
         ix = Index(0)
         cs = [Context(0), Context(0)]
         try:
@@ -113,7 +122,7 @@ def test_split_batches_match_unsplit(oracle):
             for c in cs:
                 c.close()
             ix.close()
-    # the same batches from pinned host memory on one context (split on by default)
+    # the same batches from pinned host memory on one context
     pinned = []
     for d, _, _ in batches:
         t = torch.empty(d.size, dtype=torch.uint8, pin_memory=True)
@@ -158,13 +167,16 @@ def test_sync_helpers_leave_held_tickets_alone(oracle):
         blobs_equal(c.results(), want[1])
 
 
-@pytest.mark.parametrize("nctx,order", [(2, 0), (3, 1)])
+@pytest.mark.parametrize("nctx,order", [(2, 0), (3, 0), (3, 1)])
 def test_shared_index_two_contexts_six_batches(oracle, nctx, order):
     """One session, two (three) contexts on their own streams, one index: six batches of C1 (tree
     corpus) and C4 (small files) data with duplicates across batches and contexts, submitted back
     to back (one batch per context in flight); verdicts equal the oracle over the concatenated
-    batches.  order = BW_OPT_ORDER_HASH (scans and leaf passes serialized across the contexts)."""
+    batches.  order = BW_OPT_ORDER_HASH (scans and leaf passes serialized across the contexts; the
+    diagnostic build only)."""
     from backuwup_amd._lib import BW_OPT_ORDER_HASH
+    if order and not _diag_lib():
+        pytest.skip("BW_OPT_ORDER_HASH is a diagnostic variant (BW_DIAG build)")
     import torch
     t_data, t_offs, t_lens = tree_corpus(48 << 20, seed=77, max_file=6 << 20)
     s_data, s_offs, s_lens = small_files(3000, seed=78)
@@ -732,13 +744,19 @@ def test_rccl_init_deadline_when_a_rank_never_joins():
     assert int(rc) == BW_ECOMM and 3.5 < float(dt) < 30, line
 
 
-@pytest.mark.parametrize("scan_waves,latency,loads,upper,group",
-                         [(8, 0, 1, 0, 4), (16, 1, 1, 0, 4), (8, 1, 0, 0, 4), (16, 0, 0, 0, 4), (16, 0, 2, 1, 4),
-                          (8, 1, 2, 1, 2), (16, 0, 2, 0, 4), (16, 0, 2, 0, 2), (8, 0, 2, 0, 1)])
+# the shipped kernels: one scan per tile size, k_b3_lines with 4 / 2 / 1 leaves per lane.  The
+# diagnostic variants (8-wave scan blocks, the latency stream, the other leaf loaders, the fused
+# upper levels) run only with the BW_DIAG library (BW_LIB=...libbackuwup_amd_debug.so).
+_VARIANTS = [(16, 0, 2, 0, 4), (16, 0, 2, 0, 2), (16, 0, 2, 0, 1)]
+_DIAG_VARIANTS = [(8, 0, 1, 0, 4), (16, 1, 1, 0, 4), (8, 1, 0, 0, 4), (16, 0, 0, 0, 4), (16, 0, 2, 1, 4),
+                  (8, 1, 2, 1, 2), (8, 0, 2, 0, 1)]
+
+
+@pytest.mark.parametrize("scan_waves,latency,loads,upper,group", _VARIANTS + (_DIAG_VARIANTS if _diag_lib() else []))
 def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads, upper, group):
-    """The scheduling variants (8-wave scan blocks, the high-priority latency stream, both BLAKE3
-    load modes) change only where and when kernels run: results equal the oracle, including two
-    batches in flight on two contexts that share an index."""
+    """Two batches in flight on two contexts that share an index, four batches of a tree corpus,
+    for each leaf grouping (and, with the diagnostic build, each scheduling variant): results equal
+    the oracle."""
     import torch
     from backuwup_amd._lib import BW_OPT_B3_GROUP, BW_OPT_B3_LOADS, BW_OPT_B3_UPPER, BW_OPT_LATENCY_STREAM, BW_OPT_SCAN_WAVES
     data, offs, lens = tree_corpus(80 << 20, seed=21, max_file=20 << 20)
@@ -752,10 +770,11 @@ def test_kernel_variants_bit_exact(oracle, scan_waves, latency, loads, upper, gr
         for c in cs:
             c.set_stream(torch.cuda.Stream().cuda_stream)
             c.attach_index(ix)
-            c.set_option(BW_OPT_SCAN_WAVES, scan_waves)
-            c.set_option(BW_OPT_LATENCY_STREAM, latency)
-            c.set_option(BW_OPT_B3_LOADS, loads)
-            c.set_option(BW_OPT_B3_UPPER, upper)
+            if (scan_waves, latency, loads, upper) != (16, 0, 2, 0):
+                c.set_option(BW_OPT_SCAN_WAVES, scan_waves)
+                c.set_option(BW_OPT_LATENCY_STREAM, latency)
+                c.set_option(BW_OPT_B3_LOADS, loads)
+                c.set_option(BW_OPT_B3_UPPER, upper)
             c.set_option(BW_OPT_B3_GROUP, group)
         cs[0].index_reset()
         tickets = [cs[k % 2].submit_device(t.data_ptr(), d.size, o, l) for k, (t, (d, o, l)) in enumerate(zip(devs, batches))]

@@ -69,6 +69,18 @@ def main():
         assert same(c.process_files(data, offs, lens, make_params(*SMALL)),
                     oracle.process_files(data, offs, lens, *SMALL))
         checks += 3
+        # round 4: the variants pruned from the product library (BW_DIAG) stay parity-checked here
+        from backuwup_amd._lib import (BW_OPT_B3_LOADS, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH, BW_OPT_SCAN_WAVES,
+                                       BW_OPT_SPLIT)
+        data, offs, lens = tree_corpus(96 << 20, seed=9, max_file=20 << 20)
+        want = oracle.process_files(data, offs, lens, threads=8)
+        for opt, v in ((BW_OPT_B3_LOADS, 0), (BW_OPT_B3_LOADS, 1), (BW_OPT_SCAN_WAVES, 8), (BW_OPT_LATENCY_STREAM, 1),
+                       (BW_OPT_ORDER_HASH, 1), (BW_OPT_SPLIT, 2)):
+            with Context(0) as v_ctx:
+                v_ctx.set_option(opt, v)
+                v_ctx.index_reset()
+                assert same(v_ctx.process_files(data, offs, lens), want), (opt, v)
+                checks += 1
     print("BW_DEBUG build: %d parity checks passed, no device assert fired" % checks)
 
 
