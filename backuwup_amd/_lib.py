@@ -158,6 +158,10 @@ SIGNATURES = [
     ("bw_index_load_files", ctypes.c_int, [vp, vp, vp, ctypes.POINTER(BwIndexFile), ctypes.c_uint64, vp,
                                            ctypes.c_uint64, u64p, u64p]),
     ("bw_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
+    ("bw_fastcdc_chunks_hashed", ctypes.c_int, [vp, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_uint32, vp, ctypes.c_uint64, u64p, u64p]),
+    ("bw_fastcdc_release", None, [ctypes.c_uint64]),
+    ("bw_blake3_kept_hits", ctypes.c_uint64, []),
     ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
     ("bw_profile_intervals", ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, u64p]),
     ("bw_calibrate_b3", ctypes.c_int, [vp, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),

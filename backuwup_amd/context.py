@@ -157,6 +157,30 @@ class Context:
                                         ctypes.byref(n)), self.h)
         return [(out[i].hash, out[i].offset, out[i].length) for i in range(n.value)]
 
+    def fastcdc_chunks_hashed(self, buf, min_size, avg_size, max_size):
+        """bw_fastcdc_chunks_hashed over a contiguous uint8 numpy array (kept alive by the caller until
+        release): ([(hash, offset, length)], handle).  blake3_at(buf, offset, length) of one of these
+        chunks then returns the kept digest; fastcdc_release(handle) drops them."""
+        assert isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags.c_contiguous
+        cap = buf.size // max(min(2 * (min_size // 2), max_size), 1) + 2
+        out = (_lib.BwChunk * cap)()
+        n, h = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._L.bw_fastcdc_chunks_hashed(self.h, _ptr(buf), buf.size, min_size, avg_size, max_size, out, cap,
+                                               ctypes.byref(n), ctypes.byref(h)), self.h)
+        return [(out[i].hash, out[i].offset, out[i].length) for i in range(n.value)], h.value
+
+    def fastcdc_release(self, handle):
+        self._L.bw_fastcdc_release(handle)
+
+    def blake3_at(self, buf, offset, length):
+        """blake3::hash(&buf[offset..offset+length]) on the caller's own memory (no copy), as the
+        reference hashes each chunk slice of its mmap (dir_packer.rs:262-265, :286)."""
+        assert isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and offset + length <= buf.size
+        out = (ctypes.c_uint8 * 32)()
+        p = ctypes.cast(buf.ctypes.data + offset, _lib.u8p)
+        check(self._L.bw_blake3_hash(self.h, p, length, out), self.h)
+        return bytes(out)
+
     def blake3_many(self, data, offsets, lengths):
         buf = _as_u8(data)
         off = np.ascontiguousarray(offsets, dtype=np.uint64)

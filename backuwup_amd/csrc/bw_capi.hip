@@ -1682,7 +1682,92 @@ int bw::hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const ui
     return dedup ? check_collision(c) : BW_OK;
 }
 
+// ---- kept chunk digests (bw_fastcdc_chunks_hashed): the reference chunks a file and then hashes
+// each chunk slice of it (dir_packer.rs:254-266, :286); the chunking submit hashes them at once and
+// the per-chunk blake3::hash calls find their digest here by (pointer, length).
+namespace {
+struct Kept {
+    const uint8_t* base;
+    uint64_t len;
+    std::vector<uint64_t> off, clen;  // chunk offsets (ascending) and lengths
+    std::vector<uint8_t> dig;         // 32 B per chunk
+};
+std::mutex g_kept_mu;
+std::unordered_map<uint64_t, Kept> g_kept;         // handle -> file
+std::atomic<uint64_t> g_kept_next{1}, g_kept_hits{0};
+
+bool kept_lookup(const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    std::lock_guard<std::mutex> lk(g_kept_mu);
+    for (auto& kv : g_kept) {  // a handful of files are open at once (one per task)
+        const Kept& k = kv.second;
+        if (data < k.base || data >= k.base + k.len) continue;
+        const uint64_t o = (uint64_t)(data - k.base);
+        auto it = std::lower_bound(k.off.begin(), k.off.end(), o);
+        if (it == k.off.end() || *it != o) continue;
+        const size_t i = it - k.off.begin();
+        if (k.clen[i] != len) continue;
+        memcpy(out, k.dig.data() + 32 * i, 32);
+        g_kept_hits++;
+        return true;
+    }
+    return false;
+}
+}  // namespace
+
+extern "C" int bw_fastcdc_chunks_hashed(bw_ctx* c, const uint8_t* src, uint64_t len, uint32_t mn, uint32_t av,
+                                        uint32_t mx, bw_chunk* out, uint64_t cap, uint64_t* n_out, uint64_t* handle) {
+    if (!c || !n_out || !handle || (len && !src)) return BW_EINVAL;
+    *handle = 0;
+    Masks mk;
+    if (int rc = make_masks(mn, av, mx, &mk)) return rc;
+    *n_out = 0;
+    if (len == 0) return BW_OK;
+    bw_params p;
+    p.min_size = mn;
+    p.avg_size = av;
+    p.max_size = mx;
+    p.flags = BW_F_NO_DEDUP;  // chunk + hash; the gate stays the caller's (add_blob)
+    p.small_file_threshold = 0;
+    const uint64_t off = 0;
+    std::vector<bw_blob> tmp(len / std::min<uint64_t>(mk.s0, mk.max) + 2);
+    uint64_t n = 0;
+    if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
+    *n_out = n;
+    if (n > cap) return BW_ENOSPC;
+    Kept k;
+    k.base = src;
+    k.len = len;
+    k.off.resize(n);
+    k.clen.resize(n);
+    k.dig.resize(32 * n);
+    for (uint64_t i = 0; i < n; i++) {
+        out[i].hash = tmp[i].gear_hash;
+        out[i].offset = tmp[i].offset;
+        out[i].length = tmp[i].length;
+        k.off[i] = tmp[i].offset;
+        k.clen[i] = tmp[i].length;
+        memcpy(k.dig.data() + 32 * i, tmp[i].digest, 32);
+    }
+    const uint64_t h = g_kept_next++;
+    {
+        std::lock_guard<std::mutex> lk(g_kept_mu);
+        g_kept.emplace(h, std::move(k));
+    }
+    *handle = h;
+    return BW_OK;
+}
+
+extern "C" void bw_fastcdc_release(uint64_t handle) {
+    if (!handle) return;
+    std::lock_guard<std::mutex> lk(g_kept_mu);
+    g_kept.erase(handle);
+}
+
+extern "C" uint64_t bw_blake3_kept_hits(void) { return g_kept_hits.load(); }
+
 extern "C" int bw_blake3_hash(bw_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    if (!c || !out || (len && !data)) return BW_EINVAL;
+    if (len && kept_lookup(data, len, out)) return BW_OK;
     const uint64_t off = 0;
     static const uint8_t empty[16] = {0};
     return bw_blake3_hash_many(c, len ? data : empty, len, &off, &len, 1, out);

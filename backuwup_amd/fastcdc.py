@@ -3,13 +3,17 @@
     let chunker = FastCDC::new(&mmap, min, avg, max);      // dir_packer.rs:254-259
     for chunk in chunker { &mmap[chunk.offset..chunk.offset + chunk.length] }   // :261-266
 
-Here `FastCDC(source, min_size, avg_size, max_size)` chunks the whole source on the GPU when
-it is constructed and iterates `Chunk(hash, offset, length)` like the crate's iterator.  Size
-parameters outside the crate's asserted ranges raise ValueError (the crate panics).
+Here `FastCDC(source, min_size, avg_size, max_size)` chunks AND hashes the whole source on the GPU
+in one submit when it is constructed (bw_fastcdc_chunks_hashed) and iterates `Chunk(hash, offset,
+length)` like the crate's iterator.  While the object lives, `blake3.hash(view[offset:offset +
+length])` of one of its chunks (a zero-copy view of the same memory, as the reference slices its
+mmap) is answered from the kept digests instead of a second trip to the GPU.  Size parameters
+outside the crate's asserted ranges raise ValueError (the crate panics).
 """
 from collections import namedtuple
 
 from ._lib import BW_EINVAL, BwError
+from .blake3 import _as_bytes_view
 from .context import default_context
 
 MINIMUM_MIN = 64
@@ -33,13 +37,25 @@ class FastCDC:
             raise ChunkParameterError("fastcdc size parameters out of range: %d/%d/%d"
                                       % (min_size, avg_size, max_size))
         ctx = ctx or default_context()
+        self._kept, self._ctx = 0, ctx
         try:
-            self._chunks = [Chunk(*c) for c in ctx.fastcdc_chunks(source, min_size, avg_size, max_size)]
+            buf = _as_bytes_view(source)
+            if buf.size and buf.flags.c_contiguous:
+                cuts, self._kept = ctx.fastcdc_chunks_hashed(buf, min_size, avg_size, max_size)
+                self._buf = buf  # the kept digests name this memory: keep it alive with them
+            else:
+                cuts = ctx.fastcdc_chunks(source, min_size, avg_size, max_size)
+            self._chunks = [Chunk(*c) for c in cuts]
         except BwError as e:
             if e.rc == BW_EINVAL:
                 raise ChunkParameterError(str(e)) from e
             raise
         self.min_size, self.avg_size, self.max_size = min_size, avg_size, max_size
+
+    def __del__(self):  # the crate's FastCDC borrows the source; its digests go with the object
+        kept, self._kept = getattr(self, "_kept", 0), 0
+        if kept:
+            self._ctx.fastcdc_release(kept)
 
     def __iter__(self):
         return iter(self._chunks)

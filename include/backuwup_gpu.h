@@ -114,6 +114,20 @@ int bw_fastcdc_chunks(bw_ctx* ctx, const uint8_t* src, uint64_t len, uint32_t mi
                       uint32_t avg_size, uint32_t max_size, bw_chunk* out, uint64_t cap,
                       uint64_t* n_out);
 
+/* The reference's per-file call pattern (dir_packer.rs:254-266 then :286 per chunk) without a second
+ * trip per chunk: FastCDC::new(src, min, avg, max).collect() as bw_fastcdc_chunks, with every
+ * chunk's BLAKE3 digest computed in the same submit and kept under *handle until
+ * bw_fastcdc_release(handle).  Until then bw_blake3_hash of exactly one of these chunks (pointer
+ * src + offset, that length; any context, any thread) returns the kept digest without touching
+ * the GPU.  The caller keeps src unchanged until the release: the Rust drop-in's FastCDC borrows
+ * the mmap for its lifetime and releases in Drop (rust/backuwup-gpu). */
+int bw_fastcdc_chunks_hashed(bw_ctx* ctx, const uint8_t* src, uint64_t len, uint32_t min_size,
+                             uint32_t avg_size, uint32_t max_size, bw_chunk* out, uint64_t cap,
+                             uint64_t* n_out, uint64_t* handle);
+void bw_fastcdc_release(uint64_t handle);
+/* digests answered from kept chunk digests since the process started (diagnostic) */
+uint64_t bw_blake3_kept_hits(void);
+
 /* blake3::hash(data) -> 32 bytes, host buffer. */
 int bw_blake3_hash(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
 /* n independent messages data[offsets[i] .. offsets[i]+lengths[i]) -> out[32*i..] */

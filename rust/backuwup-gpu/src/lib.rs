@@ -155,6 +155,11 @@ pub mod ffi {
 
         pub fn bw_fastcdc_chunks(ctx: *mut bw_ctx, src: *const u8, len: u64, min_size: u32, avg_size: u32,
                                  max_size: u32, out: *mut bw_chunk, cap: u64, n_out: *mut u64) -> c_int;
+        pub fn bw_fastcdc_chunks_hashed(ctx: *mut bw_ctx, src: *const u8, len: u64, min_size: u32, avg_size: u32,
+                                        max_size: u32, out: *mut bw_chunk, cap: u64, n_out: *mut u64,
+                                        handle: *mut u64) -> c_int;
+        pub fn bw_fastcdc_release(handle: u64);
+        pub fn bw_blake3_kept_hits() -> u64;
         pub fn bw_blake3_hash(ctx: *mut bw_ctx, data: *const u8, len: u64, out: *mut u8) -> c_int;
         pub fn bw_blake3_hash_many(ctx: *mut bw_ctx, data: *const u8, data_len: u64, offsets: *const u64,
                                    lengths: *const u64, n: u64, out: *mut u8) -> c_int;
@@ -343,6 +348,21 @@ impl Context {
         })?;
         out.truncate(n as usize);
         Ok(out)
+    }
+
+    /// As `fastcdc_chunks`, with every chunk's digest kept under the returned handle for
+    /// `blake3_hash` of the chunk slices (release with `ffi::bw_fastcdc_release`).
+    pub fn fastcdc_chunks_hashed(&mut self, src: &[u8], min_size: u32, avg_size: u32, max_size: u32)
+                                 -> Result<(Vec<ffi::bw_chunk>, u64)> {
+        let shortest = std::cmp::max(std::cmp::min(2 * (min_size / 2), max_size), 1) as usize;
+        let mut out = vec![ffi::bw_chunk::default(); src.len() / shortest + 2];
+        let (mut n, mut kept) = (0u64, 0u64);
+        self.check(unsafe {
+            ffi::bw_fastcdc_chunks_hashed(self.raw, src.as_ptr(), src.len() as u64, min_size, avg_size, max_size,
+                                          out.as_mut_ptr(), out.len() as u64, &mut n, &mut kept)
+        })?;
+        out.truncate(n as usize);
+        Ok((out, kept))
     }
 
     /// `blake3::hash(data).into()`
@@ -582,11 +602,22 @@ pub mod fastcdc {
             pub length: usize,
         }
 
-        /// `fastcdc::v2020::FastCDC`: the whole source is chunked on the GPU at construction and
-        /// the iterator replays the cuts (identical boundaries and `Chunk.hash`).
+        /// `fastcdc::v2020::FastCDC`: the whole source is chunked AND every chunk hashed on the GPU
+        /// in one submit at construction (`bw_fastcdc_chunks_hashed`); the iterator replays the cuts
+        /// (identical boundaries and `Chunk.hash`), and `blake3::hash(&source[off..off + len])` of a
+        /// chunk (dir_packer.rs:262-265 -> :286) is answered from the kept digests with no second
+        /// trip to the GPU.  The borrow of `source` guarantees the bytes stay put until `Drop`
+        /// releases the digests.
         pub struct FastCDC<'a> {
             source: &'a [u8],
             chunks: std::vec::IntoIter<Chunk>,
+            kept: u64,
+        }
+
+        impl Drop for FastCDC<'_> {
+            fn drop(&mut self) {
+                unsafe { crate::ffi::bw_fastcdc_release(self.kept) }
+            }
         }
 
         impl<'a> FastCDC<'a> {
@@ -595,13 +626,15 @@ pub mod fastcdc {
                 assert!((MINIMUM_MIN..=MINIMUM_MAX).contains(&min_size));
                 assert!((AVERAGE_MIN..=AVERAGE_MAX).contains(&avg_size));
                 assert!((MAXIMUM_MIN..=MAXIMUM_MAX).contains(&max_size));
-                let cuts = super::super::with_default(|c| c.fastcdc_chunks(source, min_size, avg_size, max_size))
-                    .expect("GPU chunking failed");
+                let (cuts, kept) = super::super::with_default(|c| {
+                    c.fastcdc_chunks_hashed(source, min_size, avg_size, max_size)
+                })
+                .expect("GPU chunking failed");
                 let chunks: Vec<Chunk> = cuts
                     .iter()
                     .map(|c| Chunk { hash: c.hash, offset: c.offset as usize, length: c.length as usize })
                     .collect();
-                FastCDC { source, chunks: chunks.into_iter() }
+                FastCDC { source, chunks: chunks.into_iter(), kept }
             }
 
             pub fn source(&self) -> &'a [u8] {

@@ -414,3 +414,43 @@ def _exchange_world1(ctx, torch, DeviceShardOps, exchange_dedup, small_files):
     ctx.set_stream(0)  # back to the context's own stream
     assert np.array_equal(host, want["is_dup"])
     assert host.sum() > 0
+
+
+# ------------------------------------------------------------------ the reference's per-file call pattern
+
+def test_dropin_call_sites_kept_digests(ctx, oracle):
+    """dir_packer.rs:254-266 chunks a file, then :286 hashes each chunk slice of it.
+    bw_fastcdc_chunks_hashed chunks and hashes in one submit; bw_blake3_hash of exactly one of its
+    chunk slices returns the kept digest (counted by bw_blake3_kept_hits), anything else is hashed
+    on the GPU, and after the release nothing is answered from them.  Every digest equals the
+    oracle's, and so do the Python drop-ins (fastcdc.FastCDC + blake3.hash on memoryview slices)."""
+    from backuwup_amd import _lib
+    from backuwup_amd import blake3 as b3
+    from backuwup_amd import fastcdc as fc
+    L = _lib.load()
+    data = splitmix_bytes(77, (20 << 20) + 333)
+    want = oracle.fastcdc(data, *BK)
+    chunks, h = ctx.fastcdc_chunks_hashed(data, *BK)
+    assert chunks == want and h != 0
+    hits0 = L.bw_blake3_kept_hits()
+    for _, off, ln in chunks:
+        assert ctx.blake3_at(data, off, ln) == oracle.blake3(data[off:off + ln])
+    assert L.bw_blake3_kept_hits() - hits0 == len(chunks)
+    # not a chunk of it: hashed on the GPU (same pointer, other length; other pointer, same length)
+    n0 = chunks[0][2]
+    assert ctx.blake3_at(data, 0, n0 - 1) == oracle.blake3(data[:n0 - 1])
+    assert ctx.blake3_at(data, 1, n0) == oracle.blake3(data[1:n0 + 1])
+    assert L.bw_blake3_kept_hits() - hits0 == len(chunks)
+    ctx.fastcdc_release(h)
+    assert ctx.blake3_at(data, 0, n0) == oracle.blake3(data[:n0])
+    assert L.bw_blake3_kept_hits() - hits0 == len(chunks)
+    # the Python drop-ins, written exactly like the reference's loop
+    mv = memoryview(data)
+    hits1 = L.bw_blake3_kept_hits()
+    chunker = fc.FastCDC(mv, *BK, ctx=ctx)
+    got = [b3.hash(mv[c.offset:c.offset + c.length], ctx=ctx) for c in chunker]
+    assert got == [oracle.blake3(data[o:o + n]) for _, o, n in want]
+    assert L.bw_blake3_kept_hits() - hits1 == len(want)
+    del chunker
+    # empty source: no chunks, nothing kept
+    assert ctx.fastcdc_chunks_hashed(np.zeros(0, np.uint8), *BK) == ([], 0)

@@ -1,0 +1,155 @@
+// tools/dropin_c1.cpp -- the reference's unchanged call sites, driven from C++ through the C ABI the
+// Rust drop-ins bind.  Per file, exactly as dir_packer.rs:246-286 does:
+//   len > 1 MiB: FastCDC::new(&mmap, 256 KiB, 1 MiB, 3 MiB), then blake3::hash(&mmap[off..off+len])
+//                per chunk;   len <= 1 MiB: blake3::hash(whole file)
+// on T threads (one tokio task per file; one context per thread, the shim's thread-local default),
+// over C1's files in pageable host memory (the mmap'd page cache of the reference).
+//   sync  bw_fastcdc_chunks + bw_blake3_hash per chunk: every chunk crosses PCIe twice, one
+//         synchronous GPU round trip per call
+//   kept  bw_fastcdc_chunks_hashed (chunks and hashes the file in one submit) + bw_blake3_hash per
+//         chunk answered from the kept digests + bw_fastcdc_release: what the Rust FastCDC drop-in
+//         does behind the same signatures
+// Prints GB/s of file bytes per mode (best of reps) and checks that both modes give the same
+// chunks and digests (the GPU results are checked against the oracle in tests/test_gpu_parity.py).
+//
+// Build (CPU, after the library):
+//   hipcc -O2 -std=c++17 -I include tools/dropin_c1.cpp -L backuwup_amd -lbackuwup_amd \
+//     -Wl,-rpath,$PWD/backuwup_amd -lpthread -o build_ab/dropin_c1
+// Run: build_ab/dropin_c1 <corpus.bin> [threads=16] [reps=3]
+//   corpus.bin = u64 n, n offsets, n lengths, then the bytes (tools/gpu_dropin.sh writes bench.py's C1)
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "backuwup_gpu.h"
+
+struct Corpus {
+    std::vector<uint64_t> off, len;
+    std::vector<uint8_t> data;
+};
+
+struct FileOut {
+    std::vector<bw_chunk> chunks;
+    std::vector<uint8_t> dig;
+};
+
+static bool load(const char* path, Corpus& c) {
+    FILE* f = fopen(path, "rb");
+    uint64_t n = 0;
+    if (!f || fread(&n, 8, 1, f) != 1) return false;
+    c.off.resize(n);
+    c.len.resize(n);
+    if (fread(c.off.data(), 8, n, f) != n || fread(c.len.data(), 8, n, f) != n) return false;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) total = std::max(total, c.off[i] + c.len[i]);
+    c.data.resize(total);
+    const bool ok = fread(c.data.data(), 1, total, f) == total;
+    fclose(f);
+    return ok;
+}
+
+static const uint64_t SMALL = 1 << 20;  // dir_packer.rs:246
+
+static int process(bw_ctx* ctx, const uint8_t* p, uint64_t n, bool kept, FileOut& o, std::string& err) {
+    o.chunks.clear();
+    o.dig.clear();
+    uint8_t d[32];
+    if (n <= SMALL) {  // fs::read + add_file_blob
+        if (int rc = bw_blake3_hash(ctx, p, n, d)) return err = bw_last_error(ctx), rc;
+        o.chunks.push_back({0, 0, n});
+        o.dig.insert(o.dig.end(), d, d + 32);
+        return 0;
+    }
+    std::vector<bw_chunk> ch(n / (256 << 10) + 2);
+    uint64_t nc = 0, handle = 0;
+    int rc = kept ? bw_fastcdc_chunks_hashed(ctx, p, n, 256 << 10, 1 << 20, 3 << 20, ch.data(), ch.size(), &nc, &handle)
+                  : bw_fastcdc_chunks(ctx, p, n, 256 << 10, 1 << 20, 3 << 20, ch.data(), ch.size(), &nc);
+    if (rc) return err = bw_last_error(ctx), rc;
+    ch.resize(nc);
+    for (const bw_chunk& c : ch) {  // for chunk in chunker { add_file_blob(&mmap[off..off+len]) }
+        if ((rc = bw_blake3_hash(ctx, p + c.offset, c.length, d))) break;
+        o.dig.insert(o.dig.end(), d, d + 32);
+    }
+    bw_fastcdc_release(handle);
+    if (rc) return err = bw_last_error(ctx), rc;
+    o.chunks = std::move(ch);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s corpus.bin [threads] [reps]\n", argv[0]);
+        return 2;
+    }
+    Corpus c;
+    if (!load(argv[1], c)) {
+        fprintf(stderr, "cannot read %s\n", argv[1]);
+        return 2;
+    }
+    const int T = argc > 2 ? atoi(argv[2]) : 16, reps = argc > 3 ? atoi(argv[3]) : 3;
+    const uint64_t nf = c.off.size();
+    uint64_t bytes = 0, big = 0;
+    for (uint64_t i = 0; i < nf; i++) {
+        bytes += c.len[i];
+        big += c.len[i] > SMALL;
+    }
+    printf("corpus: %llu files (%llu > 1 MiB), %.3f GB; %d threads, one context each\n", (unsigned long long)nf,
+           (unsigned long long)big, bytes / 1e9, T);
+    std::vector<bw_ctx*> ctxs(T);
+    for (int t = 0; t < T; t++)
+        if (bw_create(0, &ctxs[t])) return 3;
+    std::vector<FileOut> ref(nf), got(nf);
+    int rc_all = 0;
+    for (int mode = 0; mode < 2; mode++) {
+        const bool kept = mode == 1;
+        std::vector<FileOut>& out = kept ? got : ref;
+        double best = 1e30;
+        const uint64_t hits0 = bw_blake3_kept_hits();
+        for (int r = 0; r < reps + 1; r++) {  // the first pass warms the contexts' buffers
+            std::atomic<uint64_t> next{0};
+            std::atomic<int> fail{0};
+            std::string errs[64];
+            auto t0 = std::chrono::steady_clock::now();
+            std::vector<std::thread> th;
+            for (int t = 0; t < T; t++)
+                th.emplace_back([&, t] {
+                    for (uint64_t i; (i = next++) < nf && !fail;) {
+                        if (int rc = process(ctxs[t], c.data.data() + c.off[i], c.len[i], kept, out[i], errs[t % 64]))
+                            fail = rc;
+                    }
+                });
+            for (auto& x : th) x.join();
+            const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (fail) {
+                for (auto& e : errs)
+                    if (!e.empty()) fprintf(stderr, "error: %s\n", e.c_str());
+                return 4;
+            }
+            if (r) best = std::min(best, s);
+        }
+        uint64_t nchunks = 0;
+        for (auto& o : out) nchunks += o.chunks.size();
+        printf("%-4s %8.2f GB/s (%.2f ms per pass, best of %d; %llu blobs; kept-digest answers %llu)\n",
+               kept ? "kept" : "sync", bytes / best / 1e9, best * 1e3, reps, (unsigned long long)nchunks,
+               (unsigned long long)(bw_blake3_kept_hits() - hits0));
+        fflush(stdout);
+    }
+    for (uint64_t i = 0; i < nf; i++) {
+        bool same = ref[i].chunks.size() == got[i].chunks.size() && ref[i].dig == got[i].dig;
+        for (size_t k = 0; same && k < ref[i].chunks.size(); k++)
+            same = ref[i].chunks[k].offset == got[i].chunks[k].offset && ref[i].chunks[k].length == got[i].chunks[k].length &&
+                   ref[i].chunks[k].hash == got[i].chunks[k].hash;
+        if (!same) {
+            fprintf(stderr, "file %llu: sync and kept results differ\n", (unsigned long long)i);
+            rc_all = 5;
+        }
+    }
+    printf("sync == kept on every file: %s\n", rc_all ? "NO" : "yes");
+    for (bw_ctx* x : ctxs) bw_destroy(x);
+    return rc_all;
+}
