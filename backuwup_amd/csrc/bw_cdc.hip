@@ -445,14 +445,37 @@ __device__ void rescan_range(const uint8_t* __restrict__ data, uint64_t n_bytes,
 // compaction adds the block base and copies the slots.
 constexpr int TS_BLOCK = 256;  // threads per block, 4 counts each
 
+// Candidate-dense batches (small parameters: most tiles overflow) rescan their overflowed tiles
+// in a kernel of their own, the list spread over the whole grid (inside k_tile_partial a
+// block owns 1,024 tiles, so a 64 MiB batch of 64 KiB tiles rescanned all of them on one block);
+// sparse ones (backuwup's parameters: no overflow on random data) keep the rescan inside
+// k_tile_partial / k_compact and save the two launches.
+template <bool WRITE>
+__global__ __launch_bounds__(RESCAN_THREADS) void k_rescan(const uint8_t* __restrict__ data, uint64_t n_bytes, Masks mk,
+                                                            const uint32_t* __restrict__ ovf, uint32_t* __restrict__ cnt,
+                                                            const uint64_t* __restrict__ off, uint64_t* __restrict__ cand,
+                                                            uint64_t cap, const uint64_t* ctr) {
+    __shared__ uint64_t s_gear[256], s_scan[RESCAN_THREADS];
+    const uint64_t novf = ctr[C_NOVF];
+    if (blockIdx.x >= novf) return;  // uniform per block
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_gear[i] = c_gear[i];
+    __syncthreads();
+    for (uint64_t k = blockIdx.x; k < novf; k += gridDim.x) {
+        const uint64_t tile = ovf[k];
+        const uint64_t total = rescan_tile<WRITE>(data, n_bytes, mk, tile, WRITE ? off[tile] : 0, cand, cap, s_gear, s_scan);
+        if (!WRITE && threadIdx.x == 0) cnt[tile] = (uint32_t)total | TILE_OVF;
+    }
+}
+
 __global__ __launch_bounds__(TS_BLOCK) void k_tile_partial(const uint8_t* __restrict__ data, uint64_t n_bytes, Masks mk,
                                                            const uint32_t* __restrict__ ovf, uint32_t* __restrict__ cnt,
                                                            uint64_t n, uint64_t* __restrict__ off,
-                                                           uint64_t* __restrict__ btot, uint64_t cap, uint64_t* ctr) {
+                                                           uint64_t* __restrict__ btot, uint64_t cap, uint64_t* ctr,
+                                                           bool spread) {
     __shared__ uint64_t s[TS_BLOCK];
     __shared__ uint64_t s_gear[256];
     // exact counts of this block's overflowed tiles first (what a separate k_rescan<false> did)
-    const uint64_t novf = ctr[C_NOVF];
+    const uint64_t novf = spread ? 0 : ctr[C_NOVF];
     if (novf) {
         const uint64_t t0 = (uint64_t)blockIdx.x * 4 * TS_BLOCK, t1 = t0 + 4 * TS_BLOCK;
         rescan_range<false>(data, n_bytes, mk, ovf, novf, t0, t1 < n ? t1 : n, cnt, nullptr, nullptr, 0, s_gear, s);
@@ -492,7 +515,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ dat
                                                  const uint32_t* __restrict__ ovf, const uint32_t* __restrict__ cnt,
                                                  const uint64_t* __restrict__ slots, uint64_t* __restrict__ off,
                                                  const uint64_t* __restrict__ bbase, uint64_t n_tiles,
-                                                 uint64_t* __restrict__ cand, uint64_t cap, uint64_t* ctr) {
+                                                 uint64_t* __restrict__ cand, uint64_t cap, uint64_t* ctr, bool spread) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n_tiles) {
         const uint64_t o = off[t] + bbase[t / (4 * TS_BLOCK)];
@@ -506,7 +529,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ dat
         }
     }
     // this block's overflowed tiles, at their final offsets (what a separate k_rescan<true> did)
-    const uint64_t novf = ctr[C_NOVF];
+    const uint64_t novf = spread ? 0 : ctr[C_NOVF];
     if (novf) {
         __shared__ uint64_t s_gear[256], s_scan[RESCAN_THREADS];
         __syncthreads();  // the block's final offsets are written
@@ -521,10 +544,22 @@ void launch_compact(hipStream_t st, const uint8_t* data, uint64_t n_bytes, uint6
                     uint64_t cand_cap, uint32_t* ovf_list, uint64_t* ctr, uint64_t* btot) {
     if (!n_tiles) return;
     const uint64_t nb = (n_tiles + 4 * TS_BLOCK - 1) / (4 * TS_BLOCK);
+    // candidate-dense parameters: expected flagged 64-byte blocks per tile (the scan's prefilter
+    // keeps 2^-popcount(pre_hi) of the bytes) above half of the SCAN_CAP slots a tile holds
+    const double flagged = (double)(1ull << mk.tile_shift) / 64.0 *
+                           (1.0 - pow(1.0 - ldexp(1.0, -__builtin_popcount(mk.pre_hi)), 64.0));
+    const bool spread = flagged > SCAN_CAP / 2;
+    const unsigned rb = (unsigned)std::min<uint64_t>(n_tiles, 2048);
+    if (spread)
+        hipLaunchKernelGGL(k_rescan<false>, dim3(rb), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_count,
+                           nullptr, nullptr, 0, ctr);
     hipLaunchKernelGGL(k_tile_partial, dim3((unsigned)nb), dim3(TS_BLOCK), 0, st, data, n_bytes, mk, ovf_list,
-                       tile_count, n_tiles, tile_off, btot, cand_cap, ctr);
+                       tile_count, n_tiles, tile_off, btot, cand_cap, ctr, spread);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, data, n_bytes, mk, ovf_list,
-                       tile_count, tile_slots, tile_off, btot, n_tiles, cand, cand_cap, ctr);
+                       tile_count, tile_slots, tile_off, btot, n_tiles, cand, cand_cap, ctr, spread);
+    if (spread)
+        hipLaunchKernelGGL(k_rescan<true>, dim3(rb), dim3(RESCAN_THREADS), 0, st, data, n_bytes, mk, ovf_list, tile_count,
+                           tile_off, cand, cand_cap, ctr);
 }
 
 // ======================================================================== the boundary walker

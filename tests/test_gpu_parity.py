@@ -341,6 +341,43 @@ def _dense_input():
     return data
 
 
+def _dense_input_bk(n=8 << 20):
+    """A 64-byte period one of whose windows is an exact MaskL candidate at backuwup's parameters:
+    a candidate every 64 bytes, so every scan tile overflows while the parameters keep the rescan
+    inside k_tile_partial / k_compact (the sparse-parameter path; SMALL takes the spread k_rescan)."""
+    from oracle import oracle as o
+    gear = np.array([int(x) for x in o.gear_table()], dtype=np.uint64)
+    _, ml = o.masks(*BK)
+    rng = np.random.default_rng(2024)
+    for _ in range(64):
+        pat = rng.integers(0, 256, (4096, 64), dtype=np.uint8)
+        g = gear[pat]
+        for r in range(64):  # window hash ending at period position r: sum_k GEAR[pat[r - k]] << k
+            h = np.zeros(len(pat), dtype=np.uint64)
+            for k in range(64):
+                h += g[:, (r - k) % 64] << np.uint64(k)
+            hit = np.nonzero((h & np.uint64(ml)) == 0)[0]
+            if hit.size:
+                body = np.tile(pat[hit[0]], n // 64 + 1)[:n]
+                body[:1000] = splitmix_bytes(3, 1000)
+                return body
+    pytest.skip("no periodic MaskL candidate found")
+
+
+def test_candidate_dense_backuwup_params(ctx, oracle):
+    """candidate-dense data at backuwup's own parameters (every tile overflows, exact
+    rescans inside the compaction kernels) and at small parameters (the rescans spread over a grid
+    of their own): boundaries, Chunk.hash and digests equal the oracle."""
+    data = _dense_input_bk()
+    assert ctx.fastcdc_chunks(data, *BK) == chunks_oracle(oracle, data, BK)
+    offs = np.array([0, 3 << 20, 5 << 20], dtype=np.uint64)
+    lens = np.array([3 << 20, 2 << 20, data.size - (5 << 20)], dtype=np.uint64)
+    ctx.index_reset()
+    blobs_equal(ctx.process_files(data, offs, lens), oracle.process_files(data, offs, lens))
+    small = _dense_input()
+    assert ctx.fastcdc_chunks(small, *SMALL) == chunks_oracle(oracle, small, SMALL)
+
+
 @pytest.mark.parametrize("small_bytes", [0, 2**64 - 1])
 def test_scan_tile_sizes(oracle, small_bytes):
     """Batches below 4 GiB scan half-size tiles (bw_capi.hip submit): force each tile size
