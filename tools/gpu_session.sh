@@ -22,4 +22,7 @@ if [[ "$MODE" == *prof* || "$MODE" == all ]]; then
   # the bench command itself (default steps / batches in flight), so the per-launch durations of
   # the timed region can be compared with the bench line (tools/trace_split.py)
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline || exit 1
+  # the leaf pass's timed launches from the trace: mean, union per step, achieved on the union
+  T=$(find "$OUT/prof" -name "*kernel_trace.csv" | head -1)
+  [ -n "$T" ] && python3 "$GRAFT_REPO_ROOT/tools/trace_split.py" "$T" k_b3_lines 2 320 17179869184 > "$OUT/trace_split.json" 2>&1
 fi
