@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
-: > "$OUT/summary.txt"
+: > "$OUT/dropin_summary.txt"
 python3 - <<'EOF' > "$OUT/corpus.log" 2>&1 || exit 1
 import numpy as np, sys
 sys.path.insert(0, ".")
@@ -21,8 +21,8 @@ print("files", len(o), "bytes", int(np.sum(l)))
 EOF
 for t in ${THREADS:-16 8}; do
   timeout -k 10 300 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 > "$OUT/dropin_t$t.log" 2>&1
-  rc=$?; echo "dropin t=$t rc=$rc" >> "$OUT/summary.txt"; [ $rc -eq 0 ] || exit 1
+  rc=$?; echo "dropin t=$t rc=$rc" >> "$OUT/dropin_summary.txt"; [ $rc -eq 0 ] || exit 1
 done
 timeout -k 10 600 python3 bench.py --workload c1 --steps 300 > "$OUT/bench_c1.log" 2>&1
-rc=$?; echo "bench c1 rc=$rc" >> "$OUT/summary.txt"; [ $rc -eq 0 ] || exit 1
+rc=$?; echo "bench c1 rc=$rc" >> "$OUT/dropin_summary.txt"; [ $rc -eq 0 ] || exit 1
 exit 0

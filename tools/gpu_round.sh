@@ -1,0 +1,47 @@
+#!/bin/bash
+# One GPU session of several steps (round 4), chosen by STEPS (default: all).  Every step runs under
+# its own time limit; a step that times out, aborts or faults (rc 124/134/137/139 or a signal) ends
+# the session there, any other failure is recorded and the next step runs.  Results go to
+# gpurun_out/ (summary.txt lists each step's rc).
+#   tests    pytest -m gpu                       smoke   __graft_entry__.smoke()
+#   collide  tools/collide.hip (BLAKE3 8-byte prefix collision -> gpurun_out/*.json)
+#   slab     tools/gpu_slab.sh (Infinity-Cache reuse of the leaf pass)
+#   dropin   tools/gpu_dropin.sh (the reference's call sites on C1)
+#   bench    python bench.py $BENCH_ARGS         prof    rocprofv3 --kernel-trace --stats of the bench
+#   pmc      tools/gpu_pmc.sh (FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json)
+#   debug    tools/debug_check.py (BW_DEBUG + BW_DIAG library)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT="$GRAFT_REPO_ROOT/gpurun_out"
+mkdir -p "$OUT"
+: > "$OUT/summary.txt"
+STEPS=${STEPS:-"tests smoke collide slab dropin bench"}
+step() {
+  local name=$1 t=$2; shift 2
+  echo "== $name $(date +%T)" >&2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/summary.txt" >&2
+  case $rc in
+    0|1|2|3|4|5) return 0 ;;
+    *) echo "stopping after $name (rc=$rc)" >> "$OUT/summary.txt"; exit 1 ;;
+  esac
+}
+for s in $STEPS; do
+  case $s in
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 300 python __graft_entry__.py ;;
+    collide) step collide 120 ./build_ab/collide "$OUT/blake3_prefix_collision.json" 14 32768 1 ;;
+    slab) step slab 900 bash tools/gpu_slab.sh ;;
+    dropin) step dropin 900 bash tools/gpu_dropin.sh ;;
+    bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
+        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline) || exit 1
+      T=$(find "$OUT/prof" -name "*kernel_trace.csv" | head -1)
+      [ -n "$T" ] && python3 tools/trace_split.py "$T" k_b3_lines 2 320 17179869184 > "$OUT/trace_split.json" 2>&1 ;;
+    pmc) step pmc 900 bash tools/gpu_pmc.sh ;;
+    debug) step debug_check 600 python tools/debug_check.py ;;
+  esac
+done
+exit 0

@@ -9,7 +9,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
-: > "$OUT/summary.txt"
+: > "$OUT/slab_summary.txt"
 HOLD=${HOLD:-10}
 CONFIGS=${CONFIGS:-"cold:0:4 cold:0:1 slab:64:1 slab:128:1 slab:96:2 slab:192:1 slab:64:4 scan:0:4 hash:0:4"}
 for cfg in $CONFIGS; do
@@ -20,7 +20,7 @@ for cfg in $CONFIGS; do
   timeout -k 10 120 ./build_ab/slab "$mode" "$s" "$g" "$HOLD" > "$OUT/slab_$name.log" 2>&1
   RC=$?
   wait $P
-  echo "$name rc=$RC $(head -1 "$OUT/slab_$name.log")" >> "$OUT/summary.txt"
+  echo "$name rc=$RC $(head -1 "$OUT/slab_$name.log")" >> "$OUT/slab_summary.txt"
   [ $RC -eq 0 ] || exit 1
 done
 cd /tmp && export TMPDIR=/tmp
@@ -29,6 +29,6 @@ for cfg in ${PMC_CONFIGS:-"cold:0:1 slab:128:1 slab:64:1 cold:0:4"}; do
   name="${mode}_${s}_${g}"
   timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_$name" -o run --pmc FETCH_SIZE -- \
     "$GRAFT_REPO_ROOT/build_ab/slab" "$mode" "$s" "$g" > "$OUT/pmc_$name.log" 2>&1 || exit 1
-  echo "pmc $name rc=0" >> "$OUT/summary.txt"
+  echo "pmc $name rc=0" >> "$OUT/slab_summary.txt"
 done
 exit 0
