@@ -188,3 +188,27 @@ def test_blake3_simd_baseline_is_bit_exact(oracle):
     finally:
         oracle.set_blake3_simd(False)
     assert np.array_equal(a, b)
+
+
+def _prefix_collision():
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "blake3_prefix_collision.json")
+    if not os.path.exists(p):
+        pytest.skip("tests/golden/blake3_prefix_collision.json not generated (tools/collide.hip)")
+    return json.load(open(p))
+
+
+def test_blake3_prefix_collision_fixture(oracle):
+    """A genuine collision of BLAKE3 on the first 8 digest bytes (found on the GPU by tools/collide.hip,
+    parallel collision search): two distinct 8-byte messages whose digests share the 64-bit key the
+    round-3 device index merged slots by.  The oracle's BLAKE3 confirms both digests."""
+    fx = _prefix_collision()
+    m1, m2 = bytes.fromhex(fx["m1"]), bytes.fromhex(fx["m2"])
+    d1, d2 = oracle.blake3(m1), oracle.blake3(m2)
+    assert m1 != m2 and len(m1) == len(m2) == 8
+    assert d1.hex() == fx["digest1"] and d2.hex() == fx["digest2"]
+    assert d1[:8] == d2[:8] and d1 != d2
+    ix = oracle.Index()  # the reference's BlobIndex keeps both
+    assert not ix.is_blob_duplicate(d1) and ix.insert(d1) == 0
+    assert not ix.is_blob_duplicate(d2) and ix.insert(d2) == 0
