@@ -1731,7 +1731,17 @@ extern "C" int bw_fastcdc_chunks_hashed(bw_ctx* c, const uint8_t* src, uint64_t 
     const uint64_t off = 0;
     std::vector<bw_blob> tmp(len / std::min<uint64_t>(mk.s0, mk.max) + 2);
     uint64_t n = 0;
-    if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
+    {
+        // the file comes in through the context's pinned staging ring (memcpy on up to 16 host
+        // threads, DMA on the copy stream) rather than a pageable hipMemcpy: the reference's tasks
+        // call this from many threads at once, one mmap'd file each
+        hipSetDevice(c->device);
+        Slot& s = c->sync_slot;
+        s.ticket = 0;
+        if (int rc = stream_in(c, s, src, len)) return rc;
+        if (int rc = submit(c, s, P<uint8_t>(s.input), len, &off, &len, 1, &p)) return rc;
+        if (int rc = slot_results(c, s, tmp.data(), tmp.size(), &n)) return rc;
+    }
     *n_out = n;
     if (n > cap) return BW_ENOSPC;
     Kept k;
