@@ -3,7 +3,7 @@
 # failure before anything ran (status=transient / no box free, exit 3), honouring the
 # back-off it announces.  Never retries a command that actually ran on the GPU.
 cmd="$1"; tmo="${2:-1200}"
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 ${GPU_TRIES:-40}); do
   # archive the previous call's scratch where the judge can read it: every file (the verdict
   # .last_call.json and any .graft_* marker included) goes to profiles/<round>/calls/<time>/; files
   # over 8 MiB (raw traces) are listed there by size instead of copied
