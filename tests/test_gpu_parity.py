@@ -491,3 +491,37 @@ def test_dropin_call_sites_kept_digests(ctx, oracle):
     del chunker
     # empty source: no chunks, nothing kept
     assert ctx.fastcdc_chunks_hashed(np.zeros(0, np.uint8), *BK) == ([], 0)
+
+
+def test_dropin_call_sites_many_threads(oracle):
+    """The reference runs process_file as one tokio task per file (dir_packer.rs:166): four threads,
+    one context each, chunk + hash their own files through the kept-digest drop-ins at the same
+    time (the kept digests are one process-wide registry); every chunk and digest equals the
+    oracle's and every per-chunk hash is answered from the kept digests."""
+    import threading
+    from backuwup_amd import Context, _lib
+    L = _lib.load()
+    files = [splitmix_bytes(900 + k, (3 << 20) + 7919 * k) for k in range(8)]
+    want = [[(o, n, oracle.blake3(f[o:o + n])) for _, o, n in oracle.fastcdc(f, *BK)] for f in files]
+    got = [None] * len(files)
+    errors = []
+    hits0 = L.bw_blake3_kept_hits()
+
+    def worker(t):
+        try:
+            with Context(0) as c:
+                for k in range(t, len(files), 4):
+                    chunks, h = c.fastcdc_chunks_hashed(files[k], *BK)
+                    got[k] = [(o, n, c.blake3_at(files[k], o, n)) for _, o, n in chunks]
+                    c.fastcdc_release(h)
+        except Exception as e:  # reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errors, errors
+    assert got == want
+    assert L.bw_blake3_kept_hits() - hits0 == sum(len(w) for w in want)
