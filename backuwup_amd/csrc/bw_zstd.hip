@@ -617,6 +617,48 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 if (cL) xL = ld64(s + (mil - ib));
                 if (c3) x3 = ld64(s + (m3 - ib));
                 if (cS) xS = ld32(s + (mis - ib));
+                // In the same round, the extension of lane 0's candidates (on compressible data most
+                // steps match at lane 0): lanes 16g .. 16g + 15 compare the first 128 forward bytes
+                // and the first 16 backward byte pairs of candidate kind g (0 repeat, 1 long, 2 long
+                // at pos + 1, 3 short), exactly as wave_extend would; a match that is resolved inside
+                // those windows skips wave_extend's round of loads.
+                const uint32_t sg = lane >> 4, sj = lane & 15;
+                uint32_t sp, sm, skn;
+                bool sval;
+                {
+                    const uint32_t p0 = rdlane(pos, 0);
+                    const bool v0 = rdlane((uint32_t)valid, 0) != 0;
+                    const uint32_t l0 = rdlane(mil, 0), s0m = rdlane(mis, 0), t0 = rdlane(m3, 0);
+                    sp = (sg == 0 || sg == 2) ? p0 + 1 : p0;
+                    skn = (sg == 1 || sg == 2) ? 8 : 4;
+                    if (sg == 0) {
+                        sval = v0 && o1 != 0 && o1 <= sp;
+                        sm = sp - o1;
+                    } else {
+                        const uint32_t mi = sg == 1 ? l0 : (sg == 2 ? t0 : s0m);
+                        sval = v0 && mi > pli;
+                        sm = mi - ib;
+                    }
+                }
+                uint32_t sfd = 8;
+                bool sbeq = false;
+                if (sval) {
+                    const uint32_t so = sp + skn + 8 * sj, smm = sm + skn + 8 * sj;
+                    if (so + 8 <= iend) {
+                        const uint64_t x = ld64(s + so) ^ ld64(s + smm);
+                        if (x) sfd = (uint32_t)__builtin_ctzll(x) >> 3;
+                    } else if (so < iend) {
+                        const uint32_t rem = iend - so;
+                        sfd = rem;
+                        for (uint32_t i = 0; i < rem; i++)
+                            if (s[so + i] != s[smm + i]) { sfd = i; break; }
+                    } else {
+                        sfd = 0;
+                    }
+                    const uint32_t slim = sg == 0 ? 0 : ((sp - anchor) < (sm - plo) ? sp - anchor : sm - plo);
+                    if (sj < slim) sbeq = s[sp - 1 - sj] == s[sm - 1 - sj];
+                }
+                const uint64_t sfm = __ballot(sfd < 8), sbn = __ballot(!sbeq);
                 const bool evR = valid && o1 && vrep == (uint32_t)v8n;
                 const bool evL = cL && xL == v8, evS = cS && xS == (uint32_t)v8, ev3 = c3 && x3 == v8n;
                 const uint64_t emask = __ballot(evR || evL || evS);
@@ -666,7 +708,17 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 }
                 if (!eR) lim = (p - anchor) < (m - plo) ? p - anchor : m - plo;
                 uint32_t fwd, back;
-                wave_extend(s, p + known, m + known, iend, p, m, lim, lane, fwd, back);
+                const uint32_t gsel = eR ? 0 : (eL ? 1 : (rdlane(ev3, e) ? 2 : 3));
+                const uint64_t gm = 0xFFFFull << (16 * gsel);
+                const uint64_t fm = sfm & gm, bm = sbn & gm;
+                if (e == 0 && fm && (gsel == 0 || bm)) {  // resolved by the speculative windows
+                    const uint32_t L = (uint32_t)__builtin_ctzll(fm);
+                    const uint32_t n = 8 * (L - 16 * gsel) + rdlane(sfd, L), a = p + known;
+                    fwd = (a + n > iend) ? iend - a : n;
+                    back = gsel == 0 ? 0 : (uint32_t)__builtin_ctzll(bm) - 16 * gsel;
+                } else {
+                    wave_extend(s, p + known, m + known, iend, p, m, lim, lane, fwd, back);
+                }
                 uint32_t mLength = fwd + known;
                 if (eR) {
                     if (lane == 0) sq[nseq] = seq_pack(p - anchor, mLength - 3, 1);

@@ -10,12 +10,13 @@
 #   bench    python bench.py $BENCH_ARGS         prof    rocprofv3 --kernel-trace --stats of the bench
 #   pmc      tools/gpu_pmc.sh (FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json)
 #   debug    tools/debug_check.py (BW_DEBUG + BW_DIAG library)
+#   zstd     tools/zstd_bench.py on 1 GiB and 8 GiB of text (level-3 frames, oracle-checked sample)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
 : > "$OUT/summary.txt"
-STEPS=${STEPS:-"tests smoke collide slab dropin bench"}
+STEPS=${STEPS:-"tests smoke collide zstd slab dropin bench"}
 step() {
   local name=$1 t=$2; shift 2
   echo "== $name $(date +%T)" >&2
@@ -42,6 +43,8 @@ for s in $STEPS; do
       [ -n "$T" ] && python3 tools/trace_split.py "$T" k_b3_lines 2 320 17179869184 > "$OUT/trace_split.json" 2>&1 ;;
     pmc) step pmc 900 bash tools/gpu_pmc.sh ;;
     debug) step debug_check 600 python tools/debug_check.py ;;
+    zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
+          step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
   esac
 done
 exit 0
