@@ -30,7 +30,7 @@ step() {
 }
 for s in $STEPS; do
   case $s in
-    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu --maxfail 20 -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python __graft_entry__.py ;;
     collide) step collide 120 ./build_ab/collide "$OUT/blake3_prefix_collision.json" 14 32768 1 ;;
     slab) step slab 900 bash tools/gpu_slab.sh ;;
