@@ -818,11 +818,14 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                         c8 = win8(dw, p - 1 - wb);
                         rA = (uint32_t)win8(dw, p - wb);
                         rB = o2 ? (uint32_t)win8(sbw, roff) : ~rA;
+                        // the lane shuffles run with every lane active (a shuffle from an inactive lane
+                        // is undefined); group gsel's words sit in lanes 16 gsel .. 16 gsel + 15
+                        const uint64_t t8 = win8_lane(dw, p + lane - wb), t8n = win8_lane(dw, p + lane + 1 - wb);
+                        const uint32_t trep = (uint32_t)win8_lane(sbw, 128 * gsel + boff + lane);
                         if (p + lane < ilimit) {
-                            pv8 = win8_lane(dw, p + lane - wb);
-                            pv8n = win8_lane(dw, p + lane + 1 - wb);
-                            // group gsel's words sit in lanes 16 gsel .. 16 gsel + 15: byte 128 gsel + boff
-                            pvrep = (uint32_t)win8_lane(sbw, 128 * gsel + boff + lane);
+                            pv8 = t8;
+                            pv8n = t8n;
+                            pvrep = trep;
                         }
                     } else
 #endif
