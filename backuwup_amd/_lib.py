@@ -158,7 +158,7 @@ SIGNATURES = [
     ("bw_index_load_files", ctypes.c_int, [vp, vp, vp, ctypes.POINTER(BwIndexFile), ctypes.c_uint64, vp,
                                            ctypes.c_uint64, u64p, u64p]),
     ("bw_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
-    ("bw_fastcdc_chunks_hashed", ctypes.c_int, [vp, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+    ("bw_fastcdc_chunks_hashed", ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                                 ctypes.c_uint32, vp, ctypes.c_uint64, u64p, u64p]),
     ("bw_fastcdc_release", None, [ctypes.c_uint64]),
     ("bw_blake3_kept_hits", ctypes.c_uint64, []),

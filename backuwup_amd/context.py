@@ -177,8 +177,7 @@ class Context:
         reference hashes each chunk slice of its mmap (dir_packer.rs:262-265, :286)."""
         assert isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and offset + length <= buf.size
         out = (ctypes.c_uint8 * 32)()
-        p = ctypes.cast(buf.ctypes.data + offset, _lib.u8p)
-        check(self._L.bw_blake3_hash(self.h, p, length, out), self.h)
+        check(self._L.bw_blake3_hash(self.h, ctypes.c_void_p(buf.ctypes.data + offset), length, out), self.h)
         return bytes(out)
 
     def blake3_many(self, data, offsets, lengths):

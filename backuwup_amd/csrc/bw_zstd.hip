@@ -119,25 +119,6 @@ __device__ __forceinline__ uint32_t seq_ov(uint64_t q) { return (uint32_t)(q >> 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
-__device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
-    return (uint64_t)rdlane((uint32_t)v, l) | ((uint64_t)rdlane((uint32_t)(v >> 32), l) << 32);
-}
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t l) {
-    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, (int)l) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)l) << 32);
-}
-// 8 bytes at byte offset `off` of a window held as one 8-byte word per lane (word i = bytes
-// [8i, 8i + 8)), off uniform (off / 8 + 1 < 64 when off is not a multiple of 8)
-__device__ __forceinline__ uint64_t win8(uint64_t w, uint32_t off) {
-    const uint32_t li = off >> 3, sh = (off & 7) * 8;
-    const uint64_t w0 = rdlane64(w, li);
-    return sh ? (w0 >> sh) | (rdlane64(w, li + 1) << (64 - sh)) : w0;
-}
-// the same with a per-lane offset
-__device__ __forceinline__ uint64_t win8_lane(uint64_t w, uint32_t off) {
-    const uint32_t li = off >> 3, sh = (off & 7) * 8;
-    const uint64_t w0 = shfl64(w, li & 63), w1 = shfl64(w, (li + 1) & 63);
-    return sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-}
 
 // ------------------------------------------------------------------ FSE (serial, one lane)
 struct FseTT {
@@ -469,9 +450,6 @@ __device__ void wave_extend(const uint8_t* s, uint32_t a, uint32_t b, uint32_t l
     }
 }
 
-#ifndef BW_ZS_SPEC2
-#define BW_ZS_SPEC2 0  // experimental: the post-match round from the speculative windows (A/B variant)
-#endif
 #ifndef BW_ZS_WMIN
 #define BW_ZS_WMIN 2  // probe window after a match at lane 0 (text: the mean first-match lane is 0.2-0.3)
 #endif
@@ -639,73 +617,6 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 if (cL) xL = ld64(s + (mil - ib));
                 if (c3) x3 = ld64(s + (m3 - ib));
                 if (cS) xS = ld32(s + (mis - ib));
-                // In the same round, the extension of lane 0's candidates (on compressible data most
-                // steps match at lane 0): lanes 16g .. 16g + 15 compare the first 128 forward bytes
-                // and the first 16 backward byte pairs of candidate kind g (0 repeat, 1 long, 2 long
-                // at pos + 1, 3 short), exactly as wave_extend would; a match that is resolved inside
-                // those windows skips wave_extend's round of loads.
-                const uint32_t sg = lane >> 4, sj = lane & 15;
-                uint32_t sp, sm, skn;
-                bool sval;
-                const uint32_t p0 = rdlane(pos, 0);
-                const bool v0 = rdlane((uint32_t)valid, 0) != 0;
-#if BW_ZS_SPEC2
-                // and the bytes around it: [wb, wb + 512) one word per lane (below iend only), for the
-                // insert keys, the repeat check and the next step's data after a match at lane 0
-                const uint32_t wb = p0 >= 8 ? p0 - 8 : 0;
-                uint64_t dw = 0;
-                if (v0) {
-                    const uint32_t x = wb + 8 * lane;
-                    if (x + 8 <= iend) {
-                        dw = ld64(s + x);
-                    } else if (x < iend) {
-                        for (uint32_t i = 0; i < iend - x; i++) dw |= (uint64_t)s[x + i] << (8 * i);
-                    }
-                }
-                uint64_t sbw = 0;  // this lane's candidate-side word of its group's forward window
-                bool shb = false;  // ... loaded
-#endif
-                {
-                    const uint32_t l0 = rdlane(mil, 0), s0m = rdlane(mis, 0), t0 = rdlane(m3, 0);
-                    sp = (sg == 0 || sg == 2) ? p0 + 1 : p0;
-                    skn = (sg == 1 || sg == 2) ? 8 : 4;
-                    if (sg == 0) {
-                        sval = v0 && o1 != 0 && o1 <= sp;
-                        sm = sp - o1;
-                    } else {
-                        const uint32_t mi = sg == 1 ? l0 : (sg == 2 ? t0 : s0m);
-                        sval = v0 && mi > pli;
-                        sm = mi - ib;
-                    }
-                }
-                uint32_t sfd = 8;
-                bool sbeq = false;
-                if (sval) {
-                    const uint32_t so = sp + skn + 8 * sj, smm = sm + skn + 8 * sj;
-                    if (so + 8 <= iend) {
-                        const uint64_t bw8 = ld64(s + smm);
-                        const uint64_t x = ld64(s + so) ^ bw8;
-                        if (x) sfd = (uint32_t)__builtin_ctzll(x) >> 3;
-#if BW_ZS_SPEC2
-                        sbw = bw8;
-                        shb = true;
-#endif
-                    } else if (so < iend) {
-                        const uint32_t rem = iend - so;
-                        sfd = rem;
-                        for (uint32_t i = 0; i < rem; i++)
-                            if (s[so + i] != s[smm + i]) { sfd = i; break; }
-                    } else {
-                        sfd = 0;
-                    }
-                    const uint32_t slim = sg == 0 ? 0 : ((sp - anchor) < (sm - plo) ? sp - anchor : sm - plo);
-                    if (sj < slim) sbeq = s[sp - 1 - sj] == s[sm - 1 - sj];
-                }
-                const uint64_t sfm = __ballot(sfd < 8), sbn = __ballot(!sbeq);
-#if BW_ZS_SPEC2
-                const uint64_t shbm = __ballot(shb);
-                const uint32_t o1_before = o1, sm0 = rdlane(sm, 0);
-#endif
                 const bool evR = valid && o1 && vrep == (uint32_t)v8n;
                 const bool evL = cL && xL == v8, evS = cS && xS == (uint32_t)v8, ev3 = c3 && x3 == v8n;
                 const uint64_t emask = __ballot(evR || evL || evS);
@@ -755,18 +666,7 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 }
                 if (!eR) lim = (p - anchor) < (m - plo) ? p - anchor : m - plo;
                 uint32_t fwd, back;
-                const uint32_t gsel = eR ? 0 : (eL ? 1 : (rdlane(ev3, e) ? 2 : 3));
-                const uint64_t gm = 0xFFFFull << (16 * gsel);
-                const uint64_t fm = sfm & gm, bm = sbn & gm;
-                const bool spec = e == 0 && fm && (gsel == 0 || bm);
-                if (spec) {  // resolved by the speculative windows
-                    const uint32_t L = (uint32_t)__builtin_ctzll(fm);
-                    const uint32_t n = 8 * (L - 16 * gsel) + rdlane(sfd, L), a = p + known;
-                    fwd = (a + n > iend) ? iend - a : n;
-                    back = gsel == 0 ? 0 : (uint32_t)__builtin_ctzll(bm) - 16 * gsel;
-                } else {
-                    wave_extend(s, p + known, m + known, iend, p, m, lim, lane, fwd, back);
-                }
+                wave_extend(s, p + known, m + known, iend, p, m, lim, lane, fwd, back);
                 uint32_t mLength = fwd + known;
                 if (eR) {
                     if (lane == 0) sq[nseq] = seq_pack(p - anchor, mLength - 3, 1);
@@ -784,64 +684,15 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 p += mLength;
                 anchor = p;
                 if (p <= ilimit) {
+                    // one round of loads: the four insert keys, the repeat check and the next step's data
                     const uint32_t iti = cu + 2, pti = iti - ib;
-                    uint64_t a8, b8, c8;
-                    uint32_t rA, rB;
-#if BW_ZS_SPEC2
-                    // After a non-repeat match at lane 0 resolved by the windows, every byte this step
-                    // needs is in registers already: the insert keys and the next step's data in the
-                    // window around p0, its repeat data (m_end + 1 + lane) in the chosen candidate's
-                    // window, and the repeat check's bytes (p - previous offset) in the repeat
-                    // candidate's window.  Only lanes 0 .. W - 1 (= 1) of the next step's data are used.
-                    bool fast = false;
-                    uint32_t roff = 0, boff = 0;
-                    if (spec && gsel != 0 && p + 12 <= wb + 504) {
-                        // the next step's repeat bytes: p + 1 + lane - offset = msel + known + fwd + 1 + lane,
-                        // at fwd + 1 + lane in the chosen candidate's window (based at msel + known)
-                        boff = fwd + 1;
-                        const uint32_t bl = 16 * gsel + (boff >> 3);
-                        bool ok = boff + 1 + 4 <= 128 && ((shbm >> bl) & 1) && ((shbm >> (bl + 1)) & 1 || (boff & 7) == 0);
-                        if (ok && o2) {  // o2 = the offset before this match: the repeat window holds p - o2
-                            const uint32_t rbase = sm0 + 4;  // group 0: (p0 + 1 - o1) + 4
-                            const uint32_t x = p - o2;
-                            ok = o2 == o1_before && x >= rbase && x - rbase + 8 <= 128;
-                            if (ok) {
-                                roff = x - rbase;
-                                ok = ((shbm >> (roff >> 3)) & 1) && ((shbm >> ((roff >> 3) + 1)) & 1);
-                            }
-                        }
-                        fast = ok;
-                    }
-                    if (fast) {
-                        a8 = win8(dw, pti - wb);
-                        b8 = win8(dw, p - 2 - wb);
-                        c8 = win8(dw, p - 1 - wb);
-                        rA = (uint32_t)win8(dw, p - wb);
-                        rB = o2 ? (uint32_t)win8(sbw, roff) : ~rA;
-                        // the lane shuffles run with every lane active (a shuffle from an inactive lane
-                        // is undefined); group gsel's words sit in lanes 16 gsel .. 16 gsel + 15
-                        const uint64_t t8 = win8_lane(dw, p + lane - wb), t8n = win8_lane(dw, p + lane + 1 - wb);
-                        const uint32_t trep = (uint32_t)win8_lane(sbw, 128 * gsel + boff + lane);
-                        if (p + lane < ilimit) {
-                            pv8 = t8;
-                            pv8n = t8n;
-                            pvrep = trep;
-                        }
-                    } else
-#endif
-                    {
-                        // one round of loads: the four insert keys, the repeat check and the next step's data
-                        a8 = ld64(s + pti);
-                        b8 = ld64(s + p - 2);
-                        c8 = ld64(s + p - 1);
-                        rA = ld32(s + p);
-                        rB = ld32(s + p - o2);
-                        // lanes past ilimit read at p - 1 (p <= ilimit: bytes up to iend, never past the block)
-                        if (p + lane < ilimit) {
-                            pv8 = ld64(s + p + lane);
-                            pv8n = ld64(s + p + lane + 1);
-                            pvrep = ld32(s + p + lane + 1 - o1);
-                        }
+                    const uint64_t a8 = ld64(s + pti), b8 = ld64(s + p - 2), c8 = ld64(s + p - 1);
+                    uint32_t rA = ld32(s + p), rB = ld32(s + p - o2);
+                    // lanes past ilimit read at p - 1 (p <= ilimit: bytes up to iend, never past the block)
+                    if (p + lane < ilimit) {
+                        pv8 = ld64(s + p + lane);
+                        pv8n = ld64(s + p + lane + 1);
+                        pvrep = ld32(s + p + lane + 1 - o1);
                     }
                     if (!o2) rB = ~rA;
                     pre = true;

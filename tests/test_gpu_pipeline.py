@@ -754,9 +754,9 @@ from backuwup_amd._lib import BwError
 t0 = time.time()
 try:
     Comm.rccl(0, 0, 2, unique_id(), timeout_ms=4000)
-    print("JOINED")
+    print("@@JOINED")
 except BwError as e:
-    print("RC", e.rc, round(time.time() - t0, 1))
+    print("@@RC", e.rc, round(time.time() - t0, 1))
 """
 
 
@@ -769,8 +769,8 @@ def test_rccl_init_deadline_when_a_rank_never_joins():
     from backuwup_amd._lib import BW_ECOMM
     root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", _NEVER_JOINED % root], capture_output=True, text=True, timeout=90)
-    line = [l for l in out.stdout.splitlines() if l.startswith(("RC", "JOINED"))]
-    assert line and line[0].startswith("RC"), (out.stdout[-2000:], out.stderr[-2000:])
+    line = [l for l in out.stdout.splitlines() if l.startswith(("@@RC", "@@JOINED"))]
+    assert line and line[0].startswith("@@RC"), (out.stdout[-2000:], out.stderr[-2000:])
     _, rc, dt = line[0].split()
     assert int(rc) == BW_ECOMM and 3.5 < float(dt) < 30, line
 

@@ -16,7 +16,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
 : > "$OUT/summary.txt"
-STEPS=${STEPS:-"tests smoke collide zstd zstd2 slab dropin bench"}
+STEPS=${STEPS:-"tests smoke slab dropin bench"}
 step() {
   local name=$1 t=$2; shift 2
   echo "== $name $(date +%T)" >&2
@@ -45,11 +45,6 @@ for s in $STEPS; do
     debug) step debug_check 600 python tools/debug_check.py ;;
     zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
           step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
-    zstd2)  # the BW_ZS_SPEC2 variant library (build: backuwup_amd.build.build(variant="zs2", defines=("-DBW_ZS_SPEC2=1",)))
-      step zstd2_tests 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zs2.so" python -u -m pytest \
-        tests/test_zstd.py tests/test_pack.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread &&
-      step zstd2_text1 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zs2.so" python tools/zstd_bench.py \
-        --gib 1 --kind text --reps 2 --check 16 ;;
   esac
 done
 exit 0

@@ -101,7 +101,8 @@ static void hash_part(hipStream_t st, const uint8_t* d, const Part& p, uint64_t 
 
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cold";
-    const uint64_t S = (argc > 2 ? atoll(argv[2]) : 64) << 20;
+    uint64_t S = (argc > 2 ? atoll(argv[2]) : 64) << 20;
+    if (S == 0) S = 64ull << 20;  // cold / scan / hash: the slab tables are built but not used
     const int G = argc > 3 ? atoi(argv[3]) : 4;
     const double hold_s = argc > 4 ? atof(argv[4]) : 0;
     const uint32_t gshift = G == 1 ? 0 : G == 2 ? 1 : 2;
