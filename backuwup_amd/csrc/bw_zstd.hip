@@ -450,6 +450,14 @@ __device__ void wave_extend(const uint8_t* s, uint32_t a, uint32_t b, uint32_t l
     }
 }
 
+// The step's table writes reach the next probes of other lanes through a workgroup fence (a wait
+// for the wave's outstanding stores).  BW_ZS_NOFENCE (diagnostic measurement only, not exact by
+// the memory model) drops the two in the step loop to size what those waits cost.
+#ifdef BW_ZS_NOFENCE
+#define BW_ZS_FENCE() ((void)0)
+#else
+#define BW_ZS_FENCE() __threadfence_block()
+#endif
 #ifndef BW_ZS_WMIN
 #define BW_ZS_WMIN 2  // probe window after a match at lane 0 (text: the mean first-match lane is 0.2-0.3)
 #endif
@@ -518,7 +526,7 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
             uint64_t pv8 = 0, pv8n = 0;
             uint32_t pvrep = 0;
             while (ip < ilimit) {
-                __threadfence_block();
+                BW_ZS_FENCE();
                 ZT_START();
                 ZT_COUNT(4);
                 // this lane's position in the skip sequence ip += ((ip - anchor) >> 8) + 1
@@ -632,7 +640,7 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                     W = W < 32 ? 2 * W : 64;
                     continue;
                 }
-                __threadfence_block();
+                BW_ZS_FENCE();
                 const uint32_t e = lastw;
                 W = e < BW_ZS_WMIN / 2 ? BW_ZS_WMIN : (e < 4 ? 8 : (e < 8 ? 16 : (e < 16 ? 32 : 64)));
                 uint32_t p = rdlane(pos, e);

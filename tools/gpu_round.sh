@@ -43,6 +43,11 @@ for s in $STEPS; do
       [ -n "$T" ] && python3 tools/trace_split.py "$T" k_b3_lines 2 320 17179869184 > "$OUT/trace_split.json" 2>&1 ;;
     pmc) step pmc 900 bash tools/gpu_pmc.sh ;;
     debug) step debug_check 600 python tools/debug_check.py ;;
+    zsdiag)  # diagnostic zstd variants: section timers (BW_ZSTD_TIMING) and the step fences dropped
+      step zstd_ztime 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_ztime.so" python tools/zstd_bench.py \
+        --gib 1 --kind text --reps 1 --check 4 &&
+      step zstd_nofence 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zsnofence.so" python tools/zstd_bench.py \
+        --gib 1 --kind text --reps 2 --check 16 ;;
     zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
           step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
   esac
