@@ -15,7 +15,7 @@
 // Build (CPU, after the library):
 //   hipcc -O2 -std=c++17 -I include tools/dropin_c1.cpp -L backuwup_amd -lbackuwup_amd \
 //     -Wl,-rpath,$PWD/backuwup_amd -lpthread -o build_ab/dropin_c1
-// Run: build_ab/dropin_c1 <corpus.bin> [threads=16] [reps=3]
+// Run: build_ab/dropin_c1 <corpus.bin> [threads=16] [reps=3] [staging chunk MiB=64]
 //   corpus.bin = u64 n, n offsets, n lengths, then the bytes (tools/gpu_dropin.sh writes bench.py's C1)
 #include <atomic>
 #include <chrono>
@@ -92,6 +92,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     const int T = argc > 2 ? atoi(argv[2]) : 16, reps = argc > 3 ? atoi(argv[3]) : 3;
+    const uint64_t stage_mib = argc > 4 ? strtoull(argv[4], nullptr, 10) : 0;  // BW_OPT_STAGE_CHUNK (0: default)
     const uint64_t nf = c.off.size();
     uint64_t bytes = 0, big = 0;
     for (uint64_t i = 0; i < nf; i++) {
@@ -101,8 +102,11 @@ int main(int argc, char** argv) {
     printf("corpus: %llu files (%llu > 1 MiB), %.3f GB; %d threads, one context each\n", (unsigned long long)nf,
            (unsigned long long)big, bytes / 1e9, T);
     std::vector<bw_ctx*> ctxs(T);
-    for (int t = 0; t < T; t++)
+    for (int t = 0; t < T; t++) {
         if (bw_create(0, &ctxs[t])) return 3;
+        if (stage_mib && bw_set_option(ctxs[t], BW_OPT_STAGE_CHUNK, stage_mib << 20)) return 3;
+    }
+    if (stage_mib) printf("pinned staging chunks of %llu MiB\n", (unsigned long long)stage_mib);
     std::vector<FileOut> ref(nf), got(nf);
     int rc_all = 0;
     for (int mode = 0; mode < 2; mode++) {

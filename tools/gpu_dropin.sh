@@ -19,10 +19,12 @@ with open("/tmp/c1.bin", "wb") as f:
     d.tofile(f)
 print("files", len(o), "bytes", int(np.sum(l)))
 EOF
-for t in ${THREADS:-16 8}; do
-  timeout -k 10 300 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 > "$OUT/dropin_t$t.log" 2>&1
-  rc=$?; echo "dropin t=$t rc=$rc" >> "$OUT/dropin_summary.txt"; [ $rc -eq 0 ] || exit 1
+for cfg in ${DROPIN_CFGS:-16:0 8:0 16:8 16:4 32:8}; do
+  IFS=: read -r t mib <<< "$cfg"
+  timeout -k 10 300 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 $mib > "$OUT/dropin_t${t}_s${mib}.log" 2>&1
+  rc=$?; echo "dropin t=$t stage=$mib rc=$rc" >> "$OUT/dropin_summary.txt"; [ $rc -eq 0 ] || exit 1
 done
+[ -n "${DROPIN_ONLY:-}" ] && exit 0
 timeout -k 10 600 python3 bench.py --workload c1 --steps 300 > "$OUT/bench_c1.log" 2>&1
 rc=$?; echo "bench c1 rc=$rc" >> "$OUT/dropin_summary.txt"; [ $rc -eq 0 ] || exit 1
 exit 0
