@@ -24,7 +24,8 @@ for cfg in $CONFIGS; do
   [ $RC -eq 0 ] || exit 1
 done
 cd /tmp && export TMPDIR=/tmp
-for cfg in ${PMC_CONFIGS:-"cold:0:1 slab:128:1 slab:64:1 cold:0:4"}; do
+PMC_CONFIGS=${PMC_CONFIGS:-"cold:0:1 slab:128:1 slab:192:1 cold:0:4"}
+for cfg in $PMC_CONFIGS; do
   IFS=: read -r mode s g <<< "$cfg"
   name="${mode}_${s}_${g}"
   timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_$name" -o run --pmc FETCH_SIZE -- \
