@@ -42,6 +42,13 @@ for s in $STEPS; do
       T=$(find "$OUT/prof" -name "*kernel_trace.csv" | head -1)
       [ -n "$T" ] && python3 tools/trace_split.py "$T" k_b3_lines 2 320 17179869184 > "$OUT/trace_split.json" 2>&1 ;;
     pmc) step pmc 900 bash tools/gpu_pmc.sh ;;
+    slabpmc) step slabpmc 600 env CONFIGS=" " bash tools/gpu_slab.sh ;;
+    dropsweep) step dropsweep 600 env DROPIN_ONLY=1 bash tools/gpu_dropin.sh ;;
+    configs)
+      step bench_c1_1 600 python bench.py --workload c1 --streams 1 --steps 1500 --no-cpu-baseline &&
+      step bench_c3 600 python bench.py --workload c3 --steps 40 --no-cpu-baseline &&
+      step bench_c4 600 python bench.py --workload c4 --steps 60 --no-cpu-baseline &&
+      step bench_c5 600 python bench.py --workload c5 --steps 3 --no-cpu-baseline ;;
     debug) step debug_check 600 python tools/debug_check.py ;;
     zsdiag)  # diagnostic zstd variants: section timers (BW_ZSTD_TIMING) and the step fences dropped
       step zstd_ztime 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_ztime.so" python tools/zstd_bench.py \
