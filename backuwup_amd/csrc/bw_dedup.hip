@@ -16,10 +16,11 @@
 // 130-148): two distinct digests that share their first 8 bytes, or the whole slot hash, simply
 // occupy two slots.  A slot never changes its digest once claimed, so every word of one slot
 // carries the same tag and atomicMin on the word is atomicMin on the position.
-//   k_append   copy the batch digests to the log tail
-//   k_claim    per digest: probe; an empty slot is CAS'd with this position, a slot whose tag
-//              matches is compared with the log entry it points at (written by an earlier launch,
-//              so visible), equal -> atomicMin, different -> keep probing
+//   k_append_claim  per digest: its log entry, then the probe: an empty slot is CAS'd with this
+//              position, a slot whose tag matches is compared with the digest it names -- from the
+//              batch's own digest array when it names a position of this batch (the log entries of
+//              this launch are not read), from the log otherwise (earlier launches) -- equal ->
+//              atomicMin, different -> keep probing
 //   k_verdict  dup iff the slot holding this digest names an earlier position; the last block
 //              advances the log length.
 #include "bw_device.h"
@@ -71,10 +72,17 @@ __device__ __forceinline__ uint64_t batch_n(const uint64_t* n_dev, uint64_t n_ho
     return n_dev ? *n_dev : n_host;
 }
 
+// The digest at log position w: positions of the running batch (>= base) from its own digest array,
+// earlier ones from the log (written by earlier launches, so visible).
+__device__ __forceinline__ Dig digest_at(uint64_t w, const uint8_t* __restrict__ log, uint64_t base,
+                                         const uint8_t* __restrict__ batch) {
+    return w >= base ? load_dig(batch + (w - base) * 32) : load_dig(log + w * 32);
+}
+
 // Claim log position seq (digest d) into the table: the first occurrence of each distinct digest
-// wins.  Every log entry a slot can point at was written by an earlier launch.
+// wins.
 __device__ __forceinline__ void claim(uint64_t* table, uint64_t cap, const uint8_t* __restrict__ log, const Dig& d,
-                                      uint64_t seq) {
+                                      uint64_t seq, uint64_t base, const uint8_t* __restrict__ batch) {
     const uint64_t mask = cap - 1, h = dig_hash(d), tag = h >> SEQ_BITS;
     const uint64_t mine = (tag << SEQ_BITS) | seq;
     uint64_t s = h & mask;
@@ -85,49 +93,44 @@ __device__ __forceinline__ void claim(uint64_t* table, uint64_t cap, const uint8
             v = atomicCAS(p, (unsigned long long)SLOT_EMPTY, (unsigned long long)mine);
             if (v == SLOT_EMPTY) return;
         }
-        if ((v >> SEQ_BITS) == tag && dig_eq(load_dig(log + (v & SEQ_MASK) * 32), d)) {
+        if ((v >> SEQ_BITS) == tag && dig_eq(digest_at(v & SEQ_MASK, log, base, batch), d)) {
             atomicMin(p, (unsigned long long)mine);
             return;
         }
     }
 }
 
-// The batch's digests to the log tail.
-__global__ void k_append(uint8_t* __restrict__ log, const uint64_t* dstate, const uint8_t* __restrict__ digests,
-                         const uint64_t* n_dev, uint64_t n_host) {
+// The batch's digests to the log tail, each claimed at its position as it is written.
+__global__ void k_append_claim(uint64_t* __restrict__ table, uint64_t cap, uint8_t* __restrict__ log,
+                               const uint64_t* dstate, const uint8_t* __restrict__ digests, const uint64_t* n_dev,
+                               uint64_t n_host) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= batch_n(n_dev, n_host)) return;
-    const uint4* s = (const uint4*)(digests + i * 32);
-    uint4* d = (uint4*)(log + (dstate[D_LOGLEN] + i) * 32);
-    d[0] = s[0];
-    d[1] = s[1];
-}
-
-// Each appended digest claimed at its position (the log entries are all in place).
-__global__ void k_claim(uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
-                        const uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= batch_n(n_dev, n_host)) return;
-    const uint64_t seq = dstate[D_LOGLEN] + i;
-    claim(table, cap, log, load_dig(log + seq * 32), seq);
+    const uint64_t base = dstate[D_LOGLEN], seq = base + i;
+    const Dig d = load_dig(digests + i * 32);
+    uint4* l = (uint4*)(log + seq * 32);
+    l[0] = d.a;
+    l[1] = d.b;
+    claim(table, cap, log, d, seq, base, digests);
 }
 
 // Verdicts of the batch (after every claim); the last block to finish advances the log length,
 // which every block read first (no separate launch).
 __global__ void k_verdict(const uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
-                          uint64_t* dstate, const uint64_t* n_dev, uint64_t n_host, uint8_t* __restrict__ is_dup) {
+                          uint64_t* dstate, const uint8_t* __restrict__ digests, const uint64_t* n_dev, uint64_t n_host,
+                          uint8_t* __restrict__ is_dup) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t n = batch_n(n_dev, n_host);
     const uint64_t base = dstate[D_LOGLEN];
     if (i < n) {
         const uint64_t seq = base + i;
-        const Dig d = load_dig(log + seq * 32);
+        const Dig d = load_dig(digests + i * 32);
         const uint64_t mask = cap - 1, h = dig_hash(d), tag = h >> SEQ_BITS;
         uint64_t s = h & mask, w = SLOT_EMPTY;
         for (uint64_t probes = 0; probes <= mask; probes++, s = (s + 1) & mask) {
             const uint64_t v = table[s];
             if (v == SLOT_EMPTY) break;  // unreachable: this position's own claim is in the table
-            if ((v >> SEQ_BITS) == tag && ((v & SEQ_MASK) == seq || dig_eq(load_dig(log + (v & SEQ_MASK) * 32), d))) {
+            if ((v >> SEQ_BITS) == tag && ((v & SEQ_MASK) == seq || dig_eq(digest_at(v & SEQ_MASK, log, base, digests), d))) {
                 w = v & SEQ_MASK;
                 break;
             }
@@ -159,16 +162,15 @@ void launch_dedup(hipStream_t st, uint64_t* table, uint64_t cap, uint8_t* log, u
                   const uint8_t* digests, const uint64_t* n_dev, uint64_t n_host, uint64_t max_n, uint8_t* is_dup) {
     if (!max_n) return;
     const dim3 g((unsigned)((max_n + 255) / 256)), b(256);
-    hipLaunchKernelGGL(k_append, g, b, 0, st, log, dstate, digests, n_dev, n_host);
-    hipLaunchKernelGGL(k_claim, g, b, 0, st, table, cap, log, dstate, n_dev, n_host);
-    hipLaunchKernelGGL(k_verdict, g, b, 0, st, table, cap, log, dstate, n_dev, n_host, is_dup);
+    hipLaunchKernelGGL(k_append_claim, g, b, 0, st, table, cap, log, dstate, digests, n_dev, n_host);
+    hipLaunchKernelGGL(k_verdict, g, b, 0, st, table, cap, log, dstate, digests, n_dev, n_host, is_dup);
 }
 
 __global__ void k_rehash(uint64_t* __restrict__ table, uint64_t cap, const uint8_t* __restrict__ log,
                          const uint64_t* dstate) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= dstate[D_LOGLEN]) return;
-    claim(table, cap, log, load_dig(log + i * 32), i);
+    claim(table, cap, log, load_dig(log + i * 32), i, ~0ull, nullptr);  // every entry from the log
 }
 
 void launch_rehash(hipStream_t st, uint64_t* table, uint64_t cap, const uint8_t* log, const uint64_t* dstate,
