@@ -1731,6 +1731,9 @@ extern "C" int bw_fastcdc_chunks_hashed(bw_ctx* c, const uint8_t* src, uint64_t 
     const uint64_t off = 0;
     std::vector<bw_blob> tmp(len / std::min<uint64_t>(mk.s0, mk.max) + 2);
     uint64_t n = 0;
+#ifdef BW_KEPT_PAGEABLE  // A/B (round 4): the upload as a pageable hipMemcpy
+    if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
+#else
     {
         // the file comes in through the context's pinned staging ring (memcpy on up to 16 host
         // threads, DMA on the copy stream) rather than a pageable hipMemcpy: the reference's tasks
@@ -1742,6 +1745,7 @@ extern "C" int bw_fastcdc_chunks_hashed(bw_ctx* c, const uint8_t* src, uint64_t 
         if (int rc = submit(c, s, P<uint8_t>(s.input), len, &off, &len, 1, &p)) return rc;
         if (int rc = slot_results(c, s, tmp.data(), tmp.size(), &n)) return rc;
     }
+#endif
     *n_out = n;
     if (n > cap) return BW_ENOSPC;
     Kept k;
