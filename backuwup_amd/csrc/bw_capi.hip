@@ -1731,21 +1731,11 @@ extern "C" int bw_fastcdc_chunks_hashed(bw_ctx* c, const uint8_t* src, uint64_t 
     const uint64_t off = 0;
     std::vector<bw_blob> tmp(len / std::min<uint64_t>(mk.s0, mk.max) + 2);
     uint64_t n = 0;
-#ifdef BW_KEPT_PAGEABLE  // A/B (round 4): the upload as a pageable hipMemcpy
+    // the file goes up as one pageable hipMemcpy, not through the context's pinned staging ring: the
+    // reference's tasks call this from many threads at once (one mmap'd file each), and 16 callers
+    // each fanning their memcpy out over 16 ring threads ran at 35 GB/s on C1 against 47-56 for
+    // the runtime's own pageable copies (profiles/r04/s05_keptab)
     if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
-#else
-    {
-        // the file comes in through the context's pinned staging ring (memcpy on up to 16 host
-        // threads, DMA on the copy stream) rather than a pageable hipMemcpy: the reference's tasks
-        // call this from many threads at once, one mmap'd file each
-        hipSetDevice(c->device);
-        Slot& s = c->sync_slot;
-        s.ticket = 0;
-        if (int rc = stream_in(c, s, src, len)) return rc;
-        if (int rc = submit(c, s, P<uint8_t>(s.input), len, &off, &len, 1, &p)) return rc;
-        if (int rc = slot_results(c, s, tmp.data(), tmp.size(), &n)) return rc;
-    }
-#endif
     *n_out = n;
     if (n > cap) return BW_ENOSPC;
     Kept k;

@@ -44,11 +44,6 @@ for s in $STEPS; do
     pmc) step pmc 900 bash tools/gpu_pmc.sh ;;
     slabpmc) step slabpmc 600 env CONFIGS=" " bash tools/gpu_slab.sh ;;
     dropsweep) step dropsweep 600 env DROPIN_ONLY=1 bash tools/gpu_dropin.sh ;;
-    keptab)  # A/B: the kept-digest drop-in's upload through the pinned ring (product) or pageable hipMemcpy
-      step keptab_corpus 300 env DROPIN_ONLY=1 DROPIN_CFGS=16:0 bash tools/gpu_dropin.sh &&
-      step keptab_pageable 300 env LD_LIBRARY_PATH="$GRAFT_REPO_ROOT/build_ab/keptpg" ./build_ab/dropin_c1 /tmp/c1.bin 16 3 &&
-      step keptab_ring 300 ./build_ab/dropin_c1 /tmp/c1.bin 16 3 &&
-      step keptab_pageable2 300 env LD_LIBRARY_PATH="$GRAFT_REPO_ROOT/build_ab/keptpg" ./build_ab/dropin_c1 /tmp/c1.bin 16 3 ;;
     configs)
       step bench_c1_1 600 python bench.py --workload c1 --streams 1 --steps 1500 --no-cpu-baseline &&
       step bench_c3 600 python bench.py --workload c3 --steps 40 --no-cpu-baseline &&
