@@ -11,6 +11,7 @@
 #   pmc      tools/gpu_pmc.sh (FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json)
 #   debug    tools/debug_check.py (BW_DEBUG + BW_DIAG library)
 #   zstd     tools/zstd_bench.py on 1 GiB and 8 GiB of text (level-3 frames, oracle-checked sample)
+#   zstream  the same 1 GiB batch with 2, 3 and 4 calls in flight
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
@@ -55,6 +56,10 @@ for s in $STEPS; do
         --gib 1 --kind text --reps 1 --check 4 &&
       step zstd_nofence 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zsnofence.so" python tools/zstd_bench.py \
         --gib 1 --kind text --reps 2 --check 16 ;;
+    zstream)  # 1 GiB text batches with 2 / 3 / 4 calls in flight (one context and host thread each)
+      step zstd_if2 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 2 --cpu-sample-mib 16 --inflight 2 &&
+      step zstd_if3 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 2 --cpu-sample-mib 16 --inflight 3 &&
+      step zstd_if4 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 2 --cpu-sample-mib 16 --inflight 4 ;;
     zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
           step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
   esac
