@@ -462,22 +462,23 @@ __device__ void wave_extend(const uint8_t* s, uint32_t a, uint32_t b, uint32_t l
 #define BW_ZS_WMIN 2  // probe window after a match at lane 0 (text: the mean first-match lane is 0.2-0.3)
 #endif
 
-__global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src, ZBlob* __restrict__ blobs,
-                                                 ZBlock* __restrict__ blocks, uint32_t* tables,
-                                                 uint64_t* __restrict__ seqs, const uint32_t* __restrict__ active) {
-    const uint32_t bi = active ? active[blockIdx.x] : blockIdx.x;
+constexpr uint32_t DUP_SLOTS = 128;  // 2 KiB of LDS: up to 8 waves per SIMD (one blob per wave)
+constexpr uint32_t SMALL_W = 8;      // windows of up to this many positions find bucket-mates in registers
+
+// The parse of one blob, with the short table's hash length MLS fixed at compile time (level 3
+// uses 4 or 5, by blob size; a runtime switch cost ~15 instructions a hash, several a step).
+template <uint32_t MLS>
+__device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ blobs, ZBlock* __restrict__ blocks,
+                           uint32_t* tables, uint64_t* __restrict__ seqs, const uint32_t bi, const ZBlob& B,
+                           unsigned long long* s_mL, unsigned long long* s_mS, uint32_t* s_h2, uint32_t* s_h,
+                           uint32_t* s_cu) {
     const uint32_t lane = threadIdx.x;
-    constexpr uint32_t DUP_SLOTS = 128;  // 2 KiB of LDS: up to 8 waves per SIMD (one blob per wave)
-    __shared__ unsigned long long s_mL[DUP_SLOTS], s_mS[DUP_SLOTS];
-    __shared__ uint32_t s_h2[64], s_h[64], s_cu[64];
-    for (uint32_t i = lane; i < DUP_SLOTS; i += 64) { s_mL[i] = 0; s_mS[i] = 0; }
-    __builtin_amdgcn_wave_barrier();
-    const ZBlob B = blobs[bi];
     const uint8_t* s = src + B.src;
     uint32_t* hl = tables + (uint64_t)B.slot * SLOT_WORDS;
     uint32_t* hs = hl + (1u << HL_MAX);
     const uint32_t ib = B.base + 1;  // index of s[0] (libzstd: dictLimit)
-    const uint32_t hlog = B.hlog, clog = B.clog, mls = B.mls, maxD = 1u << B.wlog;
+    const uint32_t hlog = B.hlog, clog = B.clog, maxD = 1u << B.wlog;
+    const uint32_t mls = MLS ? MLS : B.mls;  // MLS 0: any length, switched at run time
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
     // Probe window: a step tests the next W positions of the skip sequence (W <= 64 lanes).  Every
     // probe is a random 4-byte read from a 768 KiB table (a cache line from HBM), and on
@@ -581,6 +582,24 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                 // value, the nearest later one decides whether this lane's table write survives the
                 // step.  The pos + 1 probe sees the long-table writes up to and including its own lane.
                 uint32_t nextL = 64, nextS = 64;
+                if (nvalid <= SMALL_W) {
+                    // a short window (the usual case after a match: W = 2): each valid lane (a
+                    // prefix of the wave) reads the others' keys from their registers, in lane
+                    // order; lanes outside the window keep their empty probes
+                    for (uint32_t i = 0; i < nvalid; i++) {
+                        const uint32_t hi2 = rdlane(h2, i), hi = rdlane(h, i), ci = rdlane(curr, i);
+                        if (!valid) continue;
+                        if (hi2 == h2) {
+                            if (i < lane) mil = ci;
+                            else if (i > lane && nextL == 64) nextL = i;
+                        }
+                        if (hi == h) {
+                            if (i < lane) mis = ci;
+                            else if (i > lane && nextS == 64) nextS = i;
+                        }
+                        if (i <= lane && hi2 == h3) m3 = ci;
+                    }
+                } else {
                 uint64_t mL = 0, mS = 0, m3L = 0;
                 if (valid) {
                     atomicOr(&s_mL[h2 & (DUP_SLOTS - 1)], 1ull << lane);
@@ -618,6 +637,7 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
+                }
                 // round of candidate loads: the evidence of every path at once
                 const bool cL = mil > pli, cS = mis > pli, c3 = m3 > pli;  // (invalid lanes: 0, never > pli)
                 uint64_t xL = 0, x3 = 0;
@@ -750,6 +770,20 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
     if (lane == 0)
         for (int i = 0; i < 8; i++) blobs[bi].tm[i] += tm[i];
 #endif
+}
+
+__global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src, ZBlob* __restrict__ blobs,
+                                                 ZBlock* __restrict__ blocks, uint32_t* tables,
+                                                 uint64_t* __restrict__ seqs, const uint32_t* __restrict__ active) {
+    const uint32_t bi = active ? active[blockIdx.x] : blockIdx.x;
+    __shared__ unsigned long long s_mL[DUP_SLOTS], s_mS[DUP_SLOTS];
+    __shared__ uint32_t s_h2[64], s_h[64], s_cu[64];
+    for (uint32_t i = threadIdx.x; i < DUP_SLOTS; i += 64) { s_mL[i] = 0; s_mS[i] = 0; }
+    __builtin_amdgcn_wave_barrier();
+    const ZBlob B = blobs[bi];
+    if (B.mls == 5) parse_blob<5>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu);
+    else if (B.mls == 4) parse_blob<4>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu);
+    else parse_blob<0>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu);  // (not at level 3)
 }
 
 // ======================================================================= k_zs_stats

@@ -12,6 +12,7 @@
 #   debug    tools/debug_check.py (BW_DEBUG + BW_DIAG library)
 #   zstd     tools/zstd_bench.py on 1 GiB and 8 GiB of text (level-3 frames, oracle-checked sample)
 #   zstream  the same 1 GiB batch with 2, 3 and 4 calls in flight
+#   zspmc    SQ counter passes of the zstd kernels (1 GiB of text)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
@@ -60,6 +61,21 @@ for s in $STEPS; do
       step zstd_if2 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 2 --cpu-sample-mib 16 --inflight 2 &&
       step zstd_if3 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 2 --cpu-sample-mib 16 --inflight 3 &&
       step zstd_if4 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 2 --cpu-sample-mib 16 --inflight 4 ;;
+    zspmc)  # SQ counters of the zstd kernels (1 GiB of text, one timed call), two passes of 8
+      Z="$GRAFT_REPO_ROOT/tools/zstd_bench.py --kind text --gib 1 --reps 1 --cpu-sample-mib 1 --check 0"
+      (cd /tmp && export TMPDIR=/tmp &&
+        step zspmc1 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/zpmc1" -o run --pmc SQ_WAVES SQ_INSTS_VALU \
+          SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- python3 $Z &&
+        step zspmc2 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/zpmc2" -o run --pmc SQ_INSTS_SALU \
+          SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES -- python3 $Z) || exit 1 ;;
+    zsab)  # A/B of the zstd parse: the product library against libbackuwup_amd_zsold.so, alternating
+      ZB="python tools/zstd_bench.py --gib 1 --kind text --reps 2 --cpu-sample-mib 1"
+      ZOLD="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zsold.so"
+      step zstd_tests 600 python -u -m pytest tests/test_zstd.py tests/test_pack.py -m gpu -x -q -p no:cacheprovider \
+        --timeout 300 --timeout-method thread &&
+      step zsab_new1 300 $ZB --check 16 && step zsab_old1 300 env BW_LIB="$ZOLD" $ZB --check 2 &&
+      step zsab_new2 300 $ZB --check 2 && step zsab_old2 300 env BW_LIB="$ZOLD" $ZB --check 2 &&
+      step zsab_new_if3 600 $ZB --check 2 --inflight 3 ;;
     zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
           step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
   esac
