@@ -53,6 +53,7 @@ for s in $STEPS; do
       step bench_c5 600 python bench.py --workload c5 --steps 3 --no-cpu-baseline ;;
     debug) step debug_check 600 python tools/debug_check.py ;;
     zsdiag)  # diagnostic zstd variants: section timers (BW_ZSTD_TIMING) and the step fences dropped
+             # (build first: python backuwup_amd/build.py --ztime; build(variant="zsnofence", defines=("-DBW_ZS_NOFENCE",)))
       step zstd_ztime 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_ztime.so" python tools/zstd_bench.py \
         --gib 1 --kind text --reps 1 --check 4 &&
       step zstd_nofence 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zsnofence.so" python tools/zstd_bench.py \
@@ -68,7 +69,8 @@ for s in $STEPS; do
           SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- python3 $Z &&
         step zspmc2 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/zpmc2" -o run --pmc SQ_INSTS_SALU \
           SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES -- python3 $Z) || exit 1 ;;
-    zsab)  # A/B of the zstd parse: the product library against libbackuwup_amd_zsold.so, alternating
+    zsab)  # A/B of the zstd parse: the product library against libbackuwup_amd_zsold.so (built by hand
+           # from the previous bw_zstd.hip), alternating
       ZB="python tools/zstd_bench.py --gib 1 --kind text --reps 2 --cpu-sample-mib 1"
       ZOLD="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zsold.so"
       step zstd_tests 600 python -u -m pytest tests/test_zstd.py tests/test_pack.py -m gpu -x -q -p no:cacheprovider \
