@@ -44,7 +44,11 @@ namespace zs {
 
 constexpr uint32_t BLOCK = 131072;  // ZSTD_BLOCKSIZE_MAX
 constexpr uint32_t HL_MAX = 17, HS_MAX = 16;
-constexpr uint64_t SLOT_WORDS = (1ull << HL_MAX) + (1ull << HS_MAX);
+// A table entry holds a position AND the bytes the match test compares at it (src is immutable,
+// so they are exactly what a load at that position would return): a probe answers the candidate
+// test by itself, one memory round per step fewer than libzstd's position-only tables.  Long
+// table: 16 B {pos, 0, 8 bytes}; short table: 8 B {pos, 4 bytes}.  2.5 MiB per slot.
+constexpr uint64_t SLOT_WORDS = (1ull << HL_MAX) * 4 + (1ull << HS_MAX) * 2;
 constexpr uint32_t SEC_HDR = 256;  // sequence-section scratch: header bytes, then the bitstream
 constexpr uint32_t HUF_HDR_CAP = 256;  // table descriptions libzstd keeps are < 129 bytes
 constexpr uint32_t MAXLL = 35, MAXML = 52, MAXOFF = 31, DEFAULT_MAXOFF = 28;
@@ -471,17 +475,17 @@ template <uint32_t MLS>
 __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ blobs, ZBlock* __restrict__ blocks,
                            uint32_t* tables, uint64_t* __restrict__ seqs, const uint32_t bi, const ZBlob& B,
                            unsigned long long* s_mL, unsigned long long* s_mS, uint32_t* s_h2, uint32_t* s_h,
-                           uint32_t* s_cu) {
+                           uint32_t* s_cu, unsigned long long* s_v8) {
     const uint32_t lane = threadIdx.x;
     const uint8_t* s = src + B.src;
-    uint32_t* hl = tables + (uint64_t)B.slot * SLOT_WORDS;
-    uint32_t* hs = hl + (1u << HL_MAX);
+    uint4* hl = (uint4*)(tables + (uint64_t)B.slot * SLOT_WORDS);  // {pos, 0, bytes lo, bytes hi}
+    uint2* hs = (uint2*)(tables + (uint64_t)B.slot * SLOT_WORDS + (4u << HL_MAX));  // {pos, 4 bytes}
     const uint32_t ib = B.base + 1;  // index of s[0] (libzstd: dictLimit)
     const uint32_t hlog = B.hlog, clog = B.clog, maxD = 1u << B.wlog;
     const uint32_t mls = MLS ? MLS : B.mls;  // MLS 0: any length, switched at run time
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
     // Probe window: a step tests the next W positions of the skip sequence (W <= 64 lanes).  Every
-    // probe is a random 4-byte read from a 768 KiB table (a cache line from HBM), and on
+    // probe is a random 16-byte read from a 2.5 MiB table (a cache line from HBM), and on
     // compressible data the first match is usually a few positions ahead, so probing all 64
     // positions fetched ~20x the lines the step consumes.  W follows the data: it doubles after a
     // step without a match and shrinks to ~2x the matched lane after one.  Any W is exact (the
@@ -566,10 +570,17 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                 // small-match path -- the long table at pos + 1 (libzstd's search_next_long)
                 const uint32_t h2 = hash_long(v8, hlog), h = hash_small(v8, clog, mls), h3 = hash_long(v8n, hlog);
                 uint32_t mil = 0, mis = 0, m3 = 0;
+                uint64_t xL = 0, x3 = 0;  // the bytes at each candidate, from its table entry
+                uint32_t xS = 0;
                 if (valid) {
-                    mil = hl[h2];
-                    mis = hs[h];
-                    m3 = hl[h3];
+                    const uint4 eL = hl[h2], e3 = hl[h3];
+                    const uint2 eS = hs[h];
+                    mil = eL.x;
+                    xL = (uint64_t)eL.w << 32 | eL.z;
+                    mis = eS.x;
+                    xS = eS.y;
+                    m3 = e3.x;
+                    x3 = (uint64_t)e3.w << 32 | e3.z;
                 }
                 const uint32_t curr = ib + pos;
                 const uint64_t vmask = __ballot(valid);
@@ -588,16 +599,17 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     // order; lanes outside the window keep their empty probes
                     for (uint32_t i = 0; i < nvalid; i++) {
                         const uint32_t hi2 = rdlane(h2, i), hi = rdlane(h, i), ci = rdlane(curr, i);
+                        const uint64_t vi = (uint64_t)rdlane((uint32_t)(v8 >> 32), i) << 32 | rdlane((uint32_t)v8, i);
                         if (!valid) continue;
                         if (hi2 == h2) {
-                            if (i < lane) mil = ci;
+                            if (i < lane) { mil = ci; xL = vi; }
                             else if (i > lane && nextL == 64) nextL = i;
                         }
                         if (hi == h) {
-                            if (i < lane) mis = ci;
+                            if (i < lane) { mis = ci; xS = (uint32_t)vi; }
                             else if (i > lane && nextS == 64) nextS = i;
                         }
-                        if (i <= lane && hi2 == h3) m3 = ci;
+                        if (i <= lane && hi2 == h3) { m3 = ci; x3 = vi; }
                     }
                 } else {
                 uint64_t mL = 0, mS = 0, m3L = 0;
@@ -607,6 +619,7 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     s_h2[lane] = h2;
                     s_h[lane] = h;
                     s_cu[lane] = curr;
+                    s_v8[lane] = v8;
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (valid) { mL = s_mL[h2 & (DUP_SLOTS - 1)]; mS = s_mS[h & (DUP_SLOTS - 1)]; m3L = s_mL[h3 & (DUP_SLOTS - 1)]; }
@@ -617,7 +630,7 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     const uint64_t below = (1ull << lane) - 1, above = ~below & ~(1ull << lane);
                     for (uint64_t c = mL & below; c; c &= ~(1ull << (63 - __builtin_clzll(c)))) {
                         const uint32_t i = 63 - (uint32_t)__builtin_clzll(c);
-                        if (s_h2[i] == h2) { mil = s_cu[i]; break; }
+                        if (s_h2[i] == h2) { mil = s_cu[i]; xL = s_v8[i]; break; }
                     }
                     for (uint64_t c = mL & above; c; c &= c - 1) {
                         const uint32_t i = (uint32_t)__builtin_ctzll(c);
@@ -625,7 +638,7 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     }
                     for (uint64_t c = mS & below; c; c &= ~(1ull << (63 - __builtin_clzll(c)))) {
                         const uint32_t i = 63 - (uint32_t)__builtin_clzll(c);
-                        if (s_h[i] == h) { mis = s_cu[i]; break; }
+                        if (s_h[i] == h) { mis = s_cu[i]; xS = (uint32_t)s_v8[i]; break; }
                     }
                     for (uint64_t c = mS & above; c; c &= c - 1) {
                         const uint32_t i = (uint32_t)__builtin_ctzll(c);
@@ -633,26 +646,21 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     }
                     for (uint64_t c = m3L & (below | (1ull << lane)); c; c &= ~(1ull << (63 - __builtin_clzll(c)))) {
                         const uint32_t i = 63 - (uint32_t)__builtin_clzll(c);
-                        if (s_h2[i] == h3) { m3 = s_cu[i]; break; }
+                        if (s_h2[i] == h3) { m3 = s_cu[i]; x3 = s_v8[i]; break; }
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
                 }
-                // round of candidate loads: the evidence of every path at once
+                // the evidence of every path at once (the candidates' bytes came with the probes)
                 const bool cL = mil > pli, cS = mis > pli, c3 = m3 > pli;  // (invalid lanes: 0, never > pli)
-                uint64_t xL = 0, x3 = 0;
-                uint32_t xS = 0;
-                if (cL) xL = ld64(s + (mil - ib));
-                if (c3) x3 = ld64(s + (m3 - ib));
-                if (cS) xS = ld32(s + (mis - ib));
                 const bool evR = valid && o1 && vrep == (uint32_t)v8n;
                 const bool evL = cL && xL == v8, evS = cS && xS == (uint32_t)v8, ev3 = c3 && x3 == v8n;
                 const uint64_t emask = __ballot(evR || evL || evS);
                 ZT_LAP(0);
                 const uint32_t lastw = emask ? (uint32_t)__builtin_ctzll(emask) : nvalid - 1;
                 if (valid && lane <= lastw) {
-                    if (nextL > lastw) hl[h2] = curr;
-                    if (nextS > lastw) hs[h] = curr;
+                    if (nextL > lastw) hl[h2] = make_uint4(curr, 0u, (uint32_t)v8, (uint32_t)(v8 >> 32));
+                    if (nextS > lastw) hs[h] = make_uint2(curr, (uint32_t)v8);
                 }
                 if (!emask) {
                     const uint32_t pl = rdlane(pos, nvalid - 1);
@@ -682,7 +690,8 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     m = rdlane(mil, e) - ib;
                     known = 8;
                 } else {
-                    if (lane == 0) hl[rdlane(h3, e)] = cu + 1;
+                    const uint32_t n3lo = rdlane((uint32_t)v8n, e), n3hi = rdlane((uint32_t)(v8n >> 32), e);
+                    if (lane == 0) hl[rdlane(h3, e)] = make_uint4(cu + 1, 0u, n3lo, n3hi);
                     if (rdlane(ev3, e)) {
                         m = rdlane(m3, e) - ib;
                         p++;
@@ -725,10 +734,10 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     if (!o2) rB = ~rA;
                     pre = true;
                     if (lane == 0) {
-                        hl[hash_long(a8, hlog)] = iti;
-                        hl[hash_long(b8, hlog)] = ib + p - 2;
-                        hs[hash_small(a8, clog, mls)] = iti;
-                        hs[hash_small(c8, clog, mls)] = ib + p - 1;
+                        hl[hash_long(a8, hlog)] = make_uint4(iti, 0u, (uint32_t)a8, (uint32_t)(a8 >> 32));
+                        hl[hash_long(b8, hlog)] = make_uint4(ib + p - 2, 0u, (uint32_t)b8, (uint32_t)(b8 >> 32));
+                        hs[hash_small(a8, clog, mls)] = make_uint2(iti, (uint32_t)a8);
+                        hs[hash_small(c8, clog, mls)] = make_uint2(ib + p - 1, (uint32_t)c8);
                     }
                     while (o2 > 0 && rA == rB) {
                         const uint32_t rL = wave_count(s, p + 4, p + 4 - o2, iend, lane) + 4;
@@ -737,8 +746,8 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                         o1 = t;
                         const uint64_t v = ld64(s + p);
                         if (lane == 0) {
-                            hs[hash_small(v, clog, mls)] = ib + p;
-                            hl[hash_long(v, hlog)] = ib + p;
+                            hs[hash_small(v, clog, mls)] = make_uint2(ib + p, (uint32_t)v);
+                            hl[hash_long(v, hlog)] = make_uint4(ib + p, 0u, (uint32_t)v, (uint32_t)(v >> 32));
                             sq[nseq] = seq_pack(0, rL - 3, 1);
                         }
                         nseq++;
@@ -778,12 +787,13 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
     const uint32_t bi = active ? active[blockIdx.x] : blockIdx.x;
     __shared__ unsigned long long s_mL[DUP_SLOTS], s_mS[DUP_SLOTS];
     __shared__ uint32_t s_h2[64], s_h[64], s_cu[64];
+    __shared__ unsigned long long s_v8[64];
     for (uint32_t i = threadIdx.x; i < DUP_SLOTS; i += 64) { s_mL[i] = 0; s_mS[i] = 0; }
     __builtin_amdgcn_wave_barrier();
     const ZBlob B = blobs[bi];
-    if (B.mls == 5) parse_blob<5>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu);
-    else if (B.mls == 4) parse_blob<4>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu);
-    else parse_blob<0>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu);  // (not at level 3)
+    if (B.mls == 5) parse_blob<5>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu, s_v8);
+    else if (B.mls == 4) parse_blob<4>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu, s_v8);
+    else parse_blob<0>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu, s_v8);  // (not at level 3)
 }
 
 // ======================================================================= k_zs_stats
@@ -1677,7 +1687,7 @@ struct ZstdWork {
     DBuf blobs, blocks, hist, huf_use, huf_hdr, seqs, lits, sec, tables, active, rerun;
     std::vector<uint32_t> next_base;  // per slot: the index base its next use starts from
     uint32_t n_slots = 0;
-    uint64_t max_slots = 16384;        // hash-table slots (768 KiB each): blobs parsed at once
+    uint64_t max_slots = 16384;        // hash-table slots (2.5 MiB each): blobs parsed at once
     uint64_t max_bytes = 8ull << 30;   // input bytes per sub-batch (scratch ~4.2 x this)
     uint32_t* h_rerun = nullptr;       // pinned
     ~ZstdWork() {

@@ -181,7 +181,7 @@ enum {
                                     2 = aligned 128-byte lines through registers (k_b3_lines, default) */
     BW_OPT_SCAN_WAVES = 6,       /* gear-scan workgroup: 16 waves (default) or 8 (leaves LDS for BLAKE3) */
     BW_OPT_LATENCY_STREAM = 7,   /* 1: the small kernels between the passes on a high-priority stream */
-    BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (768 KiB of hash tables each; 16384) */
+    BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (2.5 MiB of hash tables each; 16384) */
     BW_OPT_ZSTD_BATCH_BYTES = 9, /* bw_zstd_*: input bytes per internal batch (~4.2x in scratch; 8 GiB) */
     BW_OPT_ORDER_HASH = 10,      /* 1: the scans and the BLAKE3 leaf passes of the contexts sharing an
                                     index run one at a time each, in submission order (a batch's scan
