@@ -122,6 +122,7 @@ class Context:
         check(self._L.bw_create(device, ctypes.byref(h)))
         self.h = h
         self.device = device
+        self._zs_n = {}  # zstd ticket -> blob count
 
     def close(self):
         if getattr(self, "h", None):
@@ -275,6 +276,26 @@ class Context:
                                               sl.ctypes.data_as(_lib.u64p), so.size, ctypes.c_void_p(d_dst),
                                               do.ctypes.data_as(_lib.u64p), fl.ctypes.data_as(_lib.u64p)), self.h)
         return fl
+
+    def zstd_submit_device(self, d_src, src_off, src_len, d_dst, dst_off):
+        """bw_zstd_submit_device: the batch starts on a free lane of the context and the call
+        returns its ticket at once (BW_ESTATE: every lane holds a batch); zstd_wait(ticket) blocks
+        for it and returns the frame lengths.  The device buffers stay untouched until then."""
+        so = np.ascontiguousarray(src_off, dtype=np.uint64)
+        sl = np.ascontiguousarray(src_len, dtype=np.uint64)
+        do = np.ascontiguousarray(dst_off, dtype=np.uint64)
+        t = ctypes.c_uint64()
+        check(self._L.bw_zstd_submit_device(self.h, ctypes.c_void_p(d_src), so.ctypes.data_as(_lib.u64p),
+                                            sl.ctypes.data_as(_lib.u64p), so.size, ctypes.c_void_p(d_dst),
+                                            do.ctypes.data_as(_lib.u64p), ctypes.byref(t)), self.h)
+        self._zs_n[t.value] = so.size
+        return t.value
+
+    def zstd_wait(self, ticket):
+        n = self._zs_n.pop(ticket, 0)
+        fl = np.zeros(max(n, 1), dtype=np.uint64)
+        check(self._L.bw_zstd_wait(self.h, ticket, fl.ctypes.data_as(_lib.u64p)), self.h)
+        return fl[:n]
 
     # -------------------------------------------------------------- index
     def index_reset(self, capacity_hint=0):

@@ -22,6 +22,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -178,6 +179,20 @@ struct bw_ctx {
 
     // per-blob zstd level 3 (bw_zstd.hip): hash-table slots and scratch; zs_io = host-call staging
     ZstdWork* zw = nullptr;
+    // asynchronous zstd (bw_zstd_submit_device / bw_zstd_wait): each lane runs one batch on its own
+    // stream and hash tables, driven by a library thread through the batch's host round trips
+    struct ZsLane {
+        hipStream_t st = nullptr;
+        hipEvent_t ready = nullptr;  // the context stream's work before the submit
+        ZstdWork* w = nullptr;
+        std::thread th;
+        uint64_t ticket = 0;  // 0: free
+        std::vector<uint64_t> so, sl, dof, fl;
+        int rc = 0;
+        std::string err;
+    };
+    ZsLane zs_lanes[BW_ZSTD_LANES];
+    uint64_t zs_next = 1;
     DevBuf zs_io;
     // bw_pack_compress_device: level-3 frames staged for bw_pack_build_compressed
     DevBuf pk_stage;
@@ -611,6 +626,13 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
                      &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage,
                      &c->ex_bk, &c->ex_rbk, &c->ex_perm, &c->ex_cnt, &c->ex_v, &c->ex_rv};
+    for (auto& L : c->zs_lanes) {  // batches still in flight finish first
+        if (L.th.joinable()) L.th.join();
+        if (L.st) hipStreamDestroy(L.st);
+        if (L.ready) hipEventDestroy(L.ready);
+        zstd_work_free(L.w);
+        L.w = nullptr;
+    }
     for (DevBuf* b : all) free_dev(*b);
     zstd_work_free(c->zw);
     c->zw = nullptr;
@@ -2152,6 +2174,69 @@ extern "C" int bw_zstd_compress_device(bw_ctx* c, const uint8_t* d_src, const ui
     if (!c || (n && (!d_src || !src_off || !src_len || !d_dst || !dst_off || !frame_len))) return BW_EINVAL;
     hipSetDevice(c->device);
     return zstd_compress(c->stream, c->zw, d_src, src_off, src_len, n, d_dst, dst_off, frame_len, c->err);
+}
+
+extern "C" int bw_zstd_submit_device(bw_ctx* c, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
+                                     uint64_t n, uint8_t* d_dst, const uint64_t* dst_off, uint64_t* ticket) {
+    if (!c || !ticket || (n && (!d_src || !src_off || !src_len || !d_dst || !dst_off))) return BW_EINVAL;
+    *ticket = 0;
+    for (uint64_t i = 0; i < n; i++)
+        if (src_len[i] > 3ull * 1024 * 1024) {
+            c->err = "zstd: blob larger than BLOB_MAX_UNCOMPRESSED_SIZE (3 MiB)";
+            return BW_EINVAL;
+        }
+    bw_ctx::ZsLane* L = nullptr;
+    for (auto& x : c->zs_lanes)
+        if (!x.ticket) {
+            L = &x;
+            break;
+        }
+    if (!L) {
+        c->err = "every zstd lane holds a batch (BW_ZSTD_LANES = " + std::to_string(BW_ZSTD_LANES) +
+                 "): bw_zstd_wait for one first";
+        return BW_ESTATE;
+    }
+    hipSetDevice(c->device);
+    if (!L->st) HIPCHK(c, hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking));
+    if (!L->ready) HIPCHK(c, hipEventCreateWithFlags(&L->ready, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(L->ready, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(L->st, L->ready, 0));
+    zstd_work_copy_limits(L->w, c->zw);  // the context's BW_OPT_ZSTD_* limits
+    L->so.assign(src_off, src_off + n);
+    L->sl.assign(src_len, src_len + n);
+    L->dof.assign(dst_off, dst_off + n);
+    L->fl.assign(n, 0);
+    L->rc = BW_OK;
+    L->err.clear();
+    L->ticket = c->zs_next++;
+    const int dev = c->device;
+    L->th = std::thread([L, dev, d_src, d_dst, n] {
+        hipSetDevice(dev);
+        L->rc = zstd_compress(L->st, L->w, d_src, L->so.data(), L->sl.data(), n, d_dst, L->dof.data(), L->fl.data(),
+                              L->err);
+    });
+    *ticket = L->ticket;
+    return BW_OK;
+}
+
+extern "C" int bw_zstd_wait(bw_ctx* c, uint64_t ticket, uint64_t* frame_len) {
+    if (!c || !ticket) return BW_EINVAL;
+    for (auto& L : c->zs_lanes) {
+        if (L.ticket != ticket) continue;
+        if (L.th.joinable()) L.th.join();
+        L.ticket = 0;
+        if (L.rc) {
+            c->err = L.err;
+            return L.rc;
+        }
+        if (!L.fl.empty()) {
+            if (!frame_len) return BW_EINVAL;
+            memcpy(frame_len, L.fl.data(), L.fl.size() * 8);
+        }
+        return BW_OK;
+    }
+    c->err = "zstd ticket " + std::to_string(ticket) + " is not (or no longer) held by the context";
+    return BW_ESTATE;
 }
 
 extern "C" int bw_zstd_compress(bw_ctx* c, const uint8_t* src, const uint64_t* src_off, const uint64_t* src_len, uint64_t n,

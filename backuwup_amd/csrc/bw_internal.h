@@ -304,6 +304,7 @@ void launch_index_gather(hipStream_t st, const uint8_t* pt, const uint64_t* file
 struct ZstdWork;
 void zstd_work_free(ZstdWork* w);
 void zstd_work_limits(ZstdWork*& w, uint64_t max_slots, uint64_t max_bytes);
+void zstd_work_copy_limits(ZstdWork*& dst, const ZstdWork* src);  // dst created if null
 // frames of n blobs (device buffers, host offset tables); synchronous on st; frame_len is host
 int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
                   uint64_t n, uint8_t* d_dst, const uint64_t* dst_off, uint64_t* frame_len, std::string& err);

@@ -1699,6 +1699,14 @@ struct ZstdWork {
 
 void zstd_work_free(ZstdWork* w) { delete w; }
 
+void zstd_work_copy_limits(ZstdWork*& dst, const ZstdWork* src) {
+    if (!dst) dst = new ZstdWork();
+    if (src) {
+        dst->max_slots = src->max_slots;
+        dst->max_bytes = src->max_bytes;
+    }
+}
+
 void zstd_work_limits(ZstdWork*& w, uint64_t max_slots, uint64_t max_bytes) {
     if (!w) w = new ZstdWork();
     if (max_slots) w->max_slots = max_slots;

@@ -241,6 +241,9 @@ pub mod ffi {
                                        n: u64, d_dst: *mut u8, dst_off: *const u64, frame_len: *mut u64) -> c_int;
         pub fn bw_zstd_compress(ctx: *mut bw_ctx, src: *const u8, src_off: *const u64, src_len: *const u64, n: u64,
                                 dst: *mut u8, dst_off: *const u64, frame_len: *mut u64) -> c_int;
+        pub fn bw_zstd_submit_device(ctx: *mut bw_ctx, d_src: *const u8, src_off: *const u64, src_len: *const u64,
+                                     n: u64, d_dst: *mut u8, dst_off: *const u64, ticket: *mut u64) -> c_int;
+        pub fn bw_zstd_wait(ctx: *mut bw_ctx, ticket: u64, frame_len: *mut u64) -> c_int;
         pub fn bw_pack_compress_device(ctx: *mut bw_ctx, d_src: *const u8, src_off: *const u64, src_len: *const u64,
                                        n: u64, frame_len: *mut u64) -> c_int;
         pub fn bw_pack_build_compressed(ctx: *mut bw_ctx, prk: *const u8, hashes: *const u8, kinds: *const u8,

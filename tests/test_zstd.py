@@ -136,3 +136,47 @@ def test_gpu_zstd_rejects_blob_over_3mib(ctx):
     from backuwup_amd._lib import BwError
     with pytest.raises(BwError):
         ctx.zstd_compress([bytes(3 * 1024 * 1024 + 1)])
+
+
+@pytest.mark.gpu
+def test_gpu_zstd_async_lanes_equal_oracle(oracle):
+    """bw_zstd_submit_device / bw_zstd_wait: BW_ZSTD_LANES batches in flight on one context (each
+    lane its own stream and hash tables, one with small slot limits so its tables are reused),
+    waited out of order; every frame equals the oracle's; a submit with every lane busy and a
+    wait on an unknown ticket are BW_ESTATE."""
+    import torch
+    from backuwup_amd import Context, _lib
+    from backuwup_amd._lib import BwError
+    rng = np.random.default_rng(23)
+    batches = []
+    for b in range(_lib.BW_ZSTD_LANES):
+        blobs = [zstd_corpus.blob(zstd_corpus.KINDS[(b + i) % len(zstd_corpus.KINDS)],
+                                  int(rng.choice([rng.integers(0, 500), rng.integers(500, 200000)])), 3000 + 100 * b + i)
+                 for i in range(40)]
+        lens = np.array([len(x) for x in blobs], dtype=np.uint64)
+        so = np.concatenate([[0], np.cumsum(lens + 16)[:-1]]).astype(np.uint64)
+        host = np.zeros(int(so[-1] + lens[-1]) + 16, dtype=np.uint8)
+        for o, x in zip(so, blobs):
+            host[int(o):int(o) + len(x)] = np.frombuffer(x, np.uint8)
+        cap = np.array([_lib.load().bw_zstd_store_size(int(x)) for x in lens], dtype=np.uint64)
+        do = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.uint64)
+        batches.append((blobs, so, lens, do, torch.from_numpy(host).cuda(),
+                        torch.zeros(int(cap.sum()), dtype=torch.uint8, device="cuda")))
+    with Context(0) as c:
+        c.set_option(_lib.BW_OPT_ZSTD_SLOTS, 5)  # copied to the lanes: internal batches of 5 blobs
+        tickets = [c.zstd_submit_device(src.data_ptr(), so, lens, dst.data_ptr(), do)
+                   for blobs, so, lens, do, src, dst in batches]
+        with pytest.raises(BwError):
+            c.zstd_submit_device(batches[0][4].data_ptr(), batches[0][1], batches[0][2], batches[0][5].data_ptr(),
+                                 batches[0][3])
+        fls = {t: c.zstd_wait(t) for t in reversed(tickets)}
+        with pytest.raises(BwError):
+            c.zstd_wait(tickets[0])
+        again = c.zstd_submit_device(batches[1][4].data_ptr(), batches[1][1], batches[1][2], batches[1][5].data_ptr(),
+                                     batches[1][3])  # a lane is free again
+        fl_again = c.zstd_wait(again)
+    for t, (blobs, so, lens, do, src, dst) in zip(tickets, batches):
+        out = dst.cpu().numpy()
+        frames = [out[int(do[i]):int(do[i] + fls[t][i])].tobytes() for i in range(len(blobs))]
+        _check_frames(oracle, blobs, frames)
+    assert np.array_equal(fl_again, fls[tickets[1]])

@@ -83,6 +83,8 @@ for s in $STEPS; do
       ZOLD="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zsold.so"
       step zsab8_new1 300 $ZB8 && step zsab8_old1 300 env BW_LIB="$ZOLD" $ZB8 &&
       step zsab8_new2 300 $ZB8 && step zsab8_old2 300 env BW_LIB="$ZOLD" $ZB8 ;;
+    zlanes)  # 1 GiB text batches through one context's asynchronous lanes, one host thread
+      step zstd_lanes3 600 python tools/zstd_bench.py --gib 1 --kind text --reps 3 --check 2 --cpu-sample-mib 1 --lanes 3 ;;
     zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
           step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
   esac

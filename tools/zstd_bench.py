@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--check", type=int, default=8, help="frames checked against the oracle")
     ap.add_argument("--slots", type=int, default=None, help="BW_OPT_ZSTD_SLOTS (blobs parsed at once)")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="also time the stream through ONE context's asynchronous lanes (bw_zstd_submit_device / "
+                         "bw_zstd_wait), this many batches in flight (<= BW_ZSTD_LANES), from one host thread")
     ap.add_argument("--inflight", type=int, default=1,
                     help="also time a stream of batches: this many contexts (own stream and table pool), "
                          "one host thread each, compressing the batch back to back")
@@ -105,6 +108,27 @@ def main():
             c.close()
     comp = int(fl.sum())
 
+    lanes = None
+    if args.lanes:
+        from backuwup_amd import _lib
+        k = min(args.lanes, _lib.BW_ZSTD_LANES)
+        ldst = [dst] + [torch.empty_like(dst) for _ in range(k - 1)]
+        for d in ldst:  # warm-up: every lane's tables and scratch allocated
+            ctx.zstd_wait(ctx.zstd_submit_device(data.data_ptr(), src_off, lens, d.data_ptr(), dst_off))
+        calls = k * max(args.reps, 2)
+        torch.cuda.synchronize()
+        pending, same = [], True
+        t0 = time.perf_counter()
+        for i in range(calls):
+            if len(pending) == k:
+                same &= bool(np.array_equal(ctx.zstd_wait(pending.pop(0)), fl))
+            pending.append(ctx.zstd_submit_device(data.data_ptr(), src_off, lens, ldst[i % k].data_ptr(), dst_off))
+        for t in pending:
+            same &= bool(np.array_equal(ctx.zstd_wait(t), fl))
+        wall = time.perf_counter() - t0
+        lanes = {"lanes": k, "calls": calls, "bytes": raw * calls, "ms": round(wall * 1e3, 2),
+                 "GBps": round(raw * calls / wall / 1e9, 2), "frame_lengths_equal": same}
+
     from oracle import oracle
     rng = np.random.default_rng(3)
     ok = True
@@ -132,7 +156,7 @@ def main():
     line = {"what": "per-blob zstd level 3 (pack.rs:58-64) on the GPU", "corpus": args.kind,
             "blobs": int(len(lens)), "raw_bytes": raw, "frame_bytes": comp, "ratio": round(raw / max(comp, 1), 3),
             "ms": round(best * 1e3, 3), "GBps": round(raw / best / 1e9, 2), "reps_ms": [round(x * 1e3, 2) for x in times],
-            "bit_exact_sample": bool(ok), "checked": int(len(picks)), "stream": stream,
+            "bit_exact_sample": bool(ok), "checked": int(len(picks)), "stream": stream, "lanes": lanes,
             "cpu_libzstd": {"version": zstd_ref.lib().ZSTD_versionNumber(), "sample_bytes": sb, "blobs": k,
                             "one_thread_GBps": round(sb / one / 1e9, 3),
                             "threads": args.threads, "all_threads_GBps": round(sb / many / 1e9, 3)}}
