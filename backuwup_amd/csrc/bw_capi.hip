@@ -2191,11 +2191,17 @@ extern "C" int bw_zstd_submit_device(bw_ctx* c, const uint8_t* d_src, const uint
             L = &x;
             break;
         }
-    // lane 0 runs on the context's own stream: HIP maps a process's streams onto 4 hardware queues
-    // (GPU_MAX_HW_QUEUES), and two lanes sharing a queue run one after the other (measured: three
-    // lanes on three new streams beside the context's and the caller's reached 1.64 GB/s on 1 GiB
-    // text batches, three contexts 2.8-2.9)
-    const bool own = L != &c->zs_lanes[0];
+    // Every lane on a stream of its own when the process has hardware queues for them: HIP maps a
+    // process's streams onto GPU_MAX_HW_QUEUES queues (4 by default), and two lanes sharing one run
+    // one after the other.  With the default, lane 0 runs on the context's stream instead, and the
+    // other lanes' submit-time wait on that stream then also covers lane 0's batch.  Measured on
+    // 1 GiB text batches, three lanes: own streams 1.64-1.66 GB/s with 4 queues and 2.91 with 8;
+    // lane 0 on the context's stream 2.29-2.31 either way (profiles/r04/s17_lanesab, s18_lanesq8).
+    static const int hw_queues = [] {
+        const char* q = getenv("GPU_MAX_HW_QUEUES");
+        return q && atoi(q) > 0 ? atoi(q) : 4;
+    }();
+    const bool own = L != &c->zs_lanes[0] || hw_queues >= BW_ZSTD_LANES + 2;  // + the context's, the caller's
     if (!L) {
         c->err = "every zstd lane holds a batch (BW_ZSTD_LANES = " + std::to_string(BW_ZSTD_LANES) +
                  "): bw_zstd_wait for one first";

@@ -460,9 +460,10 @@ int bw_zstd_compress(bw_ctx* ctx, const uint8_t* src, const uint64_t* src_off, c
                      uint8_t* dst, const uint64_t* dst_off, uint64_t* frame_len);
 /* Asynchronous form: one call lasts as long as its largest blob's serial parse, so a packer keeps
  * several batches in flight.  bw_zstd_submit_device copies the offset tables, starts the batch on
- * one of the context's BW_ZSTD_LANES lanes (each its own hash tables; the first runs on the
- * context's stream, the others on streams of their own ordered after the work already on it)
- * and returns at once with *ticket; BW_ESTATE when every
+ * one of the context's BW_ZSTD_LANES lanes (each its own hash tables and a stream of its own,
+ * ordered after the work already on the context's stream; with fewer than BW_ZSTD_LANES + 2
+ * hardware queues per process -- HIP's GPU_MAX_HW_QUEUES, 4 by default -- the first lane runs on
+ * the context's stream instead) and returns at once with *ticket; BW_ESTATE when every
  * lane holds a batch (wait for one first).  d_src and d_dst stay untouched by the caller until
  * bw_zstd_wait(ticket), which blocks for the batch and writes its n frame sizes to frame_len. */
 #define BW_ZSTD_LANES 3

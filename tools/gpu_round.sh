@@ -85,6 +85,9 @@ for s in $STEPS; do
       step zsab8_new2 300 $ZB8 && step zsab8_old2 300 env BW_LIB="$ZOLD" $ZB8 ;;
     zlanes)  # 1 GiB text batches through one context's asynchronous lanes, one host thread
       step zstd_lanes3 600 python tools/zstd_bench.py --gib 1 --kind text --reps 3 --check 2 --cpu-sample-mib 1 --lanes 3 ;;
+    lanesq)  # the zstd lanes from one host thread with HIP's default 4 hardware queues and with 8
+      ZL="python tools/zstd_bench.py --gib 1 --kind text --reps 3 --check 1 --cpu-sample-mib 1 --lanes 3"
+      step lanes_q4 300 $ZL && step lanes_q8 300 env GPU_MAX_HW_QUEUES=8 $ZL ;;
     zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
           step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
   esac
