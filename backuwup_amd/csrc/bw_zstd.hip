@@ -468,18 +468,62 @@ __device__ void wave_extend(const uint8_t* s, uint32_t a, uint32_t b, uint32_t l
 
 constexpr uint32_t DUP_SLOTS = 128;  // 2 KiB of LDS: up to 8 waves per SIMD (one blob per wave)
 constexpr uint32_t SMALL_W = 8;      // windows of up to this many positions find bucket-mates in registers
+constexpr uint32_t ZS_WIDE_MAX_BLOBS = 2048;  // sub-batches of at most this many blobs use wide tables (~2 per SIMD)
+
+// A slot's two tables in one of two layouts (host: zstd_compress picks one per sub-batch):
+//   wide    entries carry the bytes at their position (long 16 B, short 8 B): a probe answers the
+//           match test itself -- one dependent round fewer, for calls of few blobs, where one
+//           wave per SIMD waits out every round;
+//   narrow  libzstd's u32 positions (768 KiB of the slot) and a round of candidate loads -- for
+//           many blobs, where the 3.3x smaller tables keep more of the caches and TLBs.
+template <bool WIDE>
+struct ZTab;
+template <>
+struct ZTab<true> {
+    uint4* hl;
+    uint2* hs;
+    __device__ explicit ZTab(uint32_t* slot) : hl((uint4*)slot), hs((uint2*)(slot + (4u << HL_MAX))) {}
+    __device__ void probe(uint32_t h2, uint32_t h, uint32_t h3, uint32_t& mil, uint64_t& xL, uint32_t& mis,
+                          uint32_t& xS, uint32_t& m3, uint64_t& x3) const {
+        const uint4 eL = hl[h2], e3 = hl[h3];
+        const uint2 eS = hs[h];
+        mil = eL.x;
+        xL = (uint64_t)eL.w << 32 | eL.z;
+        mis = eS.x;
+        xS = eS.y;
+        m3 = e3.x;
+        x3 = (uint64_t)e3.w << 32 | e3.z;
+    }
+    __device__ void put_long(uint32_t k, uint32_t pos, uint64_t v) const {
+        hl[k] = make_uint4(pos, 0u, (uint32_t)v, (uint32_t)(v >> 32));
+    }
+    __device__ void put_short(uint32_t k, uint32_t pos, uint64_t v) const { hs[k] = make_uint2(pos, (uint32_t)v); }
+};
+template <>
+struct ZTab<false> {
+    uint32_t* hl;
+    uint32_t* hs;
+    __device__ explicit ZTab(uint32_t* slot) : hl(slot), hs(slot + (1u << HL_MAX)) {}
+    __device__ void probe(uint32_t h2, uint32_t h, uint32_t h3, uint32_t& mil, uint64_t&, uint32_t& mis, uint32_t&,
+                          uint32_t& m3, uint64_t&) const {
+        mil = hl[h2];
+        mis = hs[h];
+        m3 = hl[h3];
+    }
+    __device__ void put_long(uint32_t k, uint32_t pos, uint64_t) const { hl[k] = pos; }
+    __device__ void put_short(uint32_t k, uint32_t pos, uint64_t) const { hs[k] = pos; }
+};
 
 // The parse of one blob, with the short table's hash length MLS fixed at compile time (level 3
 // uses 4 or 5, by blob size; a runtime switch cost ~15 instructions a hash, several a step).
-template <uint32_t MLS>
+template <uint32_t MLS, bool WIDE>
 __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ blobs, ZBlock* __restrict__ blocks,
                            uint32_t* tables, uint64_t* __restrict__ seqs, const uint32_t bi, const ZBlob& B,
                            unsigned long long* s_mL, unsigned long long* s_mS, uint32_t* s_h2, uint32_t* s_h,
                            uint32_t* s_cu, unsigned long long* s_v8) {
     const uint32_t lane = threadIdx.x;
     const uint8_t* s = src + B.src;
-    uint4* hl = (uint4*)(tables + (uint64_t)B.slot * SLOT_WORDS);  // {pos, 0, bytes lo, bytes hi}
-    uint2* hs = (uint2*)(tables + (uint64_t)B.slot * SLOT_WORDS + (4u << HL_MAX));  // {pos, 4 bytes}
+    const ZTab<WIDE> T(tables + (uint64_t)B.slot * SLOT_WORDS);
     const uint32_t ib = B.base + 1;  // index of s[0] (libzstd: dictLimit)
     const uint32_t hlog = B.hlog, clog = B.clog, maxD = 1u << B.wlog;
     const uint32_t mls = MLS ? MLS : B.mls;  // MLS 0: any length, switched at run time
@@ -570,18 +614,9 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                 // small-match path -- the long table at pos + 1 (libzstd's search_next_long)
                 const uint32_t h2 = hash_long(v8, hlog), h = hash_small(v8, clog, mls), h3 = hash_long(v8n, hlog);
                 uint32_t mil = 0, mis = 0, m3 = 0;
-                uint64_t xL = 0, x3 = 0;  // the bytes at each candidate, from its table entry
+                uint64_t xL = 0, x3 = 0;  // the bytes at each candidate (wide: from its table entry)
                 uint32_t xS = 0;
-                if (valid) {
-                    const uint4 eL = hl[h2], e3 = hl[h3];
-                    const uint2 eS = hs[h];
-                    mil = eL.x;
-                    xL = (uint64_t)eL.w << 32 | eL.z;
-                    mis = eS.x;
-                    xS = eS.y;
-                    m3 = e3.x;
-                    x3 = (uint64_t)e3.w << 32 | e3.z;
-                }
+                if (valid) T.probe(h2, h, h3, mil, xL, mis, xS, m3, x3);
                 const uint32_t curr = ib + pos;
                 const uint64_t vmask = __ballot(valid);
                 const uint32_t nvalid = (uint32_t)__popcll(vmask);
@@ -653,14 +688,19 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                 }
                 // the evidence of every path at once (the candidates' bytes came with the probes)
                 const bool cL = mil > pli, cS = mis > pli, c3 = m3 > pli;  // (invalid lanes: 0, never > pli)
+                if constexpr (!WIDE) {  // narrow tables: a round of candidate loads
+                    if (cL) xL = ld64(s + (mil - ib));
+                    if (c3) x3 = ld64(s + (m3 - ib));
+                    if (cS) xS = ld32(s + (mis - ib));
+                }
                 const bool evR = valid && o1 && vrep == (uint32_t)v8n;
                 const bool evL = cL && xL == v8, evS = cS && xS == (uint32_t)v8, ev3 = c3 && x3 == v8n;
                 const uint64_t emask = __ballot(evR || evL || evS);
                 ZT_LAP(0);
                 const uint32_t lastw = emask ? (uint32_t)__builtin_ctzll(emask) : nvalid - 1;
                 if (valid && lane <= lastw) {
-                    if (nextL > lastw) hl[h2] = make_uint4(curr, 0u, (uint32_t)v8, (uint32_t)(v8 >> 32));
-                    if (nextS > lastw) hs[h] = make_uint2(curr, (uint32_t)v8);
+                    if (nextL > lastw) T.put_long(h2, curr, v8);
+                    if (nextS > lastw) T.put_short(h, curr, v8);
                 }
                 if (!emask) {
                     const uint32_t pl = rdlane(pos, nvalid - 1);
@@ -691,7 +731,7 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     known = 8;
                 } else {
                     const uint32_t n3lo = rdlane((uint32_t)v8n, e), n3hi = rdlane((uint32_t)(v8n >> 32), e);
-                    if (lane == 0) hl[rdlane(h3, e)] = make_uint4(cu + 1, 0u, n3lo, n3hi);
+                    if (lane == 0) T.put_long(rdlane(h3, e), cu + 1, (uint64_t)n3hi << 32 | n3lo);
                     if (rdlane(ev3, e)) {
                         m = rdlane(m3, e) - ib;
                         p++;
@@ -734,10 +774,10 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                     if (!o2) rB = ~rA;
                     pre = true;
                     if (lane == 0) {
-                        hl[hash_long(a8, hlog)] = make_uint4(iti, 0u, (uint32_t)a8, (uint32_t)(a8 >> 32));
-                        hl[hash_long(b8, hlog)] = make_uint4(ib + p - 2, 0u, (uint32_t)b8, (uint32_t)(b8 >> 32));
-                        hs[hash_small(a8, clog, mls)] = make_uint2(iti, (uint32_t)a8);
-                        hs[hash_small(c8, clog, mls)] = make_uint2(ib + p - 1, (uint32_t)c8);
+                        T.put_long(hash_long(a8, hlog), iti, a8);
+                        T.put_long(hash_long(b8, hlog), ib + p - 2, b8);
+                        T.put_short(hash_small(a8, clog, mls), iti, a8);
+                        T.put_short(hash_small(c8, clog, mls), ib + p - 1, c8);
                     }
                     while (o2 > 0 && rA == rB) {
                         const uint32_t rL = wave_count(s, p + 4, p + 4 - o2, iend, lane) + 4;
@@ -746,8 +786,8 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                         o1 = t;
                         const uint64_t v = ld64(s + p);
                         if (lane == 0) {
-                            hs[hash_small(v, clog, mls)] = make_uint2(ib + p, (uint32_t)v);
-                            hl[hash_long(v, hlog)] = make_uint4(ib + p, 0u, (uint32_t)v, (uint32_t)(v >> 32));
+                            T.put_short(hash_small(v, clog, mls), ib + p, v);
+                            T.put_long(hash_long(v, hlog), ib + p, v);
                             sq[nseq] = seq_pack(0, rL - 3, 1);
                         }
                         nseq++;
@@ -783,7 +823,8 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
 
 __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src, ZBlob* __restrict__ blobs,
                                                  ZBlock* __restrict__ blocks, uint32_t* tables,
-                                                 uint64_t* __restrict__ seqs, const uint32_t* __restrict__ active) {
+                                                 uint64_t* __restrict__ seqs, const uint32_t* __restrict__ active,
+                                                 int wide) {
     const uint32_t bi = active ? active[blockIdx.x] : blockIdx.x;
     __shared__ unsigned long long s_mL[DUP_SLOTS], s_mS[DUP_SLOTS];
     __shared__ uint32_t s_h2[64], s_h[64], s_cu[64];
@@ -791,9 +832,17 @@ __global__ __launch_bounds__(64) void k_zs_parse(const uint8_t* __restrict__ src
     for (uint32_t i = threadIdx.x; i < DUP_SLOTS; i += 64) { s_mL[i] = 0; s_mS[i] = 0; }
     __builtin_amdgcn_wave_barrier();
     const ZBlob B = blobs[bi];
-    if (B.mls == 5) parse_blob<5>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu, s_v8);
-    else if (B.mls == 4) parse_blob<4>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu, s_v8);
-    else parse_blob<0>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu, s_v8);  // (not at level 3)
+#define BW_ZS_PARSE(M, W) parse_blob<M, W>(src, blobs, blocks, tables, seqs, bi, B, s_mL, s_mS, s_h2, s_h, s_cu, s_v8)
+    if (wide) {
+        if (B.mls == 5) BW_ZS_PARSE(5, true);
+        else if (B.mls == 4) BW_ZS_PARSE(4, true);
+        else BW_ZS_PARSE(0, true);  // (not at level 3)
+    } else {
+        if (B.mls == 5) BW_ZS_PARSE(5, false);
+        else if (B.mls == 4) BW_ZS_PARSE(4, false);
+        else BW_ZS_PARSE(0, false);
+    }
+#undef BW_ZS_PARSE
 }
 
 // ======================================================================= k_zs_stats
@@ -1686,6 +1735,7 @@ bool dgrow(DBuf& b, size_t bytes, hipStream_t st, std::string& err) {
 struct ZstdWork {
     DBuf blobs, blocks, hist, huf_use, huf_hdr, seqs, lits, sec, tables, active, rerun;
     std::vector<uint32_t> next_base;  // per slot: the index base its next use starts from
+    std::vector<uint8_t> layout;      // per slot: 0 zero-filled, 1 narrow, 2 wide (a switch clears it)
     uint32_t n_slots = 0;
     uint64_t max_slots = 16384;        // hash-table slots (2.5 MiB each): blobs parsed at once
     uint64_t max_bytes = 8ull << 30;   // input bytes per sub-batch (scratch ~4.2 x this)
@@ -1759,7 +1809,12 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
             w->tables = nt;
             w->n_slots = (uint32_t)(nt.cap / (SLOT_WORDS * 4));
             w->next_base.assign(w->n_slots, 0);
+            w->layout.assign(w->n_slots, 0);
         }
+        // wide table entries for sub-batches of few blobs (one wave per SIMD: latency-bound), narrow
+        // ones when the blobs fill the SIMDs several times over (measured: wide +3 % on 836 blobs of
+        // 1 GiB of text, -1..-9 % on 6,808 blobs of 8 GiB; profiles/r04/s10_zsfat, s13_zsab8)
+        const bool wide = nb <= ZS_WIDE_MAX_BLOBS;
         hb.resize(nb);
         hk.clear();
         uint64_t seqCap = 0, litCap = 0, secCap = 0;
@@ -1777,11 +1832,15 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
             // index range of this use, with room for every rerun (one block flips per rerun)
             uint32_t& nbase = w->next_base[j];
             const uint64_t need = (uint64_t)(B.nblocks + 2) * (len + 2);
-            if ((uint64_t)nbase + need >= 0xFFFFFF00ull) {
+            uint8_t& lay = w->layout[j];
+            const uint8_t want = wide ? 2 : 1;
+            if ((uint64_t)nbase + need >= 0xFFFFFF00ull || (lay && lay != want)) {  // (a switch: the other
+                                                                                     // layout's words are no entries)
                 if (hipMemsetAsync(w->tables.p ? (uint8_t*)w->tables.p + (uint64_t)j * SLOT_WORDS * 4 : nullptr, 0,
                                    SLOT_WORDS * 4, st) != hipSuccess) { err = "hipMemsetAsync failed"; return BW_EHIP; }
                 nbase = 0;
             }
+            lay = want;
             B.base = nbase;
             nbase += (uint32_t)need;
             for (uint32_t k = 0; k < B.nblocks; k++) {
@@ -1824,7 +1883,7 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
             hipMemsetAsync(dR, 0, 4, st);
             if (nBlocks) {
                 hipLaunchKernelGGL(k_zs_parse, dim3(nBlobs), dim3(64), 0, st, d_src, dB, dK, (uint32_t*)w->tables.p,
-                                   (uint64_t*)w->seqs.p, blobList);
+                                   (uint64_t*)w->seqs.p, blobList, (int)wide);
                 hipLaunchKernelGGL(k_zs_stats, dim3((uint32_t)nBlocks), dim3(ST_THREADS), 0, st, d_src, dB, dK,
                                    (const uint64_t*)w->seqs.p, (uint8_t*)w->lits.p, (uint8_t*)w->sec.p,
                                    (uint32_t*)w->hist.p, blockList);

@@ -180,3 +180,23 @@ def test_gpu_zstd_async_lanes_equal_oracle(oracle):
         frames = [out[int(do[i]):int(do[i] + fls[t][i])].tobytes() for i in range(len(blobs))]
         _check_frames(oracle, blobs, frames)
     assert np.array_equal(fl_again, fls[tickets[1]])
+
+
+@pytest.mark.gpu
+def test_gpu_zstd_table_layouts_and_switches(oracle):
+    """Sub-batches of more than 2,048 blobs parse with narrow (libzstd u32) tables, smaller ones with
+    wide entries that carry their bytes; a slot that changes layout is cleared first.  One context:
+    narrow, wide, narrow again over the same slots; every frame equals the oracle's."""
+    from backuwup_amd import Context
+    rng = np.random.default_rng(29)
+    many = [zstd_corpus.blob(zstd_corpus.KINDS[i % len(zstd_corpus.KINDS)], int(rng.integers(0, 3000)), 5000 + i)
+            for i in range(2100)]
+    few = [zstd_corpus.blob(zstd_corpus.KINDS[i % len(zstd_corpus.KINDS)], int(rng.integers(1000, 300000)), 9000 + i)
+           for i in range(30)]
+    with Context(0) as c:
+        f_many = c.zstd_compress(many)
+        f_few = c.zstd_compress(few)
+        f_many2 = c.zstd_compress(many[::-1])
+    _check_frames(oracle, many, f_many)
+    _check_frames(oracle, few, f_few)
+    _check_frames(oracle, many[::-1], f_many2)

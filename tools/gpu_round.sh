@@ -78,6 +78,9 @@ for s in $STEPS; do
       step zsab_new1 300 $ZB --check 16 && step zsab_old1 300 env BW_LIB="$ZOLD" $ZB --check 2 &&
       step zsab_new2 300 $ZB --check 2 && step zsab_old2 300 env BW_LIB="$ZOLD" $ZB --check 2 &&
       step zsab_new_if3 600 $ZB --check 2 --inflight 3 ;;
+    zstests)  # the zstd and pack GPU tests alone
+      step zstd_tests 600 python -u -m pytest tests/test_zstd.py tests/test_pack.py -m gpu -x -q -p no:cacheprovider \
+        --timeout 300 --timeout-method thread ;;
     zsab8)  # the same A/B on 8 GiB of text (the throughput case: ~6.8 k blobs, several waves per SIMD)
       ZB8="python tools/zstd_bench.py --gib 8 --kind text --reps 1 --cpu-sample-mib 1 --check 2"
       ZOLD="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_zsold.so"
