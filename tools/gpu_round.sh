@@ -91,6 +91,10 @@ for s in $STEPS; do
     lanesq)  # the zstd lanes from one host thread with HIP's default 4 hardware queues and with 8
       ZL="python tools/zstd_bench.py --gib 1 --kind text --reps 3 --check 1 --cpu-sample-mib 1 --lanes 3"
       step lanes_q4 300 $ZL && step lanes_q8 300 env GPU_MAX_HW_QUEUES=8 $ZL ;;
+    zprof)  # rocprofv3 kernel trace + stats of one 1 GiB text zstd call (and its warm-up)
+      (cd /tmp && export TMPDIR=/tmp && step zprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/zprof" -o run \
+        --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/zstd_bench.py" --gib 1 --kind text --reps 1 --check 1 \
+        --cpu-sample-mib 1) || exit 1 ;;
     zstd) step zstd_text1 600 python tools/zstd_bench.py --gib 1 --kind text --reps 2 --check 16 &&
           step zstd_text8 600 python tools/zstd_bench.py --gib 8 --kind text --reps 1 --check 4 ;;
   esac
