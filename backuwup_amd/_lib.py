@@ -128,6 +128,7 @@ SIGNATURES = [
     ("bw_comm_last_error", ctypes.c_char_p, [vp]),
     ("bw_comm_set_capacity", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("bw_exchange_dedup", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+    ("bw_comm_progress", ctypes.c_int, [vp]),
     ("bw_tree_serialize", ctypes.c_int, [ctypes.POINTER(BwTree), vp, vp, ctypes.c_uint64, u64p]),
     ("bw_tree_blobs", ctypes.c_int, [vp, ctypes.POINTER(BwTree), ctypes.c_uint64, ctypes.c_uint32, vp,
                                      ctypes.POINTER(BwTreeBlob), ctypes.c_uint64, u64p]),
@@ -165,6 +166,8 @@ SIGNATURES = [
                                                 ctypes.c_uint32, vp, ctypes.c_uint64, u64p, u64p]),
     ("bw_fastcdc_release", None, [ctypes.c_uint64]),
     ("bw_blake3_kept_hits", ctypes.c_uint64, []),
+    ("bw_blake3_hash_dropin", ctypes.c_int, [vp, vp, ctypes.c_uint64, u8p]),
+    ("bw_blake3_coalesce_stats", ctypes.c_int, [ctypes.c_int, u64p, u64p]),
     ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
     ("bw_profile_intervals", ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, u64p]),
     ("bw_calibrate_b3", ctypes.c_int, [vp, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),

@@ -21,10 +21,27 @@ def _as_bytes_view(data):
     return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
 
 
+def _immutable(data):
+    """True for memory nobody can rewrite through Python: bytes, and read-only buffers (a
+    memoryview of bytes, an mmap opened with ACCESS_READ).  Only such memory may be answered from
+    the digests a FastCDC drop-in kept (a rewritten bytearray or numpy buffer must be
+    hashed again, never answered from an earlier chunking)."""
+    if isinstance(data, bytes):
+        return True
+    if isinstance(data, np.ndarray):
+        return False  # writeable=False can be a view of memory writable through its base
+    try:
+        return memoryview(data).readonly
+    except TypeError:
+        return False
+
+
 def hash(data, ctx=None):  # noqa: A001 - mirrors blake3::hash
-    """blake3::hash(data) -> 32 bytes (the crate's Hash converted with .into())."""
+    """blake3::hash(data) -> 32 bytes (the crate's Hash converted with .into()).  Calls from many
+    threads at once are coalesced into one launch by the library (bw_blake3_hash)."""
     buf = _as_bytes_view(data)
-    return (ctx or default_context()).blake3(buf)
+    ctx = ctx or default_context()
+    return ctx.blake3_dropin(buf) if _immutable(data) else ctx.blake3(buf)
 
 
 def hash_many(data, offsets, lengths, ctx=None):

@@ -73,7 +73,12 @@ class Comm:
         return cls(h, keep=cb)
 
     def set_capacity(self, cap):
+        """Obsolete (round 5): exchanges size every transfer from their own counts; ignored."""
         check(self._L.bw_comm_set_capacity(self.h, int(cap)))
+
+    def progress(self):
+        """Finish the queued exchanges whose counts have arrived (never waits)."""
+        check(self._L.bw_comm_progress(self.h))
 
     def set_timeout(self, timeout_ms):
         check(self._L.bw_comm_set_timeout(self.h, int(timeout_ms)))

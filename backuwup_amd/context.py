@@ -173,12 +173,22 @@ class Context:
     def fastcdc_release(self, handle):
         self._L.bw_fastcdc_release(handle)
 
-    def blake3_at(self, buf, offset, length):
+    def blake3_at(self, buf, offset, length, kept=False):
         """blake3::hash(&buf[offset..offset+length]) on the caller's own memory (no copy), as the
-        reference hashes each chunk slice of its mmap (dir_packer.rs:262-265, :286)."""
+        reference hashes each chunk slice of its mmap (dir_packer.rs:262-265, :286).  kept=True goes
+        through the drop-in entry (bw_blake3_hash_dropin), which answers a chunk of a live
+        fastcdc_chunks_hashed handle from its kept digest: only for memory that cannot change."""
         assert isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and offset + length <= buf.size
         out = (ctypes.c_uint8 * 32)()
-        check(self._L.bw_blake3_hash(self.h, ctypes.c_void_p(buf.ctypes.data + offset), length, out), self.h)
+        fn = self._L.bw_blake3_hash_dropin if kept else self._L.bw_blake3_hash
+        check(fn(self.h, ctypes.c_void_p(buf.ctypes.data + offset), length, out), self.h)
+        return bytes(out)
+
+    def blake3_dropin(self, data):
+        """bw_blake3_hash_dropin over read-only memory (see blake3_at)."""
+        buf = _as_u8(data)
+        out = (ctypes.c_uint8 * 32)()
+        check(self._L.bw_blake3_hash_dropin(self.h, _ptr(buf), buf.size, out), self.h)
         return bytes(out)
 
     def blake3_many(self, data, offsets, lengths):

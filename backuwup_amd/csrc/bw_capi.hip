@@ -76,6 +76,16 @@ struct Slot {
     // a batch split by BW_OPT_SPLIT: its tail part is ticket tail_ticket of the context's helper,
     // holding files [tail_file0, n_files)
     uint64_t tail_ticket = 0, tail_file0 = 0;
+    // bw_exchange_dedup of this batch: its digests grouped by owner (ex_dig, source positions
+    // ex_perm), the counts message (ex_msg, device) and the counts of every rank (ex_h, pinned:
+    // [0, 2W) mine, [2W, 4W) received); ex_part fires after the partition, ex_ready once ex_h holds
+    // the counts.  ex_state: 0 = none, 1 = queued (waiting for the counts), 2 = enqueued, 3 = failed.
+    DevBuf ex_dig, ex_perm, ex_msg;
+    PinBuf ex_h;
+    hipEvent_t ex_part = nullptr, ex_ready = nullptr;
+    int ex_state = 0, ex_rc = 0;
+    bool ex_now = false;     // the counts arrived synchronously (host transport)
+    uint64_t ex_since = 0;   // when the counts were enqueued (steady clock, ns)
 };
 
 }  // namespace
@@ -115,9 +125,11 @@ struct bw_ctx {
     DevBuf b_gdone;  // per blob: BLAKE3 groups finished (fused upper levels); zero between passes
     DevBuf cv, cv2, data, scratch, ucnt, ubtot;
     DevBuf bk_blk, bk_pack, bk_v;  // multi-GPU exchange buckets (bw_partition_buckets, ...)
-    // bw_exchange_dedup: my buckets and the ones received, their source positions, the counts
-    // (mine, received, and scratch for the capacity agreement), verdicts out and back
-    DevBuf ex_bk, ex_rbk, ex_perm, ex_cnt, ex_v, ex_rv;
+    // bw_exchange_dedup: the digests received (source-major), the owner's verdicts on them, and
+    // the verdicts on this rank's digests that come back; the exchange's transfers, gate and
+    // scatter run on ex_st once its counts arrived (the per-batch parts live in the slot)
+    DevBuf ex_rbk, ex_v, ex_rv;
+    hipStream_t ex_st = nullptr;
 
     // batches in flight: ring of result slots addressed by ticket
     Slot slots[MAX_DEPTH];
@@ -238,6 +250,7 @@ static int ensure(bw_ctx* c, DevBuf& b, size_t bytes) {
     if (b.p) {
         hipStreamSynchronize(c->stream);
         if (c->copy) hipStreamSynchronize(c->copy);
+        if (c->ex_st) hipStreamSynchronize(c->ex_st);
         hipFree(b.p);
         b.p = nullptr;
         b.cap = 0;
@@ -596,6 +609,8 @@ extern "C" int bw_create(int device, bw_ctx** out) {
         if (hipEventCreateWithFlags(&sl.meta_done, EV_ORDER) != hipSuccess ||
             hipEventCreateWithFlags(&sl.input_free, EV_ORDER) != hipSuccess ||
             hipEventCreateWithFlags(&sl.copied, EV_ORDER) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.ex_part, EV_ORDER) != hipSuccess ||
+            hipEventCreateWithFlags(&sl.ex_ready, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
             bw_destroy(c);
             return BW_EHIP;
@@ -616,8 +631,13 @@ extern "C" void bw_destroy(bw_ctx* c) {
                 c->host_ms[2] / c->host_batches, c->host_ms[3] / c->host_batches, c->host_ms[4] / c->host_batches,
                 c->host_ms[5] / c->host_batches);
     hipSetDevice(c->device);
+    for (int k = 0; k <= MAX_DEPTH; k++) {  // exchanges of this context still waiting for their counts
+        Slot& s = k < MAX_DEPTH ? c->slots[k] : c->sync_slot;
+        if (s.ex_state == 1 && s.comm) exchange_progress(s.comm, &s);
+    }
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->copy) hipStreamSynchronize(c->copy);
+    if (c->ex_st) hipStreamSynchronize(c->ex_st);
     DevBuf* all[] = {&c->tile_count, &c->tile_slots, &c->tile_off, &c->tile_btot, &c->cand, &c->ovf, &c->meta,
                      &c->chains, &c->chain_n, &c->chain_cptr, &c->merge, &c->seg_M,
                      &c->seg_cnt, &c->cf_invalid, &c->fb_starts, &c->fb_count, &c->b_start, &c->b_len,
@@ -625,7 +645,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->data, &c->scratch, &c->ucnt, &c->ubtot, &c->seal_items, &c->seal_keys, &c->seal_parts,
                      &c->seal_ok, &c->seal_io, &c->pk_blobs, &c->pk_files, &c->pk_hdr, &c->pk_src, &c->pk_out,
                      &c->ix_io, &c->ix_tab, &c->ix_dig, &c->bk_blk, &c->bk_pack, &c->bk_v, &c->zs_io, &c->pk_stage,
-                     &c->ex_bk, &c->ex_rbk, &c->ex_perm, &c->ex_cnt, &c->ex_v, &c->ex_rv};
+                     &c->ex_rbk, &c->ex_v, &c->ex_rv};
     for (auto& L : c->zs_lanes) {  // batches still in flight finish first
         if (L.th.joinable()) L.th.join();
         if (L.st && &L != &c->zs_lanes[0]) hipStreamDestroy(L.st);
@@ -642,8 +662,14 @@ extern "C" void bw_destroy(bw_ctx* c) {
         free_dev(s.digests);
         free_dev(s.is_dup);
         free_dev(s.input);
+        free_dev(s.ex_dig);
+        free_dev(s.ex_perm);
+        free_dev(s.ex_msg);
         free_host(s.meta);
         free_host(s.res);
+        free_host(s.ex_h);
+        if (s.ex_part) hipEventDestroy(s.ex_part);
+        if (s.ex_ready) hipEventDestroy(s.ex_ready);
         if (s.done) hipEventDestroy(s.done);
         if (s.meta_done) hipEventDestroy(s.meta_done);
         if (s.input_free) hipEventDestroy(s.input_free);
@@ -667,6 +693,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
         if (e) hipEventDestroy(e);
     if (c->hi) hipStreamDestroy(c->hi);
     if (c->copy) hipStreamDestroy(c->copy);
+    if (c->ex_st) hipStreamDestroy(c->ex_st);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
 }
@@ -917,15 +944,16 @@ static int stage_prepare(bw_ctx* c, Slot& s, uint64_t max_blobs, uint64_t* want_
     return BW_OK;
 }
 
-static int stage_results(bw_ctx* c, Slot& s, bool written = false, uint64_t want = 0) {
+static int stage_results(bw_ctx* c, Slot& s, bool written = false, uint64_t want = 0, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     if (!written) {
         if (int rc = stage_prepare(c, s, s.max_blobs, &want, nullptr)) return rc;
         // one copy: the counters and the first `want` records lie back to back on the device (two
         // copies cost the stream a ~12 us gap between them with one batch in flight, profiles/r03)
         HIPCHK(c, hipMemcpyAsync(s.res.p, s.res_dev.p, CTR_BYTES + want * sizeof(bw_blob), hipMemcpyDeviceToHost,
-                                 c->stream));
+                                 st));
     }
-    HIPCHK(c, hipEventRecord(s.done, c->stream));
+    HIPCHK(c, hipEventRecord(s.done, st));
     s.res_n = want;
     return BW_OK;
 }
@@ -1310,6 +1338,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     s.dedup = do_dedup;
     s.hashed = do_hash;
     s.comm = nullptr;
+    s.ex_state = 0;
+    s.ex_rc = 0;
     if (stage)
         if (int r5 = stage_results(c, s, zero_copy, want)) return r5;
     phase(5);
@@ -1318,9 +1348,13 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
 }
 
 // Claim the next slot of the ring (the batch it held, if any, is dropped) and give it a ticket.
+// A dropped batch whose exchange is still queued is finished first, and the new batch's kernels
+// wait for the exchange's transfers, gate and scatter on ex_st (they use the slot's buffers).
 static Slot& claim_slot(bw_ctx* c, uint64_t* ticket) {
     const uint64_t t = c->next_ticket++;
     Slot& s = c->slots[(t - 1) % (uint64_t)c->depth];
+    if (s.ex_state == 1 && s.comm) exchange_progress(s.comm, &s);
+    if (s.ex_state == 2) hipStreamWaitEvent(c->stream, s.done, 0);
     s.ticket = t;
     c->last_ticket = t;
     if (ticket) *ticket = t;
@@ -1507,6 +1541,9 @@ extern "C" int bw_host_unregister(void* p) {
 // Results of the batch in slot s (waits for it).  Repeatable until the ring reuses the slot.
 static int slot_results(bw_ctx* c, Slot& s, bw_blob* out, uint64_t cap, uint64_t* n_out) {
     hipSetDevice(c->device);
+    if (s.ex_state == 1)  // queued exchange: its counts first, then its transfers are enqueued
+        if (int rc = exchange_progress(s.comm, &s)) return rc;
+    if (s.ex_state == 3) return s.ex_rc ? s.ex_rc : BW_ECOMM;
     if (s.comm) {  // an exchange in flight: a failed or stalled peer must not hang the wait
         if (int rc = comm_wait_event(s.comm, s.done, c->err)) return rc;
     } else {
@@ -1678,6 +1715,8 @@ extern "C" int bw_blake3_hash_many(bw_ctx* c, const uint8_t* data, uint64_t data
     return BW_OK;
 }
 
+int bw::ctx_device(const bw_ctx* c) { return c->device; }
+
 uint8_t* bw::message_stage(bw_ctx* c, size_t bytes) {
     hipSetDevice(c->device);
     if (c->msg_stage.cap < bytes) {
@@ -1702,101 +1741,6 @@ int bw::hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const ui
     if (dedup) HIPCHK(c, hipMemcpyAsync(dup, s.is_dup.p, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return dedup ? check_collision(c) : BW_OK;
-}
-
-// ---- kept chunk digests (bw_fastcdc_chunks_hashed): the reference chunks a file and then hashes
-// each chunk slice of it (dir_packer.rs:254-266, :286); the chunking submit hashes them at once and
-// the per-chunk blake3::hash calls find their digest here by (pointer, length).
-namespace {
-struct Kept {
-    const uint8_t* base;
-    uint64_t len;
-    std::vector<uint64_t> off, clen;  // chunk offsets (ascending) and lengths
-    std::vector<uint8_t> dig;         // 32 B per chunk
-};
-std::mutex g_kept_mu;
-std::unordered_map<uint64_t, Kept> g_kept;         // handle -> file
-std::atomic<uint64_t> g_kept_next{1}, g_kept_hits{0};
-
-bool kept_lookup(const uint8_t* data, uint64_t len, uint8_t out[32]) {
-    std::lock_guard<std::mutex> lk(g_kept_mu);
-    for (auto& kv : g_kept) {  // a handful of files are open at once (one per task)
-        const Kept& k = kv.second;
-        if (data < k.base || data >= k.base + k.len) continue;
-        const uint64_t o = (uint64_t)(data - k.base);
-        auto it = std::lower_bound(k.off.begin(), k.off.end(), o);
-        if (it == k.off.end() || *it != o) continue;
-        const size_t i = it - k.off.begin();
-        if (k.clen[i] != len) continue;
-        memcpy(out, k.dig.data() + 32 * i, 32);
-        g_kept_hits++;
-        return true;
-    }
-    return false;
-}
-}  // namespace
-
-extern "C" int bw_fastcdc_chunks_hashed(bw_ctx* c, const uint8_t* src, uint64_t len, uint32_t mn, uint32_t av,
-                                        uint32_t mx, bw_chunk* out, uint64_t cap, uint64_t* n_out, uint64_t* handle) {
-    if (!c || !n_out || !handle || (len && !src)) return BW_EINVAL;
-    *handle = 0;
-    Masks mk;
-    if (int rc = make_masks(mn, av, mx, &mk)) return rc;
-    *n_out = 0;
-    if (len == 0) return BW_OK;
-    bw_params p;
-    p.min_size = mn;
-    p.avg_size = av;
-    p.max_size = mx;
-    p.flags = BW_F_NO_DEDUP;  // chunk + hash; the gate stays the caller's (add_blob)
-    p.small_file_threshold = 0;
-    const uint64_t off = 0;
-    std::vector<bw_blob> tmp(len / std::min<uint64_t>(mk.s0, mk.max) + 2);
-    uint64_t n = 0;
-    // the file goes up as one pageable hipMemcpy, not through the context's pinned staging ring: the
-    // reference's tasks call this from many threads at once (one mmap'd file each), and 16 callers
-    // each fanning their memcpy out over 16 ring threads ran at 35 GB/s on C1 against 47-56 for
-    // the runtime's own pageable copies (profiles/r04/s05_keptab)
-    if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
-    *n_out = n;
-    if (n > cap) return BW_ENOSPC;
-    Kept k;
-    k.base = src;
-    k.len = len;
-    k.off.resize(n);
-    k.clen.resize(n);
-    k.dig.resize(32 * n);
-    for (uint64_t i = 0; i < n; i++) {
-        out[i].hash = tmp[i].gear_hash;
-        out[i].offset = tmp[i].offset;
-        out[i].length = tmp[i].length;
-        k.off[i] = tmp[i].offset;
-        k.clen[i] = tmp[i].length;
-        memcpy(k.dig.data() + 32 * i, tmp[i].digest, 32);
-    }
-    const uint64_t h = g_kept_next++;
-    {
-        std::lock_guard<std::mutex> lk(g_kept_mu);
-        g_kept.emplace(h, std::move(k));
-    }
-    *handle = h;
-    return BW_OK;
-}
-
-extern "C" void bw_fastcdc_release(uint64_t handle) {
-    if (!handle) return;
-    std::lock_guard<std::mutex> lk(g_kept_mu);
-    g_kept.erase(handle);
-}
-
-extern "C" uint64_t bw_blake3_kept_hits(void) { return g_kept_hits.load(); }
-
-extern "C" int bw_blake3_hash(bw_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[32]) {
-    if (!c || !out || (len && !data)) return BW_EINVAL;
-    if (len && kept_lookup(data, len, out)) return BW_OK;
-    const uint64_t off = 0;
-    static const uint8_t empty[16] = {0};
-    return bw_blake3_hash_many(c, len ? data : empty, len, &off, &len, 1, out);
 }
 
 // ------------------------------------------------------------------ multi-GPU helpers
@@ -1880,8 +1824,119 @@ extern "C" int bw_scatter_verdicts(bw_ctx* c, const uint8_t* d_verdict, const ui
     return BW_OK;
 }
 
-// One batch through the digest-prefix exchange (include/backuwup_gpu.h): the steps of
-// backuwup_amd/sharded.py's exchange_dedup, behind one C call, enqueued on the context stream.
+// ---- one batch through the digest-prefix exchange (include/backuwup_gpu.h, bw_exchange_dedup)
+// At the call, on the context stream: the batch's digests grouped by owner (owner sections back to
+// back) with the per-owner counts, then the counts all-to-all on the communicator's control stream.
+// Nothing waits for the peers.  Once the counts are in (exchange_progress, called by every later
+// exchange, by bw_wait of an exchanged batch, by claim_slot and by bw_comm_progress), on the
+// context's exchange stream: the digests to their owners (every transfer exactly its digests), the
+// owner's gate over what it received (source-major = canonical order), the verdicts back, scattered
+// into the batch's is_dup and records.  Exchanges finish in issue order, the same on every rank.
+namespace {
+struct ExPending {
+    bw_ctx* c;
+    Slot* s;
+};
+struct ExQueue {
+    std::mutex mu;
+    std::vector<ExPending> q;  // FIFO (front = index 0)
+};
+
+ExQueue* exq_of(bw_comm* comm, bool create) {
+    void*& p = comm_exq(comm);
+    if (!p && create) p = new ExQueue();
+    return (ExQueue*)p;
+}
+
+// The transfers, gate and scatter of one exchange whose counts arrived (ex_h holds them).
+int exchange_finish(bw_comm* comm, bw_ctx* c, Slot& s) {
+    hipSetDevice(c->device);
+    const uint32_t W = (uint32_t)comm_world(comm);
+    const uint64_t* h = (const uint64_t*)s.ex_h.p;
+    std::vector<uint64_t> scnt(W), rcnt(W);
+    uint64_t n = 0, rtot = 0, pad = 0;
+    for (uint32_t k = 0; k < W; k++) {
+        scnt[k] = h[2 * k];
+        rcnt[k] = h[2 * W + 2 * k];
+        pad = std::max(pad, h[2 * W + 2 * k + 1]);  // every rank's largest section: the same on all ranks
+        n += scnt[k];
+        rtot += rcnt[k];
+    }
+    if (n > s.max_blobs) {
+        c->err = "exchange counts exceed the batch's blob bound (internal error)";
+        return BW_EHIP;
+    }
+    if (!c->ex_st) HIPCHK(c, hipStreamCreateWithFlags(&c->ex_st, hipStreamNonBlocking));
+    hipStream_t st = c->ex_st;
+    int rc = 0;
+    rc |= ensure(c, c->ex_rbk, rtot * 32);
+    rc |= ensure(c, c->ex_v, rtot);
+    rc |= ensure(c, c->ex_rv, n);
+    if (rc) return BW_ENOMEM;
+    HIPCHK(c, hipStreamWaitEvent(st, s.ex_now ? s.ex_part : s.ex_ready, 0));
+    if (int r = comm_all_to_allv(comm, s.ex_dig.p, scnt.data(), c->ex_rbk.p, rcnt.data(), 32, pad, st, c->err))
+        return r;
+    if (rtot)
+        if (int r = dedup_device(c, P<uint8_t>(c->ex_rbk), nullptr, rtot, rtot, P<uint8_t>(c->ex_v), st)) return r;
+    if (int r = comm_all_to_allv(comm, c->ex_v.p, rcnt.data(), c->ex_rv.p, scnt.data(), 1, pad, st, c->err)) return r;
+    launch_owner_scatter(st, P<uint8_t>(c->ex_rv), P<uint64_t>(s.ex_perm), n, P<uint8_t>(s.is_dup), slot_records(s));
+    launch_index_snapshot(st, P<uint64_t>(c->idx->dstate), slot_ctr(s));
+    HIPCHK(c, hipGetLastError());
+    s.dedup = true;  // bw_wait now reports the index's sticky errors for this batch
+    s.mark = c->idx_mark;
+    // the records staged at submit predate the verdicts: stage them again behind the scatter
+    if (int r = stage_results(c, s, false, 0, st)) return r;
+    s.ex_state = 2;
+    return BW_OK;
+}
+}  // namespace
+
+int bw::exchange_progress(bw_comm* comm, const void* until) {
+    ExQueue* q = exq_of(comm, false);
+    if (!q) return BW_OK;
+    const Slot* u = (const Slot*)until;
+    if (u && u->ex_state != 1) u = nullptr;  // not queued (finished, failed or never exchanged)
+    if (until && !u) return ((const Slot*)until)->ex_state == 3 ? ((const Slot*)until)->ex_rc : BW_OK;
+    std::lock_guard<std::mutex> lk(q->mu);
+    while (!q->q.empty()) {
+        ExPending e = q->q.front();
+        hipSetDevice(e.c->device);
+        bool ready = e.s->ex_now;
+        int rc = ready ? BW_OK : comm_poll(comm, e.s->ex_ready, e.s->ex_since, &ready, e.c->err);
+        if (!rc && !ready) {
+            if (!u) return BW_OK;  // nothing more has its counts yet
+            rc = comm_wait_event(comm, e.s->ex_ready, e.c->err);
+        }
+        if (!rc) rc = exchange_finish(comm, e.c, *e.s);
+        if (rc) {  // the ranks no longer agree on what follows: fail every queued exchange
+            const std::string why = e.c->err;
+            for (ExPending& f : q->q) {
+                f.s->ex_state = 3;
+                f.s->ex_rc = comm_failed(comm) ? BW_ECOMM : rc;
+                if (f.c != e.c) f.c->err = "an earlier exchange on the communicator failed: " + why;
+            }
+            q->q.clear();
+            return comm_failed(comm) ? BW_ECOMM : rc;
+        }
+        q->q.erase(q->q.begin());
+        if (u && e.s == u) return BW_OK;
+    }
+    return BW_OK;
+}
+
+void bw::exchange_drain(bw_comm* comm) {
+    ExQueue* q = exq_of(comm, false);
+    if (!q) return;
+    const Slot* last = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        if (!q->q.empty()) last = q->q.back().s;
+    }
+    if (last) exchange_progress(comm, last);
+    delete q;
+    comm_exq(comm) = nullptr;
+}
+
 extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     if (!c || !comm) return BW_EINVAL;
     if (comm_device(comm) != c->device) {
@@ -1893,12 +1948,16 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
         c->err = "ticket " + std::to_string(ticket) + " is not (or no longer) held by the context";
         return BW_ESTATE;
     }
-    if (s->dedup) {
-        c->err = "the batch was gated by the local index already (submit it with BW_F_NO_DEDUP)";
+    if (s->dedup || s->ex_state) {
+        c->err = "the batch was gated already (submit it with BW_F_NO_DEDUP and exchange it once)";
         return BW_ESTATE;
     }
     if (!s->hashed) {  // BW_F_NO_HASH: its digest array holds no digests
         c->err = "the batch was submitted with BW_F_NO_HASH: no digests to exchange";
+        return BW_ESTATE;
+    }
+    if (s->tail_ticket) {
+        c->err = "the batch was split in two parts (BW_OPT_SPLIT): no single digest array";
         return BW_ESTATE;
     }
     if (comm_failed(comm)) {
@@ -1907,38 +1966,37 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     }
     hipSetDevice(c->device);
     const uint32_t W = (uint32_t)comm_world(comm);
-    hipStream_t st = c->stream;
-    if (int rc = ensure(c, c->ex_cnt, 4 * W * 8)) return rc;
-    uint64_t* cnt = P<uint64_t>(c->ex_cnt);  // [0, W): my counts, [W, 2W): received, [2W, 4W): scratch
-    // the bucket capacity: the largest per-batch bound over the ranks so far, agreed on every call
-    // (a later, larger batch on any rank grows it on all of them: ADVICE r3)
-    uint64_t cap = 0;
-    if (int rc = comm_agree_cap(comm, s->max_blobs, &cap, c->err)) return rc;
-    const uint64_t slots = (uint64_t)W * cap;
+    const uint64_t max_n = s->max_blobs;
+    const uint64_t nblk = (max_n + 4095) / 4096;
     int rc = 0;
-    rc |= ensure(c, c->ex_bk, slots * 32);
-    rc |= ensure(c, c->ex_rbk, slots * 32);
-    rc |= ensure(c, c->ex_perm, slots * 8);
-    rc |= ensure(c, c->ex_v, slots);
-    rc |= ensure(c, c->ex_rv, slots);
+    rc |= ensure(c, s->ex_dig, max_n * 32);
+    rc |= ensure(c, s->ex_perm, max_n * 8);
+    rc |= ensure(c, s->ex_msg, 2 * W * 8);
+    rc |= ensure(c, c->bk_blk, (nblk + 1) * W * 8);
     if (rc) return BW_ENOMEM;
-    const uint64_t* d_n = slot_ctr(*s) + C_NBLOBS;
-    if (int r = bw_partition_buckets(c, P<uint8_t>(s->digests), d_n, s->max_blobs, cap, W, P<uint8_t>(c->ex_bk),
-                                     P<uint64_t>(c->ex_perm), cnt))
-        return r;
-    if (int r = comm_all_to_all(comm, cnt, cnt + W, 8, st, c->err)) return r;
-    if (int r = comm_all_to_all(comm, c->ex_bk.p, c->ex_rbk.p, cap * 32, st, c->err)) return r;
-    if (int r = bw_index_check_insert_buckets(c, P<uint8_t>(c->ex_rbk), cnt + W, W, cap, P<uint8_t>(c->ex_v)))
-        return r;
-    if (int r = comm_all_to_all(comm, c->ex_v.p, c->ex_rv.p, cap, st, c->err)) return r;
-    launch_bucket_scatter(st, P<uint8_t>(c->ex_rv), P<uint64_t>(c->ex_perm), cnt, W, cap, P<uint8_t>(s->is_dup),
-                          slot_records(*s));
-    launch_index_snapshot(st, P<uint64_t>(c->idx->dstate), slot_ctr(*s));
+    if (int r = ensure_host(c, s->ex_h, 4 * W * 8)) return r;
+    launch_owner_partition(c->stream, P<uint8_t>(s->digests), slot_ctr(*s) + C_NBLOBS, max_n, W, P<uint8_t>(s->ex_dig),
+                           P<uint64_t>(s->ex_perm), P<uint64_t>(s->ex_msg), P<uint64_t>(c->bk_blk));
     HIPCHK(c, hipGetLastError());
-    s->dedup = true;  // bw_wait now reports the index's sticky errors for this batch
+    HIPCHK(c, hipEventRecord(s->ex_part, c->stream));
     s->comm = comm;
-    s->mark = c->idx_mark;
-    return stage_results(c, *s);  // the records staged at submit predate the verdicts
+    s->ex_since = comm_now_ns();
+    s->ex_rc = 0;
+    bool now = false;
+    if (int r = comm_counts(comm, s->ex_part, P<uint64_t>(s->ex_msg), (uint64_t*)s->ex_h.p, s->ex_ready, &now, c->err)) {
+        s->ex_state = 3;
+        s->ex_rc = r;
+        return r;
+    }
+    s->ex_now = now;
+    s->ex_state = 1;
+    {
+        ExQueue* q = exq_of(comm, true);
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->q.push_back(ExPending{c, s});
+    }
+    // the host transport delivered the counts already: finish now; RCCL: whatever is ready
+    return exchange_progress(comm, now ? s : nullptr);
 }
 
 // ------------------------------------------------------------------ stage timing API

@@ -31,15 +31,14 @@ static_assert(BW_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "the C ABI's id size is 
 
 struct bw_comm {
     int device = 0, rank = 0, world = 1;
-    ncclComm_t nccl = nullptr;            // RCCL transport: the data path (counts, buckets, verdicts)
-    ncclComm_t ctl = nullptr;             // split of `nccl` at the first capacity agreement (none while
-                                          // the capacity is fixed): the per-batch agreement, own stream
+    ncclComm_t nccl = nullptr;            // RCCL transport: the data path (digests out, verdicts back)
+    ncclComm_t ctl = nullptr;             // split of `nccl` at initialisation: the per-exchange counts,
+                                          // on a stream of its own
     hipStream_t ctl_st = nullptr;
-    uint64_t* ctl_buf = nullptr;          // device, 2 x world u64
+    uint64_t* ctl_buf = nullptr;          // device, 2 x world u64: the counts received
     bw_host_all_to_all host_fn = nullptr;  // or the caller's host transport
     void* user = nullptr;
-    uint64_t cap = 0;                      // bucket capacity of the session (0 = not agreed yet)
-    bool cap_fixed = false;                // set by bw_comm_set_capacity: no per-batch agreement
+    void* exq = nullptr;                   // exchanges waiting for their counts (bw_capi.hip)
     uint32_t timeout_ms = BW_COMM_DEFAULT_TIMEOUT_MS;
     bool failed = false;                   // aborted: every call returns BW_ECOMM
     void* pin_send = nullptr;              // host transport: pinned staging, 2 x pin_cap
@@ -110,7 +109,7 @@ int settle(bw_comm* c, ncclComm_t k, ncclResult_t r, const char* what, std::stri
 int bw::comm_rank(const bw_comm* c) { return c->rank; }
 int bw::comm_world(const bw_comm* c) { return c->world; }
 int bw::comm_device(const bw_comm* c) { return c->device; }
-uint64_t& bw::comm_cap(bw_comm* c) { return c->cap; }
+void*& bw::comm_exq(bw_comm* c) { return c->exq; }
 bool bw::comm_failed(const bw_comm* c) { return c->failed; }
 
 // Wait for `ev` (recorded after work that includes this communicator's collectives): polls the
@@ -134,111 +133,149 @@ int bw::comm_wait_event(bw_comm* c, hipEvent_t ev, std::string& err) {
     }
 }
 
-// d_recv[r * bytes ..] = rank r's d_send[my_rank * bytes ..], for every rank r; ordered on st.
-int bw::comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t bytes, hipStream_t st,
-                        std::string& err) {
+// The per-exchange counts (16 bytes per rank, include/backuwup_gpu.h bw_exchange_dedup): d_send[2r, 2r+1]
+// goes to rank r; h[0, 2W) = d_send, h[2W, 4W) = what every rank sent here.  RCCL: on the control
+// communicator and its own stream, after `after` (the partition that wrote d_send), without host
+// synchronization; `ready` is recorded behind the copies into h, and the data-path operations of
+// the exchange are enqueued once it fired (bw_capi.hip, exchange_progress).  The control
+// communicator is a split of the data one, so a later exchange's counts never queue behind an
+// earlier exchange's transfers on the data communicator, which wait for the host.  Host transport:
+// synchronous, *now = true.
+int bw::comm_counts(bw_comm* c, hipEvent_t after, const uint64_t* d_send, uint64_t* h, hipEvent_t ready, bool* now,
+                    std::string& err) {
     if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
-    if (!bytes) return BW_OK;
     const int W = c->world;
+    *now = false;
     if (c->nccl) {
+        hipStream_t st = c->ctl_st;
+        if (hipStreamWaitEvent(st, after, 0) != hipSuccess) return comm_err(c, err, "hipStreamWaitEvent failed");
+        ncclResult_t r = ncclGroupStart();
+        for (int k = 0; k < W && (r == ncclSuccess || r == ncclInProgress); k++) {
+            r = ncclSend(d_send + 2 * k, 16, ncclUint8, k, c->ctl, st);
+            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv(c->ctl_buf + 2 * k, 16, ncclUint8, k, c->ctl, st);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r != ncclSuccess && r != ncclInProgress)
+            return fail(c, err, std::string("counts all-to-all: ") + ncclGetErrorString(r));
+        if (int rc = settle(c, c->ctl, e, "counts all-to-all", err)) return rc;
+        if (hipMemcpyAsync(h, d_send, 2 * W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(h + 2 * W, c->ctl_buf, 2 * W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventRecord(ready, st) != hipSuccess)
+            return comm_err(c, err, "counts staging copy failed");
+        return BW_OK;
+    }
+    if (hipEventSynchronize(after) != hipSuccess ||
+        hipMemcpy(h, d_send, 2 * W * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return comm_err(c, err, "counts staging copy (device to host) failed");
+    if (int rc = c->host_fn(c->user, h, h + 2 * W, 16)) {
+        c->failed = true;
+        return comm_err(c, err, "the host all-to-all returned " + std::to_string(rc) + " (communicator failed)");
+    }
+    *now = true;
+    return BW_OK;
+}
+
+// One non-blocking look at `ev` (recorded behind this communicator's collectives, enqueued at
+// `since_ns` on the steady clock): *ready, or still running within the deadline, or failed.
+int bw::comm_poll(bw_comm* c, hipEvent_t ev, uint64_t since_ns, bool* ready, std::string& err) {
+    *ready = false;
+    if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) {
+        *ready = true;
+        return BW_OK;
+    }
+    if (q != hipErrorNotReady) return fail(c, err, std::string("hipEventQuery: ") + hipGetErrorString(q));
+    if (c->nccl) {
+        const ncclResult_t a = async_state(c);
+        if (a != ncclSuccess && a != ncclInProgress)
+            return fail(c, err, std::string("RCCL async error: ") + ncclGetErrorString(a));
+    }
+    const uint64_t now = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                             Clock::now().time_since_epoch()).count();
+    if (now - since_ns > (uint64_t)c->timeout_ms * 1000000ull)
+        return fail(c, err, "an exchange's counts did not arrive within " + std::to_string(c->timeout_ms) +
+                                " ms (a peer failed or stalled)");
+    return BW_OK;
+}
+
+uint64_t bw::comm_now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+
+// Variable all-to-all: scnt[k] elements of `elem` bytes from d_send (sections back to back in rank
+// order) to rank k, rcnt[k] from rank k into d_recv (likewise).  RCCL: one group of send/recv pairs,
+// a pair with zero elements skipped on both sides (rcnt at the receiver is the sender's scnt).
+// Host transport: equal splits of `pad` elements (>= every section on every rank).  Ordered on st.
+int bw::comm_all_to_allv(bw_comm* c, const void* d_send, const uint64_t* scnt, void* d_recv, const uint64_t* rcnt,
+                         uint64_t elem, uint64_t pad, hipStream_t st, std::string& err) {
+    if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
+    const int W = c->world;
+    uint64_t stot = 0, rtot = 0;
+    for (int k = 0; k < W; k++) {
+        stot += scnt[k];
+        rtot += rcnt[k];
+    }
+    if (c->nccl) {
+        if (!stot && !rtot) return BW_OK;  // per pair, a zero section is skipped on both sides
         if (c->tail_stream && c->tail_stream != st && hipStreamWaitEvent(st, c->tail, 0) != hipSuccess)
             return comm_err(c, err, "hipStreamWaitEvent on the communicator's last collective failed");
         ncclResult_t r = ncclGroupStart();
-        if (r != ncclSuccess) return fail(c, err, std::string("ncclGroupStart: ") + ncclGetErrorString(r));
-        for (int k = 0; k < W && r == ncclSuccess; k++) {
-            r = ncclSend((const uint8_t*)d_send + k * bytes, bytes, ncclUint8, k, c->nccl, st);
-            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv((uint8_t*)d_recv + k * bytes, bytes, ncclUint8, k, c->nccl, st);
-            if (r == ncclInProgress) r = ncclSuccess;
+        uint64_t so = 0, ro = 0;
+        for (int k = 0; k < W && (r == ncclSuccess || r == ncclInProgress); k++) {
+            if (scnt[k]) r = ncclSend((const uint8_t*)d_send + so * elem, scnt[k] * elem, ncclUint8, k, c->nccl, st);
+            if (rcnt[k] && (r == ncclSuccess || r == ncclInProgress))
+                r = ncclRecv((uint8_t*)d_recv + ro * elem, rcnt[k] * elem, ncclUint8, k, c->nccl, st);
+            so += scnt[k];
+            ro += rcnt[k];
         }
         const ncclResult_t e = ncclGroupEnd();
-        if (r != ncclSuccess) return fail(c, err, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+        if (r != ncclSuccess && r != ncclInProgress)
+            return fail(c, err, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
         if (int rc = settle(c, c->nccl, e, "ncclGroupEnd", err)) return rc;
         if (hipEventRecord(c->tail, st) != hipSuccess) return comm_err(c, err, "hipEventRecord failed");
         c->tail_stream = st;
         return BW_OK;
     }
-    // host transport: device -> pinned -> caller -> pinned -> device, synchronous on st
-    const size_t total = (size_t)bytes * W;
-    if (c->pin_cap < total) {
+    // host transport: device -> pinned, padded to `pad` per rank -> caller -> unpadded -> device;
+    // pad is the same on every rank (the largest section anywhere), so all ranks skip together
+    if (!pad) return BW_OK;
+    const size_t slot = (size_t)pad * elem, total = slot * W;
+    const size_t need = 2 * total + (size_t)(stot + rtot) * elem;
+    if (c->pin_cap < need) {
         if (c->pin_send) hipHostFree(c->pin_send);
         c->pin_send = nullptr;
         c->pin_cap = 0;
-        if (hipHostMalloc(&c->pin_send, 2 * total, hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&c->pin_send, need, hipHostMallocDefault) != hipSuccess)
             return comm_err(c, err, "hipHostMalloc of the exchange staging failed");
-        c->pin_cap = total;
+        c->pin_cap = need;
     }
     uint8_t* hs = (uint8_t*)c->pin_send;
     uint8_t* hr = hs + total;
-    if (hipMemcpyAsync(hs, d_send, total, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    uint8_t* flat_s = hr + total;
+    uint8_t* flat_r = flat_s + stot * elem;
+    if ((stot && hipMemcpyAsync(flat_s, d_send, stot * elem, hipMemcpyDeviceToHost, st) != hipSuccess) ||
         hipStreamSynchronize(st) != hipSuccess)
         return comm_err(c, err, "exchange staging copy (device to host) failed");
-    if (int rc = c->host_fn(c->user, hs, hr, bytes)) {
+    memset(hs, 0, total);
+    uint64_t so = 0, ro = 0;
+    for (int k = 0; k < W; k++) {
+        if (scnt[k] > pad) return comm_err(c, err, "exchange section larger than the agreed padding (internal error)");
+        memcpy(hs + k * slot, flat_s + so * elem, scnt[k] * elem);
+        so += scnt[k];
+    }
+    if (int rc = c->host_fn(c->user, hs, hr, slot)) {
         c->failed = true;  // the caller's transport lost a peer: the ranks no longer agree
         return comm_err(c, err, "the host all-to-all returned " + std::to_string(rc) + " (communicator failed)");
     }
-    if (hipMemcpyAsync(d_recv, hr, total, hipMemcpyHostToDevice, st) != hipSuccess ||
+    for (int k = 0; k < W; k++) {
+        if (rcnt[k] > pad) return comm_err(c, err, "exchange section larger than the agreed padding (internal error)");
+        memcpy(flat_r + ro * elem, hr + k * slot, rcnt[k] * elem);
+        ro += rcnt[k];
+    }
+    if ((rtot && hipMemcpyAsync(d_recv, flat_r, rtot * elem, hipMemcpyHostToDevice, st) != hipSuccess) ||
         hipStreamSynchronize(st) != hipSuccess)
         return comm_err(c, err, "exchange staging copy (host to device) failed");
-    return BW_OK;
-}
-
-// max of v over the ranks, now (host-synchronous, deadline-bounded).  RCCL: an all-to-all of
-// world x 8 bytes on the control communicator and its own stream, so it never waits for the
-// batches in flight on the data path; host transport: the caller's function on host buffers.
-int bw::comm_max(bw_comm* c, uint64_t v, uint64_t* out, std::string& err) {
-    if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
-    const int W = c->world;
-    std::vector<uint64_t> h(2 * W, v);
-    if (c->nccl) {
-        if (!c->ctl) {  // first agreement: split the control communicator off (every rank gets here
-                        // at its first exchange with an unfixed capacity, in the same call order)
-            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-            cfg.blocking = 0;
-            const ncclResult_t r1 = ncclCommSplit(c->nccl, 0, c->rank, &c->ctl, &cfg);
-            if (int rc = settle(c, c->ctl ? c->ctl : c->nccl, r1, "ncclCommSplit", err)) return rc;
-        }
-        uint64_t* d = c->ctl_buf;
-        hipStream_t st = c->ctl_st;
-        if (hipMemcpyAsync(d, h.data(), W * 8, hipMemcpyHostToDevice, st) != hipSuccess)
-            return comm_err(c, err, "hipMemcpyAsync failed");
-        ncclResult_t r = ncclGroupStart();
-        for (int k = 0; k < W && (r == ncclSuccess || r == ncclInProgress); k++) {
-            r = ncclSend(d + k, 8, ncclUint8, k, c->ctl, st);
-            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv(d + W + k, 8, ncclUint8, k, c->ctl, st);
-        }
-        const ncclResult_t e = ncclGroupEnd();
-        if (r != ncclSuccess && r != ncclInProgress)
-            return fail(c, err, std::string("capacity agreement: ") + ncclGetErrorString(r));
-        if (int rc = settle(c, c->ctl, e, "capacity agreement", err)) return rc;
-        hipEvent_t ev;
-        if (hipMemcpyAsync(h.data() + W, d + W, W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
-            return comm_err(c, err, "hipMemcpyAsync failed");
-        hipEventRecord(ev, st);
-        const int rc = comm_wait_event(c, ev, err);
-        hipEventDestroy(ev);
-        if (rc) return rc;
-    } else if (int rc = c->host_fn(c->user, h.data(), h.data() + W, 8)) {
-        c->failed = true;
-        return comm_err(c, err, "the host all-to-all returned " + std::to_string(rc) + " (communicator failed)");
-    }
-    uint64_t m = 0;
-    for (int k = 0; k < W; k++) m = std::max(m, h[W + k]);
-    *out = m;
-    return BW_OK;
-}
-
-// The bucket capacity for a batch with max_blobs blobs at most: agreed over the ranks on every
-// exchange (it only grows), unless the caller fixed it.
-int bw::comm_agree_cap(bw_comm* c, uint64_t max_blobs, uint64_t* cap, std::string& err) {
-    if (c->cap_fixed) {
-        *cap = c->cap;
-        return BW_OK;
-    }
-    uint64_t m = 0;
-    if (int rc = comm_max(c, max_blobs, &m, err)) return rc;
-    c->cap = std::max(c->cap, m);
-    *cap = c->cap;
     return BW_OK;
 }
 
@@ -281,6 +318,11 @@ extern "C" int bw_comm_init_timeout(int device, int rank, int world, const uint8
     const ncclResult_t r0 = ncclCommInitRankConfig(&c->nccl, world, u, rank, &cfg);
     if (!c->nccl && r0 == ncclSuccess) return bail(BW_ECOMM);
     if (settle(c, c->nccl, r0, "ncclCommInitRankConfig", err)) return bail(BW_ECOMM);
+    // the control communicator for the per-exchange counts, split off while every rank is here
+    ncclConfig_t cfg2 = NCCL_CONFIG_INITIALIZER;
+    cfg2.blocking = 0;
+    const ncclResult_t r1 = ncclCommSplit(c->nccl, 0, rank, &c->ctl, &cfg2);
+    if (settle(c, c->ctl ? c->ctl : c->nccl, r1, "ncclCommSplit", err)) return bail(BW_ECOMM);
     *out = c;
     return BW_OK;
 }
@@ -306,6 +348,7 @@ extern "C" int bw_comm_init_host(int device, int rank, int world, bw_host_all_to
 extern "C" void bw_comm_destroy(bw_comm* c) {
     if (!c) return;
     hipSetDevice(c->device);
+    bw::exchange_drain(c);  // exchanges still waiting for their counts are finished (or failed) first
     if (!c->failed && c->tail_stream) {
         std::string err;
         bw::comm_wait_event(c, c->tail, err);  // aborts on a missed deadline instead of hanging
@@ -327,11 +370,17 @@ extern "C" void bw_comm_destroy(bw_comm* c) {
     delete c;
 }
 
+// Kept for the ABI (round 4 sized fixed buckets with it): every transfer is now sized exactly from
+// the counts the exchange itself carries, so there is nothing to fix and the value is ignored.
 extern "C" int bw_comm_set_capacity(bw_comm* c, uint64_t cap) {
+    (void)cap;
+    return c ? BW_OK : BW_EINVAL;
+}
+
+extern "C" int bw_comm_progress(bw_comm* c) {
     if (!c) return BW_EINVAL;
-    c->cap = cap;
-    c->cap_fixed = cap != 0;
-    return BW_OK;
+    hipSetDevice(c->device);
+    return bw::exchange_progress(c, nullptr);
 }
 
 extern "C" int bw_comm_set_timeout(bw_comm* c, uint32_t timeout_ms) {

@@ -267,7 +267,9 @@ __device__ __forceinline__ uint64_t block_excl_sum_u64(uint64_t v, uint64_t* s, 
 
 __device__ __forceinline__ uint32_t owner_of(const uint8_t* d, uint32_t shift) { return shift >= 8 ? 0 : d[0] >> shift; }
 
-// Per block: for owner o, each thread's count of its 16 items, block-scanned.  WRITE: place them.
+// Per block: for owner o, each thread's count of its 16 items, block-scanned.  WRITE: place them
+// (bucket o at o * cap, or, with cap == FLAT, at the owner's base that k_owner_top added to blk).
+constexpr uint64_t FLAT = ~0ull;
 template <bool WRITE>
 __global__ __launch_bounds__(BP_THREADS) void k_bucket_pass(const uint8_t* __restrict__ digests, const uint64_t* n_dev,
                                                             uint32_t n_owners, uint32_t shift, uint64_t cap,
@@ -294,11 +296,12 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_pass(const uint8_t* __res
             for (int k = 0; k < BP_ITEMS; k++)
                 if (own[k] == o) {
                     if (pos < cap) {
+                        const uint64_t at = cap == FLAT ? pos : (uint64_t)o * cap + pos;
                         const uint4* a = (const uint4*)(digests + (i0 + k) * 32);
-                        uint4* d = (uint4*)(out + ((uint64_t)o * cap + pos) * 32);
+                        uint4* d = (uint4*)(out + at * 32);
                         d[0] = a[0];
                         d[1] = a[1];
-                        perm[(uint64_t)o * cap + pos] = i0 + k;
+                        perm[at] = i0 + k;
                     }
                     pos++;
                 }
@@ -336,6 +339,69 @@ void launch_bucket_partition(hipStream_t st, const uint8_t* digests, const uint6
     if (nblk)
         hipLaunchKernelGGL(k_bucket_pass<true>, dim3((unsigned)nblk), dim3(BP_THREADS), 0, st, digests, n_dev,
                            n_owners, shift, cap, blk, out, perm);
+}
+
+// ------------------------------------------------------------------ exactly sized owner sections
+// bw_exchange_dedup since round 5: the digests grouped by owner back to back (owner o's section
+// starts at the sum of the counts of the owners before it), so every transfer carries exactly its
+// digests.  One block: per owner the exclusive scan over the count pass's blocks, then the owners'
+// bases added in; msg[2o] = digests for owner o, msg[2o + 1] = the largest of them (every rank
+// learns the global largest section from the counts all-to-all: the host transport pads to it).
+__global__ __launch_bounds__(256) void k_owner_top(uint64_t* __restrict__ blk, uint64_t nblk, uint32_t n_owners,
+                                                   const uint64_t* n_dev, uint64_t* __restrict__ msg) {
+    __shared__ uint64_t s[256];
+    __shared__ uint64_t mx;
+    const uint32_t o = threadIdx.x;
+    const uint64_t used = (*n_dev + BP_CHUNK - 1) / BP_CHUNK;
+    uint64_t run = 0;
+    if (o < n_owners)
+        for (uint64_t b = 0; b < used && b < nblk; b++) {
+            const uint64_t t = blk[b * n_owners + o];
+            blk[b * n_owners + o] = run;
+            run += t;
+        }
+    if (o == 0) mx = 0;
+    __syncthreads();
+    if (o < n_owners) atomicMax((unsigned long long*)&mx, (unsigned long long)run);
+    uint64_t total;
+    const uint64_t base = block_excl_sum_u64<256>(o < n_owners ? run : 0, s, &total);
+    if (o < n_owners) {
+        for (uint64_t b = 0; b < used && b < nblk; b++) blk[b * n_owners + o] += base;
+        msg[2 * o] = run;
+        msg[2 * o + 1] = mx;
+    }
+}
+
+void launch_owner_partition(hipStream_t st, const uint8_t* digests, const uint64_t* n_dev, uint64_t max_n,
+                            uint32_t n_owners, uint8_t* out, uint64_t* perm, uint64_t* msg, uint64_t* blk) {
+    const uint32_t bits = 31 - __builtin_clz(n_owners | 1);
+    const uint32_t shift = 8 - bits;
+    const uint64_t nblk = (max_n + BP_CHUNK - 1) / BP_CHUNK;
+    if (nblk)
+        hipLaunchKernelGGL(k_bucket_pass<false>, dim3((unsigned)nblk), dim3(BP_THREADS), 0, st, digests, n_dev,
+                           n_owners, shift, FLAT, blk, out, perm);
+    hipLaunchKernelGGL(k_owner_top, dim3(1), dim3(256), 0, st, blk, nblk, n_owners, n_dev, msg);
+    if (nblk)
+        hipLaunchKernelGGL(k_bucket_pass<true>, dim3((unsigned)nblk), dim3(BP_THREADS), 0, st, digests, n_dev,
+                           n_owners, shift, FLAT, blk, out, perm);
+}
+
+// Verdicts of my owner sections (partition order) back to blob order, into is_dup and the records.
+__global__ void k_owner_scatter(const uint8_t* __restrict__ verdict, const uint64_t* __restrict__ perm, uint64_t n,
+                                uint8_t* __restrict__ is_dup, uint8_t* __restrict__ packed) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t j = perm[i];
+    const uint8_t v = verdict[i];
+    is_dup[j] = v;
+    if (packed) packed[j * sizeof(bw_blob) + offsetof(bw_blob, is_dup)] = v;
+}
+
+void launch_owner_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, uint64_t n, uint8_t* is_dup,
+                          uint8_t* packed) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_owner_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, verdict, perm, n, is_dup,
+                       packed);
 }
 
 // Owner side: the received buckets (source-major = canonical) packed contiguously, n on device.

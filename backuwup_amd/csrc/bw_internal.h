@@ -196,6 +196,13 @@ void launch_pack(hipStream_t st, uint64_t* ctr, BlobArrays b, const uint64_t* fi
                  const uint8_t* digests, const uint8_t* is_dup, uint8_t* out, uint64_t max_blobs,
                  const uint64_t* dstate, uint8_t* host = nullptr, uint64_t host_n = 0);
 void launch_index_snapshot(hipStream_t st, const uint64_t* dstate, uint64_t* ctr);
+// bw_exchange_dedup: the batch's digests grouped by owner back to back (out, perm: n_max entries),
+// msg[2o] = digests for owner o, msg[2o + 1] = the largest section; blk as for the buckets
+void launch_owner_partition(hipStream_t st, const uint8_t* digests, const uint64_t* n_dev, uint64_t max_n,
+                            uint32_t n_owners, uint8_t* out, uint64_t* perm, uint64_t* msg, uint64_t* blk);
+// is_dup[perm[i]] = verdict[i] (and the records' is_dup byte, packed may be null), i < n
+void launch_owner_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, uint64_t n, uint8_t* is_dup,
+                          uint8_t* packed);
 
 // ------------------------------------------------------------------ sealing (bw_seal.hip)
 // BW_SEAL_MAX_INFO (include/backuwup_gpu.h): HKDF info bytes that fit one HMAC block with 0x01 + padding
@@ -250,6 +257,7 @@ void parallel_ranges(uint64_t n, F fn, uint64_t work = 0) {
 }
 
 // ------------------------------------------------------------------ many small messages (bw_capi.hip)
+int ctx_device(const bw_ctx* c);
 // Pinned host staging owned by the context (valid until the next call that uses it).
 uint8_t* message_stage(bw_ctx* c, size_t bytes);
 // BLAKE3 of n whole messages lying in `staged` (from message_stage) at offs/lens, in one batch;
@@ -262,18 +270,26 @@ int hash_messages(bw_ctx* c, const uint8_t* staged, uint64_t total, const uint64
 int comm_rank(const bw_comm* c);
 int comm_world(const bw_comm* c);
 int comm_device(const bw_comm* c);
-uint64_t& comm_cap(bw_comm* c);
 bool comm_failed(const bw_comm* c);
+void*& comm_exq(bw_comm* c);  // the exchanges waiting for their counts (owned by bw_capi.hip)
+uint64_t comm_now_ns();
 // wait for ev (after work that includes the communicator's collectives) to the communicator's
 // deadline, polling RCCL's async errors; aborts the communicator on error or timeout (BW_ECOMM)
 int comm_wait_event(bw_comm* c, hipEvent_t ev, std::string& err);
-// all-to-all of equal splits: d_recv[r * bytes ..] = rank r's d_send[my_rank * bytes ..]; on st
-int comm_all_to_all(bw_comm* c, const void* d_send, void* d_recv, uint64_t bytes, hipStream_t st, std::string& err);
-// *out = max of v over the ranks (host-synchronous; RCCL: the control communicator on its own stream)
-int comm_max(bw_comm* c, uint64_t v, uint64_t* out, std::string& err);
-// the session's bucket capacity for a batch of at most max_blobs blobs: agreed on every call (grows
-// only), or the value fixed by bw_comm_set_capacity
-int comm_agree_cap(bw_comm* c, uint64_t max_blobs, uint64_t* cap, std::string& err);
+// one non-blocking look at ev (enqueued at since_ns): *ready, or BW_ECOMM past the deadline
+int comm_poll(bw_comm* c, hipEvent_t ev, uint64_t since_ns, bool* ready, std::string& err);
+// the exchange's counts, 16 B per rank: h[0, 2W) = d_send, h[2W, 4W) = received (pinned host);
+// RCCL: asynchronous after `after`, `ready` recorded behind it; host transport: synchronous, *now
+int comm_counts(bw_comm* c, hipEvent_t after, const uint64_t* d_send, uint64_t* h, hipEvent_t ready, bool* now,
+                std::string& err);
+// variable all-to-all of elem-byte elements: scnt[k] to rank k, rcnt[k] from rank k (sections back
+// to back in rank order); the host transport pads every section to `pad` elements.  On st.
+int comm_all_to_allv(bw_comm* c, const void* d_send, const uint64_t* scnt, void* d_recv, const uint64_t* rcnt,
+                     uint64_t elem, uint64_t pad, hipStream_t st, std::string& err);
+// bw_capi.hip: finish the queued exchanges whose counts arrived, in issue order (until = null: those
+// ready now; else every one up to and including the exchange of slot `until`, waiting for them)
+int exchange_progress(bw_comm* c, const void* until);
+void exchange_drain(bw_comm* c);  // every queued exchange, waiting (bw_comm_destroy)
 
 // ------------------------------------------------------------------ packfiles / index files (bw_pack.hip)
 constexpr uint32_t ZSTD_BLOCK = 131072;           // zstd ZSTD_BLOCKSIZE_MAX

@@ -13,7 +13,7 @@ outside the crate's asserted ranges raise ValueError (the crate panics).
 from collections import namedtuple
 
 from ._lib import BW_EINVAL, BwError
-from .blake3 import _as_bytes_view
+from .blake3 import _as_bytes_view, _immutable
 from .context import default_context
 
 MINIMUM_MIN = 64
@@ -40,7 +40,7 @@ class FastCDC:
         self._kept, self._ctx = 0, ctx
         try:
             buf = _as_bytes_view(source)
-            if buf.size and buf.flags.c_contiguous:
+            if buf.size and buf.flags.c_contiguous and _immutable(source):
                 cuts, self._kept = ctx.fastcdc_chunks_hashed(buf, min_size, avg_size, max_size)
                 self._buf = buf  # the kept digests name this memory: keep it alive with them
             else:

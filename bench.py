@@ -132,6 +132,9 @@ def main():
                     help="CPU baseline sample (default: 8 GiB of C2 on one core, ~10 s; up to 16 GiB of files "
                          "on 16 cores for the other workloads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-trees", action="store_true",
+                    help="C4: the CPU baseline also hashes each file's Tree blob (dir_packer.rs:274 -> :320), the "
+                         "reference's second blake3::hash per small file (tools/dropin_c4.cpp's GPU side)")
     ap.add_argument("--cpu-all-cores", action="store_true",
                     help="also time the CPU baseline on os.cpu_count() threads (a whole node that is yours; the "
                          "default measures this GPU's 16-core share and one core, and estimates the node)")
@@ -267,9 +270,9 @@ def main():
     max_blobs = sum(int(x) // (256 << 10) + 2 if int(x) > (1 << 20) else 1 for x in file_len)
     total_batches = args.warmup + args.steps + 4 + (3 if nctx > 1 else 0)
     # the host's bound of the log grows by max_blobs per batch until a result read tightens it
-    # (N > 1: by the N received buckets of cap slots each); a bound past the table's capacity is
+    # (N > 1: by the digests the exchange delivered, about max_blobs); a bound past the table's capacity is
     # tightened by a synchronizing read before it grows, so the session pre-sizes the index
-    index_hint = total_batches * max_blobs * (world if multi else 1) + 1024
+    index_hint = total_batches * max_blobs + 1024
     owner_bits = world.bit_length() - 1
     assert world == 1 << owner_bits, "world size must be a power of two (digest-prefix owners)"
 
@@ -281,7 +284,6 @@ def main():
         torch.cuda.synchronize()
 
     step_no = [0]
-    cap_fixed = [False]
     data_ptr = data.data_ptr()
     host_ptr = host.data_ptr() if host is not None else None
     file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
@@ -293,8 +295,8 @@ def main():
     comm = None
     if multi:
         # the digest exchange through the C ABI (bw_comm_init + bw_exchange_dedup): RCCL over
-        # xGMI, enqueued on the batch's stream behind its kernels, no host round trip; rank 0
-        # draws the RCCL id and the process group hands it to the others
+        # xGMI, every transfer sized from the exchange's own counts, no host wait for the peers;
+        # rank 0 draws the RCCL id and the process group hands it to the others
         from backuwup_amd.comm import Comm, unique_id
         uid = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -337,10 +339,9 @@ def main():
         t = submit(c)
         host_ms[0] += (time.perf_counter() - th) * 1e3
         if multi:
-            if not cap_fixed[0]:  # every batch has the same bound: fix the bucket capacity once (no
-                cap_fixed[0] = True  # per-batch agreement on the control communicator)
-                comm.set_capacity(c.batch_views(t)[3])
-            c.exchange_dedup(comm, t)  # owner = digest[0] >> (8 - log2 N); verdicts back into the batch
+            # owner = digest[0] >> (8 - log2 N): the counts go out now, the digests and verdicts once
+            # they arrived (the next exchange or the wait notices); the host never waits for a peer here
+            c.exchange_dedup(comm, t)
         inflight.append((c, t))
         if len(inflight) >= len(ctxs):  # one batch per context in flight: read the oldest while the rest run
             c0, t0 = inflight.pop(0)
@@ -719,6 +720,29 @@ def cpu_baseline(args, data, file_off, file_len, reps=5):
             mA, tA, bA = timed(host, fo[:kA], fl[:kA], threads)
             sample = ("first %d files (%.2f GB, %d blobs) on 16 cores, one file per task; first %d files "
                       "(%.2f GB) on one core" % (kA, mA / 1e9, bA, k1, m1 / 1e9))
+            if getattr(args, "cpu_trees", False):
+                # each file's Tree { File, "file_NNNNNNN.bin", Some(size), Some(mtime), Some(ctime),
+                # [hash], None } in bincode (96 bytes, tools/dropin_c4.cpp's layout), hashed as one
+                # blob per file on the same threads: the reference's second blake3::hash per file
+                def trees(k):
+                    t = np.zeros((k, 96), dtype=np.uint8)
+                    t[:, 4] = 16  # name length (u64 LE)
+                    names = np.frombuffer(b"".join(b"file_%07d.bin" % i for i in range(k)), np.uint8).reshape(k, 16)
+                    t[:, 12:28] = names
+                    for j, v in enumerate((fl[:k], 1700000000 + np.arange(k), 1700000000 + np.arange(k) // 2)):
+                        t[:, 28 + 9 * j] = 1
+                        t[:, 29 + 9 * j:37 + 9 * j] = np.asarray(v, np.uint64)[:, None].view(np.uint8)
+                    t[:, 55] = 1  # one child; its 32 digest bytes follow at 63, next_sibling None at 95
+                    return t.reshape(-1)
+                for k, one_core in ((kA, False), (k1, True)):
+                    tb = trees(k)
+                    offs = np.arange(k, dtype=np.uint64) * np.uint64(96)
+                    mt, tt, _ = timed(tb, offs, np.full(k, 96, np.uint64), 1 if one_core else threads)
+                    if one_core:
+                        t1 += tt
+                    else:
+                        tA += tt
+                sample += "; plus each file's 96-byte Tree blob hashed (the per-file tree hash, dir_packer.rs:320)"
             if args.cpu_all_cores:
                 mN, tN, _ = timed(host, fo[:kA], fl[:kA], nproc)
     finally:

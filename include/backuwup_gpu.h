@@ -117,10 +117,12 @@ int bw_fastcdc_chunks(bw_ctx* ctx, const uint8_t* src, uint64_t len, uint32_t mi
 /* The reference's per-file call pattern (dir_packer.rs:254-266 then :286 per chunk) without a second
  * trip per chunk: FastCDC::new(src, min, avg, max).collect() as bw_fastcdc_chunks, with every
  * chunk's BLAKE3 digest computed in the same submit and kept under *handle until
- * bw_fastcdc_release(handle).  Until then bw_blake3_hash of exactly one of these chunks (pointer
- * src + offset, that length; any context, any thread) returns the kept digest without touching
- * the GPU.  The caller keeps src unchanged until the release: the Rust drop-in's FastCDC borrows
- * the mmap for its lifetime and releases in Drop (rust/backuwup-gpu). */
+ * bw_fastcdc_release(handle).  Until then bw_blake3_hash_dropin of exactly one of these chunks
+ * (pointer src + offset, that length; any context, any thread) returns the kept digest without
+ * touching the GPU.  The caller keeps src unchanged until the release: the Rust drop-in's FastCDC
+ * borrows the mmap immutably for its lifetime and releases in Drop (rust/backuwup-gpu,
+ * INTEGRATION.md).  The registry of live handles is an ordered interval map under a reader lock
+ * with a per-thread cache, so lookups from many threads neither serialize nor scan every handle. */
 int bw_fastcdc_chunks_hashed(bw_ctx* ctx, const uint8_t* src, uint64_t len, uint32_t min_size,
                              uint32_t avg_size, uint32_t max_size, bw_chunk* out, uint64_t cap,
                              uint64_t* n_out, uint64_t* handle);
@@ -128,8 +130,20 @@ void bw_fastcdc_release(uint64_t handle);
 /* digests answered from kept chunk digests since the process started (diagnostic) */
 uint64_t bw_blake3_kept_hits(void);
 
-/* blake3::hash(data) -> 32 bytes, host buffer. */
+/* blake3::hash(data) -> 32 bytes, host buffer; always hashes the bytes given.  Messages up to
+ * BW_COALESCE_MAX_MSG from concurrent callers (any contexts, any threads) are coalesced: each caller
+ * copies its message into the open batch's pinned staging and one launch hashes the batch (one
+ * batch in flight per device; the next fills meanwhile), so N threads calling at once cost one round
+ * trip, not N.  For such messages the context is only read for its device, so any number of threads
+ * may pass the same context; larger messages run on the context itself (one thread at a time). */
+#define BW_COALESCE_MAX_MSG 4194304u
 int bw_blake3_hash(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
+/* The Rust blake3::hash drop-in's entry (dir_packer.rs:286, :320, :353): as bw_blake3_hash, except
+ * that a chunk slice of a live bw_fastcdc_chunks_hashed source is answered from its kept digest.
+ * Only for callers that guarantee those bytes are unchanged while the handle lives. */
+int bw_blake3_hash_dropin(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
+/* coalesced launches and the messages they carried on `device` since the process started */
+int bw_blake3_coalesce_stats(int device, uint64_t* batches, uint64_t* messages);
 /* n independent messages data[offsets[i] .. offsets[i]+lengths[i]) -> out[32*i..] */
 int bw_blake3_hash_many(bw_ctx* ctx, const uint8_t* data, uint64_t data_len,
                         const uint64_t* offsets, const uint64_t* lengths, uint64_t n,
@@ -271,13 +285,13 @@ int bw_index_check_insert_device(bw_ctx* ctx, const uint8_t* d_digests, uint64_t
 int bw_scatter_verdicts(bw_ctx* ctx, const uint8_t* d_verdict, const uint64_t* d_perm,
                         uint64_t n, uint8_t* d_is_dup);
 
-/* Exchange without host round trips (what the multi-GPU path uses per batch).  Every rank sends
- * every owner a bucket of `cap` digest slots, so the all-to-alls have equal splits and the counts
- * stay on the device; cap is agreed once per session (>= the largest batch's max_blobs makes
- * overflow impossible; a smaller cap that a batch exceeds sets a sticky error that
- * bw_index_check reports as BW_ENOSPC).
+/* Building blocks of a fixed-capacity exchange (round 3; bw_exchange_dedup below no longer uses
+ * them): every rank sends every owner a bucket of `cap` digest slots, so the all-to-alls have equal
+ * splits and the counts stay on the device; a batch with more digests for one owner than cap sets
+ * a sticky error that bw_index_check reports as BW_ENOSPC.
  * Device views of batch `ticket` (0 = the most recent), no synchronization: d_n_blobs points at
- * the batch's blob count in HBM; *max_blobs = its host-side upper bound. */
+ * the batch's blob count in HBM; *max_blobs = its host-side upper bound.  The verdicts of an
+ * exchanged batch are final once bw_wait(ticket) returned. */
 int bw_batch_views(bw_ctx* ctx, uint64_t ticket, const uint64_t** d_n_blobs, const uint8_t** d_digests,
                    uint8_t** d_is_dup, uint64_t* max_blobs);
 /* d_buckets[n_owners][cap][32] = digests by owner, canonical order inside each bucket;
@@ -299,21 +313,22 @@ int bw_scatter_buckets(bw_ctx* ctx, const uint8_t* d_verdicts, const uint64_t* d
  * keeps its shard in its own context's index (or a bw_index its contexts share), submits its
  * batches with BW_F_NO_DEDUP, and then calls bw_exchange_dedup once per batch, in the same batch
  * order on every rank.  Files are sharded rank-major (rank r's batch k holds canonical files
- * before rank r+1's batch k), so the owner gates the received buckets in canonical order.
- * A communicator moves bytes between the ranks with an all-to-all of equal splits, either
+ * before rank r+1's batch k), so the owner gates the received digests in canonical order.
+ * A communicator moves bytes between the ranks, either
  *   - over RCCL: rank 0 draws an id with bw_comm_unique_id, the caller hands those 128 bytes to
  *     every rank (any channel), and each rank calls bw_comm_init (blocks until all joined); or
  *   - through the caller's own host transport (bw_comm_init_host): fn(user, send, recv, bytes)
- *     must deliver send[r * bytes ..] to rank r's recv[my_rank * bytes ..] for every rank r;
- *     buffers are pinned host memory, world * bytes long; nonzero return = failure. */
+ *     must deliver send[r * bytes ..] to rank r's recv[my_rank * bytes ..] for every rank r
+ *     (equal splits: the library pads every rank's sections to the largest one); buffers are
+ *     pinned host memory, world * bytes long; nonzero return = failure. */
 #define BW_COMM_ID_BYTES 128u
 typedef struct bw_comm bw_comm;
 typedef int (*bw_host_all_to_all)(void* user, const void* send, void* recv, uint64_t bytes_per_rank);
 int bw_comm_unique_id(uint8_t id[BW_COMM_ID_BYTES]);
 /* world: a power of two <= 256; device must be the device of the contexts it serves.
  * Every wait on the peers has a deadline (the reference's transport sends with timeouts,
- * net_p2p/transport.rs:127-128): initialisation, each collective's enqueue, the capacity
- * agreement and bw_wait of an exchanged batch.  On an RCCL error or a missed deadline the
+ * net_p2p/transport.rs:127-128): initialisation, each collective's enqueue, the arrival of an
+ * exchange's counts (counted from its bw_exchange_dedup) and bw_wait of an exchanged batch.  On an RCCL error or a missed deadline the
  * communicator is aborted (ncclCommAbort), the call returns BW_ECOMM, and so does every later
  * call on it; bw_comm_destroy then only releases it.  bw_comm_init uses the default deadline. */
 #define BW_COMM_DEFAULT_TIMEOUT_MS 120000u
@@ -326,20 +341,24 @@ int bw_comm_status(const bw_comm* comm);
 int bw_comm_init_host(int device, int rank, int world, bw_host_all_to_all fn, void* user, bw_comm** out);
 void bw_comm_destroy(bw_comm* comm);
 const char* bw_comm_last_error(const bw_comm* comm);
-/* Digest slots per (source, owner) bucket.  0 (default): agreed on every exchange as the largest
- * max_blobs over the ranks so far (8 bytes per rank over a second RCCL communicator on its own
- * stream, so it never waits for the batches in flight; it only grows).  A fixed capacity skips
- * the agreement; a batch with more blobs for one owner than it sets the sticky BW_ENOSPC of
- * bw_index_check. */
+/* Obsolete since round 5 (accepted and ignored): every transfer of bw_exchange_dedup is sized
+ * exactly from the counts the exchange carries, so there is no bucket capacity to fix or agree. */
 int bw_comm_set_capacity(bw_comm* comm, uint64_t cap);
-/* Batch `ticket` of ctx (0 = the most recent; submitted with BW_F_NO_DEDUP and hashed, else
- * BW_ESTATE):
- * partition its digests by owner = digest[0] >> (8 - log2 world), all-to-all of the counts and
- * the buckets, the owner's gate against ctx's index, all-to-all of the verdicts back, scattered
- * into the batch's is_dup (bw_wait / bw_batch_views see them).  Enqueued on ctx's stream with no
- * host synchronization (RCCL; the host transport synchronizes inside).  Every rank calls it for
- * its k-th batch in the same order. */
+/* Batch `ticket` of ctx (0 = the most recent; submitted with BW_F_NO_DEDUP, hashed and not split,
+ * else BW_ESTATE) through the exchange: its digests are grouped by owner = digest[0] >> (8 - log2
+ * world), and the per-owner counts go to every rank (16 bytes per rank, on a control communicator
+ * split off at bw_comm_init and a stream of its own).  The call returns without waiting for any
+ * peer.  Once the counts have arrived -- noticed by any later call on the communicator (the next
+ * bw_exchange_dedup, bw_comm_progress, bw_wait of an exchanged batch, a submit that reuses its
+ * slot) -- the digests travel to their owners (each transfer exactly its digests), the owner gates
+ * them against ctx's index in source-rank order (canonical when files are sharded rank-major), and
+ * the verdicts come back into the batch's is_dup and records (bw_wait).  Exchanges finish in the
+ * order they were issued; every rank calls this for its k-th batch in the same order, and the
+ * contexts sharing a communicator are driven from one thread.  The host transport runs the whole
+ * exchange inside the call (its all-to-all is synchronous). */
 int bw_exchange_dedup(bw_ctx* ctx, bw_comm* comm, uint64_t ticket);
+/* Finish the queued exchanges whose counts have arrived (never waits).  BW_ECOMM once aborted. */
+int bw_comm_progress(bw_comm* comm);
 
 /* ---- tree blobs: split_serialize_tree + add_tree_to_blobs, dir_packer.rs:314-390 ----
  * Tree { kind: TreeKind, name: String, metadata: TreeMetadata { size, mtime, ctime: Option<u64> },

@@ -35,6 +35,7 @@ pub mod ffi {
     pub const BW_OK: c_int = 0;
     pub const BW_EINVAL: c_int = -1;
     pub const BW_ENOSPC: c_int = -2;
+    pub const BW_COALESCE_MAX_MSG: u64 = 4_194_304;
     pub const BW_EHIP: c_int = -3;
     pub const BW_ENOMEM: c_int = -4;
     pub const BW_ECOLLISION: c_int = -5;
@@ -161,6 +162,8 @@ pub mod ffi {
         pub fn bw_fastcdc_release(handle: u64);
         pub fn bw_blake3_kept_hits() -> u64;
         pub fn bw_blake3_hash(ctx: *mut bw_ctx, data: *const u8, len: u64, out: *mut u8) -> c_int;
+        pub fn bw_blake3_hash_dropin(ctx: *mut bw_ctx, data: *const u8, len: u64, out: *mut u8) -> c_int;
+        pub fn bw_blake3_coalesce_stats(device: c_int, batches: *mut u64, messages: *mut u64) -> c_int;
         pub fn bw_blake3_hash_many(ctx: *mut bw_ctx, data: *const u8, data_len: u64, offsets: *const u64,
                                    lengths: *const u64, n: u64, out: *mut u8) -> c_int;
 
@@ -218,6 +221,7 @@ pub mod ffi {
         pub fn bw_comm_last_error(comm: *const bw_comm) -> *const c_char;
         pub fn bw_comm_set_capacity(comm: *mut bw_comm, cap: u64) -> c_int;
         pub fn bw_exchange_dedup(ctx: *mut bw_ctx, comm: *mut bw_comm, ticket: u64) -> c_int;
+        pub fn bw_comm_progress(comm: *mut bw_comm) -> c_int;
 
         pub fn bw_tree_serialize(tree: *const bw_tree, next_sibling: *const u8, out: *mut u8, cap: u64,
                                  n_out: *mut u64) -> c_int;
@@ -372,6 +376,15 @@ impl Context {
     pub fn blake3_hash(&mut self, data: &[u8]) -> Result<[u8; 32]> {
         let mut h = [0u8; 32];
         self.check(unsafe { ffi::bw_blake3_hash(self.raw, data.as_ptr(), data.len() as u64, h.as_mut_ptr()) })?;
+        Ok(h)
+    }
+
+    /// `blake3::hash(data).into()` through the drop-in entry: a chunk slice of a live
+    /// `fastcdc_chunks_hashed` source is answered from its kept digest.  The caller guarantees
+    /// those bytes do not change while the handle lives (the `FastCDC` drop-in borrows them).
+    pub fn blake3_hash_dropin(&mut self, data: &[u8]) -> Result<[u8; 32]> {
+        let mut h = [0u8; 32];
+        self.check(unsafe { ffi::bw_blake3_hash_dropin(self.raw, data.as_ptr(), data.len() as u64, h.as_mut_ptr()) })?;
         Ok(h)
     }
 
@@ -556,10 +569,20 @@ impl Comm {
         Ok(Comm { raw, _host: Some(state) })
     }
 
+    /// Obsolete since round 5 (accepted and ignored): the exchange sizes its transfers itself.
     pub fn set_capacity(&mut self, cap: u64) -> Result<()> {
         let rc = unsafe { ffi::bw_comm_set_capacity(self.raw, cap) };
         if rc != ffi::BW_OK {
             return Err(Error { rc, msg: "bw_comm_set_capacity".into() });
+        }
+        Ok(())
+    }
+
+    /// Finish the queued exchanges whose digest counts have arrived; never waits for a peer.
+    pub fn progress(&mut self) -> Result<()> {
+        let rc = unsafe { ffi::bw_comm_progress(self.raw) };
+        if rc != ffi::BW_OK {
+            return Err(Error { rc, msg: message(unsafe { ffi::bw_comm_last_error(self.raw) }) });
         }
         Ok(())
     }
@@ -571,20 +594,34 @@ impl Drop for Comm {
     }
 }
 
+// The drop-ins' contexts: the reference's calls carry none, and tokio runs one worker thread per
+// core (client/src/main.rs:43, 256 on an MI355X node), so the threads share a small pool
+// (BACKUWUP_GPU_CONTEXTS, default 16) instead of holding one context each; a thread takes the
+// first free one from its own starting point and only blocks when all are busy.  blake3::hash
+// of small messages needs none of them for long: the library coalesces concurrent calls into one
+// launch of its own (bw_blake3_hash).
+static POOL: std::sync::OnceLock<Vec<std::sync::Mutex<Context>>> = std::sync::OnceLock::new();
+static NEXT_SLOT: std::sync::atomic::AtomicUsize = std::sync::atomic::AtomicUsize::new(0);
 thread_local! {
-    // the drop-ins' context: the reference's calls carry none (one per tokio worker thread)
-    static DEFAULT: RefCell<Option<Context>> = RefCell::new(None);
+    static SLOT: RefCell<Option<usize>> = RefCell::new(None);
 }
 
 fn with_default<R>(f: impl FnOnce(&mut Context) -> R) -> R {
-    DEFAULT.with(|cell| {
-        let mut slot = cell.borrow_mut();
-        if slot.is_none() {
-            let dev = std::env::var("BACKUWUP_GPU_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0);
-            *slot = Some(Context::new(dev).expect("no MI355X for backuwup-gpu"));
+    let pool = POOL.get_or_init(|| {
+        let dev = std::env::var("BACKUWUP_GPU_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0);
+        let n = std::env::var("BACKUWUP_GPU_CONTEXTS").ok().and_then(|v| v.parse().ok()).unwrap_or(16usize).max(1);
+        (0..n).map(|_| std::sync::Mutex::new(Context::new(dev).expect("no MI355X for backuwup-gpu"))).collect()
+    });
+    let start = SLOT.with(|s| {
+        *s.borrow_mut().get_or_insert_with(|| NEXT_SLOT.fetch_add(1, std::sync::atomic::Ordering::Relaxed))
+    }) % pool.len();
+    for k in 0..pool.len() {
+        if let Ok(mut c) = pool[(start + k) % pool.len()].try_lock() {
+            return f(&mut c);
         }
-        f(slot.as_mut().unwrap())
-    })
+    }
+    let mut c = pool[start].lock().unwrap_or_else(|e| e.into_inner());
+    f(&mut c)
 }
 
 /// Drop-in for the `fastcdc` crate 3.0.3, module `v2020`, as backuwup uses it.
@@ -681,8 +718,20 @@ pub mod blake3 {
         }
     }
 
-    /// `blake3::hash(input)` -- standard unkeyed BLAKE3, 32-byte output, computed on the GPU.
+    /// `blake3::hash(input)` -- standard unkeyed BLAKE3, 32-byte output, computed on the GPU.  A
+    /// chunk of a live `FastCDC` drop-in is answered from the digest its construction kept (safe
+    /// Rust cannot change those bytes while the `FastCDC` borrows them); concurrent calls from many
+    /// threads share one launch.
     pub fn hash(input: &[u8]) -> Hash {
-        Hash(super::with_default(|c| c.blake3_hash(input)).expect("GPU hashing failed"))
+        if input.len() as u64 <= crate::ffi::BW_COALESCE_MAX_MSG {
+            // coalesced: the library only reads the context's device, so no pool slot is held while
+            // the call waits for its batch (holding one would cap a batch at the pool's size)
+            let raw = super::with_default(|c| c.raw);
+            let mut h = [0u8; 32];
+            let rc = unsafe { crate::ffi::bw_blake3_hash_dropin(raw, input.as_ptr(), input.len() as u64, h.as_mut_ptr()) };
+            assert_eq!(rc, crate::ffi::BW_OK, "GPU hashing failed");
+            return Hash(h);
+        }
+        Hash(super::with_default(|c| c.blake3_hash_dropin(input)).expect("GPU hashing failed"))
     }
 }

@@ -4,6 +4,8 @@ Integer/byte work only, so every comparison is exact.  Inputs are seeded; sizes 
 oracle finishes in seconds.  Edge cases follow SURVEY.md §4 item 4: odd tails, lengths at
 min/avg/max +-1, all-zero data (every chunk = max), byte-shifted copies, empty inputs.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -457,10 +459,11 @@ def _exchange_world1(ctx, torch, DeviceShardOps, exchange_dedup, small_files):
 
 def test_dropin_call_sites_kept_digests(ctx, oracle):
     """dir_packer.rs:254-266 chunks a file, then :286 hashes each chunk slice of it.
-    bw_fastcdc_chunks_hashed chunks and hashes in one submit; bw_blake3_hash of exactly one of its
-    chunk slices returns the kept digest (counted by bw_blake3_kept_hits), anything else is hashed
-    on the GPU, and after the release nothing is answered from them.  Every digest equals the
-    oracle's, and so do the Python drop-ins (fastcdc.FastCDC + blake3.hash on memoryview slices)."""
+    bw_fastcdc_chunks_hashed chunks and hashes in one submit; bw_blake3_hash_dropin of exactly one of
+    its chunk slices returns the kept digest (counted by bw_blake3_kept_hits), anything else is
+    hashed on the GPU, the generic bw_blake3_hash never answers from them, and after the
+    release nothing is answered from them.  Every digest equals the oracle's, and so do the Python
+    drop-ins (fastcdc.FastCDC + blake3.hash on memoryview slices of immutable bytes)."""
     from backuwup_amd import _lib
     from backuwup_amd import blake3 as b3
     from backuwup_amd import fastcdc as fc
@@ -471,23 +474,39 @@ def test_dropin_call_sites_kept_digests(ctx, oracle):
     assert chunks == want and h != 0
     hits0 = L.bw_blake3_kept_hits()
     for _, off, ln in chunks:
-        assert ctx.blake3_at(data, off, ln) == oracle.blake3(data[off:off + ln])
+        assert ctx.blake3_at(data, off, ln, kept=True) == oracle.blake3(data[off:off + ln])
+    assert L.bw_blake3_kept_hits() - hits0 == len(chunks)
+    # the generic entry always hashes
+    assert ctx.blake3_at(data, chunks[0][1], chunks[0][2]) == oracle.blake3(data[:chunks[0][2]])
     assert L.bw_blake3_kept_hits() - hits0 == len(chunks)
     # not a chunk of it: hashed on the GPU (same pointer, other length; other pointer, same length)
     n0 = chunks[0][2]
-    assert ctx.blake3_at(data, 0, n0 - 1) == oracle.blake3(data[:n0 - 1])
-    assert ctx.blake3_at(data, 1, n0) == oracle.blake3(data[1:n0 + 1])
+    assert ctx.blake3_at(data, 0, n0 - 1, kept=True) == oracle.blake3(data[:n0 - 1])
+    assert ctx.blake3_at(data, 1, n0, kept=True) == oracle.blake3(data[1:n0 + 1])
     assert L.bw_blake3_kept_hits() - hits0 == len(chunks)
     ctx.fastcdc_release(h)
-    assert ctx.blake3_at(data, 0, n0) == oracle.blake3(data[:n0])
+    assert ctx.blake3_at(data, 0, n0, kept=True) == oracle.blake3(data[:n0])
     assert L.bw_blake3_kept_hits() - hits0 == len(chunks)
-    # the Python drop-ins, written exactly like the reference's loop
-    mv = memoryview(data)
+    # the Python drop-ins, written exactly like the reference's loop, over immutable bytes
+    mv = memoryview(data.tobytes())
     hits1 = L.bw_blake3_kept_hits()
     chunker = fc.FastCDC(mv, *BK, ctx=ctx)
     got = [b3.hash(mv[c.offset:c.offset + c.length], ctx=ctx) for c in chunker]
     assert got == [oracle.blake3(data[o:o + n]) for _, o, n in want]
     assert L.bw_blake3_kept_hits() - hits1 == len(want)
+    del chunker
+    # a writable source is chunked without keeping digests, so rewriting it in place
+    # while the FastCDC lives gives the new bytes' digest, never the one taken at chunking time
+    buf = bytearray(data.tobytes())
+    mvw = memoryview(buf)
+    hits2 = L.bw_blake3_kept_hits()
+    chunker = fc.FastCDC(mvw, *BK, ctx=ctx)
+    cuts = [(c.offset, c.length) for c in chunker]
+    assert cuts == [(o, n) for _, o, n in want]
+    o1, n1 = cuts[1]
+    buf[o1:o1 + 64] = bytes(64)  # a reused read buffer: the chunk's bytes change
+    assert b3.hash(mvw[o1:o1 + n1], ctx=ctx) == oracle.blake3(bytes(buf[o1:o1 + n1]))
+    assert L.bw_blake3_kept_hits() == hits2
     del chunker
     # empty source: no chunks, nothing kept
     assert ctx.fastcdc_chunks_hashed(np.zeros(0, np.uint8), *BK) == ([], 0)
@@ -512,7 +531,7 @@ def test_dropin_call_sites_many_threads(oracle):
             with Context(0) as c:
                 for k in range(t, len(files), 4):
                     chunks, h = c.fastcdc_chunks_hashed(files[k], *BK)
-                    got[k] = [(o, n, c.blake3_at(files[k], o, n)) for _, o, n in chunks]
+                    got[k] = [(o, n, c.blake3_at(files[k], o, n, kept=True)) for _, o, n in chunks]
                     c.fastcdc_release(h)
         except Exception as e:  # reported below
             errors.append(repr(e))
@@ -525,3 +544,46 @@ def test_dropin_call_sites_many_threads(oracle):
     assert not errors, errors
     assert got == want
     assert L.bw_blake3_kept_hits() - hits0 == sum(len(w) for w in want)
+
+
+def test_coalesced_hash_many_threads(oracle):
+    """the reference calls blake3::hash once per small file and once per tree blob,
+    from every tokio worker at once (dir_packer.rs:166, :286, :320).  Sixteen threads hash thousands
+    of small messages (0 B - 70 KiB, trees' ~100 B included) through bw_blake3_hash at the same time:
+    the library coalesces them into shared launches, and every digest equals the oracle's."""
+    import threading
+    from backuwup_amd import Context, _lib
+    L = _lib.load()
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 70 << 10, 4000)
+    lens[::7] = rng.integers(60, 140, len(lens[::7]))  # tree-blob sized
+    lens[:3] = [0, 1, 1024]
+    blob = splitmix_bytes(31, int(lens.sum()) + 64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    want = [oracle.blake3(blob[o:o + n]) for o, n in zip(offs, lens)]
+    got = [None] * len(lens)
+    errors = []
+    b0, m0 = ctypes.c_uint64(), ctypes.c_uint64()
+    L.bw_blake3_coalesce_stats(0, ctypes.byref(b0), ctypes.byref(m0))
+    ctxs = [Context(0) for _ in range(4)]  # 16 threads over 4 contexts: small messages only name the device
+
+    def worker(t):
+        try:
+            for i in range(t, len(lens), 16):
+                got[i] = ctxs[t % 4].blake3_at(blob, int(offs[i]), int(lens[i]))
+        except Exception as e:  # reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=240)
+    for c in ctxs:
+        c.close()
+    assert not errors, errors
+    assert got == want
+    b1, m1 = ctypes.c_uint64(), ctypes.c_uint64()
+    L.bw_blake3_coalesce_stats(0, ctypes.byref(b1), ctypes.byref(m1))
+    assert m1.value - m0.value == len(lens)
+    assert b1.value - b0.value < len(lens)  # some launches carried several callers' messages

@@ -563,7 +563,6 @@ def test_exchange_dedup_rccl_world1_c_abi(oracle):
             c.set_stream(torch.cuda.Stream().cuda_stream)
             c.attach_index(ix)
         cs[0].index_reset(1 << 16)
-        comm.set_capacity(2000)  # the largest batch's bound (batch 3 holds 2000 small files)
         p = make_params(flags=BW_F_NO_DEDUP)
         tickets = []
         for k, (t, (d, o, l)) in enumerate(zip(devs, batches)):
@@ -586,28 +585,29 @@ def test_exchange_dedup_rccl_world1_c_abi(oracle):
         with pytest.raises(BwError) as e:
             cs[0].exchange_dedup(comm, tk)
         assert e.value.rc == BW_ESTATE
-        # the capacity is agreed on every exchange: a later batch with twice the first
-        # one's bound grows it on every rank and gets complete verdicts
+        # round 5: no capacity at all -- every transfer is sized from the exchange's own counts, so
+        # batches that grow and shrink on one communicator (and a set_capacity, now ignored) need
+        # nothing from the caller; several exchanges queue before any wait, and progress() finishes
+        # whatever has its counts without waiting
         cs[0].index_reset(1 << 16)
         comm2 = Comm.rccl(0, 0, 1, unique_id())
-        want2 = oracle_session(oracle, [batches[0], batches[3]])
-        for j, k in enumerate((0, 3)):
-            d, o, l = batches[k]
-            tk = cs[0].submit_device(devs[k].data_ptr(), d.size, o, l, p)
-            cs[0].exchange_dedup(comm2, tk)
-            blobs_equal(cs[0].wait(tk), want2[j], ("grown", k))
-        cs[0].index_check()
-        # a capacity fixed by the caller is not agreed: a larger batch overflows its bucket and
-        # says so instead of returning incomplete verdicts
-        cs[0].index_reset(1 << 16)
         comm2.set_capacity(1000)
-        for k in (0, 3):
+        order = (0, 3, 1, 0, 2)
+        want2 = oracle_session(oracle, [batches[k] for k in order])
+        tks = []
+        for j, k in enumerate(order):
             d, o, l = batches[k]
-            tk = cs[0].submit_device(devs[k].data_ptr(), d.size, o, l, p)
-            cs[0].exchange_dedup(comm2, tk)
-        with pytest.raises(BwError) as e:
-            cs[0].wait(tk)
-        assert e.value.rc == BW_ENOSPC
+            c = cs[j % 2]
+            tk = c.submit_device(devs[k].data_ptr(), d.size, o, l, p)
+            c.exchange_dedup(comm2, tk)
+            comm2.progress()
+            tks.append((c, tk))
+            if len(tks) > 2:  # two exchanged batches in flight, the oldest read
+                c0, t0 = tks[j - 2]
+                blobs_equal(c0.wait(t0), want2[j - 2], ("grow/shrink", j - 2))
+        for j in (len(order) - 2, len(order) - 1):
+            blobs_equal(tks[j][0].wait(tks[j][1]), want2[j], ("grow/shrink", j))
+        cs[0].index_check()
     finally:
         for c in cs:
             c.close()
@@ -632,11 +632,13 @@ def _two_rank_c_worker(rank, world, port, q):
         out = []
         with Context(0) as c, Comm.host(0, rank, world, gloo_all_to_all()) as comm:
             c.index_reset(1 << 16)
-            for batch in range(3):  # batch-major, then rank-major canonical order
+            for batch in range(4):  # batch-major, then rank-major canonical order
                 lo = ((batch % 2) * world + rank) * per // 4
                 hi = lo + per // 4 - 7 * rank * (batch == 1)  # ragged: the ranks' batch sizes differ
-                if batch == 2 and rank == 1:  # 4x the bound of its first batch: the capacity grows
+                if batch == 2 and rank == 1:  # 4x the size of its first batch
                     lo, hi = 2 * per // 2, 2 * per // 2 + per
+                if batch == 3:  # then small again (partly repeats: duplicates across the ranks)
+                    lo, hi = (rank * 37, rank * 37 + 50)
                 b = _slices(data, offs, lens, [(lo, hi)])[0]
                 t_dev = torch.from_numpy(b[0]).cuda()
                 tk = c.submit_device(t_dev.data_ptr(), b[0].size, b[1], b[2], make_params(flags=BW_F_NO_DEDUP))
@@ -669,7 +671,7 @@ def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
         assert p.exitcode == 0
     data, offs, lens = small_files(6000, seed=56)
     ix = oracle.Index()
-    for batch in range(3):
+    for batch in range(4):
         for r in range(2):
             lo, hi, dig, dup = got[r][batch]
             want = oracle.process_files(*_slices(data, offs, lens, [(lo, hi)])[0], index=ix)

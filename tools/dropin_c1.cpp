@@ -2,23 +2,27 @@
 // Rust drop-ins bind.  Per file, exactly as dir_packer.rs:246-286 does:
 //   len > 1 MiB: FastCDC::new(&mmap, 256 KiB, 1 MiB, 3 MiB), then blake3::hash(&mmap[off..off+len])
 //                per chunk;   len <= 1 MiB: blake3::hash(whole file)
-// on T threads (one tokio task per file; one context per thread, the shim's thread-local default),
-// over C1's files in pageable host memory (the mmap'd page cache of the reference).
-//   sync  bw_fastcdc_chunks + bw_blake3_hash per chunk: every chunk crosses PCIe twice, one
-//         synchronous GPU round trip per call
-//   kept  bw_fastcdc_chunks_hashed (chunks and hashes the file in one submit) + bw_blake3_hash per
-//         chunk answered from the kept digests + bw_fastcdc_release: what the Rust FastCDC drop-in
-//         does behind the same signatures
+// on T threads (one tokio task per file), one context per thread or a pool of P contexts shared
+// by the threads (a thread takes the first free one, as the Rust shim does), over C1's files in
+// pageable host memory (the mmap'd page cache of the reference).
+//   sync  bw_fastcdc_chunks + bw_blake3_hash per chunk: every chunk crosses PCIe twice (the
+//         library coalesces concurrent hash calls into shared launches)
+//   kept  bw_fastcdc_chunks_hashed (chunks and hashes the file in one submit) + bw_blake3_hash_dropin
+//         per chunk answered from the kept digests + bw_fastcdc_release: what the Rust FastCDC
+//         drop-in does behind the same signatures
 // Prints GB/s of file bytes per mode (best of reps) and checks that both modes give the same
 // chunks and digests (the GPU results are checked against the oracle in tests/test_gpu_parity.py).
 //
 // Build (CPU, after the library):
 //   hipcc -O2 -std=c++17 -I include tools/dropin_c1.cpp -L backuwup_amd -lbackuwup_amd \
 //     -Wl,-rpath,$PWD/backuwup_amd -lpthread -o build_ab/dropin_c1
-// Run: build_ab/dropin_c1 <corpus.bin> [threads=16] [reps=3] [staging chunk MiB=64]
+// Run: build_ab/dropin_c1 <corpus.bin> [threads=16] [reps=3] [staging chunk MiB=64] [contexts=0: one per thread]
 //   corpus.bin = u64 n, n offsets, n lengths, then the bytes (tools/gpu_dropin.sh writes bench.py's C1)
+#include <hip/hip_runtime.h>
+
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -72,7 +76,8 @@ static int process(bw_ctx* ctx, const uint8_t* p, uint64_t n, bool kept, FileOut
     if (rc) return err = bw_last_error(ctx), rc;
     ch.resize(nc);
     for (const bw_chunk& c : ch) {  // for chunk in chunker { add_file_blob(&mmap[off..off+len]) }
-        if ((rc = bw_blake3_hash(ctx, p + c.offset, c.length, d))) break;
+        if ((rc = kept ? bw_blake3_hash_dropin(ctx, p + c.offset, c.length, d) : bw_blake3_hash(ctx, p + c.offset, c.length, d)))
+            break;
         o.dig.insert(o.dig.end(), d, d + 32);
     }
     bw_fastcdc_release(handle);
@@ -93,16 +98,21 @@ int main(int argc, char** argv) {
     }
     const int T = argc > 2 ? atoi(argv[2]) : 16, reps = argc > 3 ? atoi(argv[3]) : 3;
     const uint64_t stage_mib = argc > 4 ? strtoull(argv[4], nullptr, 10) : 0;  // BW_OPT_STAGE_CHUNK (0: default)
+    const int P = argc > 5 && atoi(argv[5]) > 0 ? atoi(argv[5]) : T;             // contexts (0: one per thread)
     const uint64_t nf = c.off.size();
     uint64_t bytes = 0, big = 0;
     for (uint64_t i = 0; i < nf; i++) {
         bytes += c.len[i];
         big += c.len[i] > SMALL;
     }
-    printf("corpus: %llu files (%llu > 1 MiB), %.3f GB; %d threads, one context each\n", (unsigned long long)nf,
-           (unsigned long long)big, bytes / 1e9, T);
-    std::vector<bw_ctx*> ctxs(T);
-    for (int t = 0; t < T; t++) {
+    printf("corpus: %llu files (%llu > 1 MiB), %.3f GB; %d threads, %d contexts\n", (unsigned long long)nf,
+           (unsigned long long)big, bytes / 1e9, T, P);
+    size_t free0 = 0, tot = 0;
+    hipSetDevice(0);
+    hipMemGetInfo(&free0, &tot);
+    std::vector<bw_ctx*> ctxs(P);
+    std::vector<std::mutex> ctx_mu(P);
+    for (int t = 0; t < P; t++) {
         if (bw_create(0, &ctxs[t])) return 3;
         if (stage_mib && bw_set_option(ctxs[t], BW_OPT_STAGE_CHUNK, stage_mib << 20)) return 3;
     }
@@ -123,7 +133,15 @@ int main(int argc, char** argv) {
             for (int t = 0; t < T; t++)
                 th.emplace_back([&, t] {
                     for (uint64_t i; (i = next++) < nf && !fail;) {
-                        if (int rc = process(ctxs[t], c.data.data() + c.off[i], c.len[i], kept, out[i], errs[t % 64]))
+                        int k = t % P;  // the first free context from this thread's starting point
+                        for (int j = 0; j < P; j++)
+                            if (ctx_mu[(t + j) % P].try_lock()) {
+                                k = (t + j) % P;
+                                ctx_mu[k].unlock();
+                                break;
+                            }
+                        std::lock_guard<std::mutex> lk(ctx_mu[k]);
+                        if (int rc = process(ctxs[k], c.data.data() + c.off[i], c.len[i], kept, out[i], errs[t % 64]))
                             fail = rc;
                     }
                 });
@@ -138,6 +156,10 @@ int main(int argc, char** argv) {
         }
         uint64_t nchunks = 0;
         for (auto& o : out) nchunks += o.chunks.size();
+        size_t fr = 0;
+        hipMemGetInfo(&fr, &tot);
+        printf("HBM in use after the passes: %.2f GiB (%.3f GiB per context)\n", (free0 - fr) / 1073741824.0,
+               (free0 - fr) / 1073741824.0 / P);
         printf("%-4s %8.2f GB/s (%.2f ms per pass, best of %d; %llu blobs; kept-digest answers %llu)\n",
                kept ? "kept" : "sync", bytes / best / 1e9, best * 1e3, reps, (unsigned long long)nchunks,
                (unsigned long long)(bw_blake3_kept_hits() - hits0));

@@ -1,13 +1,25 @@
 #!/bin/bash
-# the reference's unchanged call sites on C1 (tools/dropin_c1.cpp, 16 threads, one
-# context each, pageable memory), then bench.py's C1 line for the 16-core CPU baseline on the same
-# files.  Build first (CPU): see tools/dropin_c1.cpp.
+# The reference's unchanged call sites through the drop-ins.
+#   C1 (tools/dropin_c1.cpp): per file FastCDC::new + blake3::hash per chunk, at 16 threads with one
+#      context each, and at 64 / 256 threads (tokio's default is one worker per core) with one
+#      context each and with the Rust shim's pool of 16 contexts; HBM per context.
+#   C4 (tools/dropin_c4.cpp): 1 M small files, blake3::hash of each file and of its Tree blob, at
+#      16 / 64 / 256 threads over a pool of 16 contexts (concurrent calls coalesced by the library).
+#   CPU on the same files: bench.py's cpu_baseline (C1; C4 with --cpu-trees).
+# Build first (CPU): see the two tools' headers.  DROPIN_PARTS picks parts (default "c1 c4 cpu").
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
 : > "$OUT/dropin_summary.txt"
-python3 - <<'EOF' > "$OUT/corpus.log" 2>&1 || exit 1
+PARTS=${DROPIN_PARTS:-"c1 c4 cpu"}
+run() {  # name seconds cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?; echo "$name rc=$rc" >> "$OUT/dropin_summary.txt"; return $rc
+}
+if [[ " $PARTS " == *" c1 "* ]]; then
+  python3 - <<'PY' > "$OUT/corpus_c1.log" 2>&1 || exit 1
 import numpy as np, sys
 sys.path.insert(0, ".")
 from backuwup_amd.synth import tree_corpus
@@ -18,13 +30,28 @@ with open("/tmp/c1.bin", "wb") as f:
     np.asarray(l, np.uint64).tofile(f)
     d.tofile(f)
 print("files", len(o), "bytes", int(np.sum(l)))
-EOF
-for cfg in ${DROPIN_CFGS:-16:0 8:0 16:8 16:4 32:8}; do
-  IFS=: read -r t mib <<< "$cfg"
-  timeout -k 10 300 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 $mib > "$OUT/dropin_t${t}_s${mib}.log" 2>&1
-  rc=$?; echo "dropin t=$t stage=$mib rc=$rc" >> "$OUT/dropin_summary.txt"; [ $rc -eq 0 ] || exit 1
-done
-[ -n "${DROPIN_ONLY:-}" ] && exit 0
-timeout -k 10 600 python3 bench.py --workload c1 --steps 300 > "$OUT/bench_c1.log" 2>&1
-rc=$?; echo "bench c1 rc=$rc" >> "$OUT/dropin_summary.txt"; [ $rc -eq 0 ] || exit 1
+PY
+  for cfg in ${DROPIN_CFGS:-16:0 64:0 256:0 64:16 256:16}; do
+    IFS=: read -r t p <<< "$cfg"
+    run dropin_c1_t${t}_p${p} 600 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 0 $p || exit 1
+  done
+fi
+if [[ " $PARTS " == *" c4 "* ]]; then
+  python3 - <<'PY' > "$OUT/corpus_c4.log" 2>&1 || exit 1
+import numpy as np, sys
+sys.path.insert(0, ".")
+from backuwup_amd.synth import small_files_table
+u, o, l = small_files_table(1000000, seed=3)  # bench.py --workload c4, rank 0 (bytes: splitmix seed 3)
+with open("/tmp/c4_table.bin", "wb") as f:
+    np.array([len(o), u, 3], np.uint64).tofile(f)
+    np.asarray(o, np.uint64).tofile(f)
+    np.asarray(l, np.uint64).tofile(f)
+print("files", len(o), "unique bytes", u, "file bytes", int(np.sum(l)))
+PY
+  run dropin_c4 900 ./build_ab/dropin_c4 /tmp/c4_table.bin ${DROPIN_C4_THREADS:-16,64,256} 16 2 || exit 1
+fi
+if [[ " $PARTS " == *" cpu "* ]]; then
+  run bench_c1_cpu 600 python3 bench.py --workload c1 --steps 300 || exit 1
+  run bench_c4_cpu 900 python3 bench.py --workload c4 --steps 20 --cpu-trees || exit 1
+fi
 exit 0

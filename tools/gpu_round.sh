@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session of several steps (round 4), chosen by STEPS (default: all).  Every step runs under
+# One GPU session of several steps (rounds 4-5), chosen by STEPS (default: all).  Every step runs under
 # its own time limit; a step that times out, aborts or faults (rc 124/134/137/139 or a signal) ends
 # the session there, any other failure is recorded and the next step runs.  Results go to
 # gpurun_out/ (summary.txt lists each step's rc).
@@ -36,7 +36,7 @@ for s in $STEPS; do
     smoke) step smoke 300 python __graft_entry__.py ;;
     collide) step collide 120 ./build_ab/collide "$OUT/blake3_prefix_collision.json" 14 32768 1 ;;
     slab) step slab 900 bash tools/gpu_slab.sh ;;
-    dropin) step dropin 900 bash tools/gpu_dropin.sh ;;
+    dropin) step dropin 1100 bash tools/gpu_dropin.sh ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
@@ -52,6 +52,11 @@ for s in $STEPS; do
       step bench_c4 600 python bench.py --workload c4 --steps 60 --no-cpu-baseline &&
       step bench_c5 600 python bench.py --workload c5 --steps 3 --no-cpu-baseline ;;
     debug) step debug_check 600 python tools/debug_check.py ;;
+    exch)  # round 5: the exactly sized, deferred exchange (host transport + RCCL world 1) and the bench's
+           # exchange path at world size 1
+      step exch_tests 600 python -u -m pytest tests/test_gpu_pipeline.py -m gpu -k "exchange or shard" -v \
+        -p no:cacheprovider --timeout 300 --timeout-method thread &&
+      step bench_exch 600 python bench.py --exchange --steps 60 --no-cpu-baseline ;;
     zsdiag)  # diagnostic zstd variants: section timers (BW_ZSTD_TIMING) and the step fences dropped
              # (build first: python backuwup_amd/build.py --ztime; build(variant="zsnofence", defines=("-DBW_ZS_NOFENCE",)))
       step zstd_ztime 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_ztime.so" python tools/zstd_bench.py \
