@@ -53,6 +53,11 @@ class BwTreeBlob(ctypes.Structure):
                 ("hash", ctypes.c_uint8 * 32), ("is_dup", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 7)]
 
 
+class BwStreamShard(ctypes.Structure):
+    _fields_ = [("ticket", ctypes.c_uint64), ("first_blob", ctypes.c_uint64), ("n_blobs", ctypes.c_uint64),
+                ("chain_start", ctypes.c_uint64), ("rounds", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
 class BwPackfile(ctypes.Structure):
     _fields_ = [("first_blob", ctypes.c_uint64), ("n_blobs", ctypes.c_uint64), ("offset", ctypes.c_uint64),
                 ("size", ctypes.c_uint64), ("header_len", ctypes.c_uint64)]
@@ -129,6 +134,9 @@ SIGNATURES = [
     ("bw_comm_set_capacity", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("bw_exchange_dedup", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("bw_comm_progress", ctypes.c_int, [vp]),
+    ("bw_stream_window", ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, u64p, u64p]),
+    ("bw_chunk_stream_shard", ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.POINTER(BwParams),
+                                             ctypes.POINTER(BwStreamShard)]),
     ("bw_tree_serialize", ctypes.c_int, [ctypes.POINTER(BwTree), vp, vp, ctypes.c_uint64, u64p]),
     ("bw_tree_blobs", ctypes.c_int, [vp, ctypes.POINTER(BwTree), ctypes.c_uint64, ctypes.c_uint32, vp,
                                      ctypes.POINTER(BwTreeBlob), ctypes.c_uint64, u64p]),

@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "libbackuwup_amd.so")
 # only when BW_LIB points at it (tools/debug_check.py), never by the product path
 LIB_DEBUG = os.path.join(HERE, "libbackuwup_amd_debug.so")
 SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_comm.hip", "bw_tree.hip", "bw_seal.hip",
-           "bw_pack.hip", "bw_zstd.hip", "bw_dropin.hip"]
+           "bw_pack.hip", "bw_zstd.hip", "bw_dropin.hip", "bw_stream.hip"]
 ROCM_LIB = "/opt/rocm/lib"
 ARCH = os.environ.get("BW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # sources that are not on the chunk -> hash -> dedup path the bench profiles (their kernels never
 # run in the C2 command), so editing them does not make the committed PMC traffic stale
-OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip", "bw_comm.hip", "bw_dropin.hip")
+OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip", "bw_comm.hip", "bw_dropin.hip", "bw_stream.hip")
 
 
 def source_digest():

@@ -650,6 +650,19 @@ class Context:
             raise _lib.BwError(rc, comm.last_error() or self._L.bw_last_error(self.h).decode())
         check(rc, self.h)
 
+    def chunk_stream_shard(self, comm, d_window, file_len, params=None):
+        """bw_chunk_stream_shard: this rank's part of one file split across the ranks of `comm`
+        (d_window = device address of file byte lo of stream_window()).  -> dict(ticket, first_blob,
+        n_blobs, chain_start, rounds); bw_wait(ticket) holds the chain, blobs [first_blob, first_blob
+        + n_blobs) are the ones this rank emits (and the exchange sends)."""
+        out = _lib.BwStreamShard()
+        rc = self._L.bw_chunk_stream_shard(self.h, comm.h, ctypes.c_void_p(d_window), int(file_len),
+                                           ctypes.byref(params) if params is not None else None, ctypes.byref(out))
+        if rc == _lib.BW_ECOMM:
+            raise _lib.BwError(rc, comm.last_error() or self._L.bw_last_error(self.h).decode())
+        check(rc, self.h)
+        return {k: int(getattr(out, k)) for k in ("ticket", "first_blob", "n_blobs", "chain_start", "rounds")}
+
     def partition_buckets(self, d_digests, d_n, max_n, cap, n_owners, d_buckets, d_perm, d_counts):
         check(self._L.bw_partition_buckets(self.h, ctypes.c_void_p(d_digests), ctypes.c_void_p(d_n), max_n, cap,
                                            n_owners, ctypes.c_void_p(d_buckets), ctypes.c_void_p(d_perm),

@@ -86,6 +86,7 @@ struct Slot {
     int ex_state = 0, ex_rc = 0;
     bool ex_now = false;     // the counts arrived synchronously (host transport)
     uint64_t ex_since = 0;   // when the counts were enqueued (steady clock, ns)
+    uint64_t ex_first = 0, ex_n = ~0ull;  // the blobs the exchange sends (batch_set_exchange_range)
 };
 
 }  // namespace
@@ -1340,6 +1341,8 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
     s.comm = nullptr;
     s.ex_state = 0;
     s.ex_rc = 0;
+    s.ex_first = 0;
+    s.ex_n = ~0ull;
     if (stage)
         if (int r5 = stage_results(c, s, zero_copy, want)) return r5;
     phase(5);
@@ -1717,6 +1720,14 @@ extern "C" int bw_blake3_hash_many(bw_ctx* c, const uint8_t* data, uint64_t data
 
 int bw::ctx_device(const bw_ctx* c) { return c->device; }
 
+int bw::batch_set_exchange_range(bw_ctx* c, uint64_t ticket, uint64_t first, uint64_t n) {
+    Slot* s = slot_of(c, ticket);
+    if (!s || s->ex_state) return BW_ESTATE;
+    s->ex_first = first;
+    s->ex_n = n;
+    return BW_OK;
+}
+
 uint8_t* bw::message_stage(bw_ctx* c, size_t bytes) {
     hipSetDevice(c->device);
     if (c->msg_stage.cap < bytes) {
@@ -1862,7 +1873,7 @@ int exchange_finish(bw_comm* comm, bw_ctx* c, Slot& s) {
         n += scnt[k];
         rtot += rcnt[k];
     }
-    if (n > s.max_blobs) {
+    if (n > (s.ex_n == ~0ull ? s.max_blobs : s.ex_n)) {
         c->err = "exchange counts exceed the batch's blob bound (internal error)";
         return BW_EHIP;
     }
@@ -1879,7 +1890,9 @@ int exchange_finish(bw_comm* comm, bw_ctx* c, Slot& s) {
     if (rtot)
         if (int r = dedup_device(c, P<uint8_t>(c->ex_rbk), nullptr, rtot, rtot, P<uint8_t>(c->ex_v), st)) return r;
     if (int r = comm_all_to_allv(comm, c->ex_v.p, rcnt.data(), c->ex_rv.p, scnt.data(), 1, pad, st, c->err)) return r;
-    launch_owner_scatter(st, P<uint8_t>(c->ex_rv), P<uint64_t>(s.ex_perm), n, P<uint8_t>(s.is_dup), slot_records(s));
+    const uint64_t first = s.ex_n == ~0ull ? 0 : s.ex_first;  // perm counts from the range's first blob
+    launch_owner_scatter(st, P<uint8_t>(c->ex_rv), P<uint64_t>(s.ex_perm), n, P<uint8_t>(s.is_dup) + first,
+                         slot_records(s) + first * sizeof(bw_blob));
     launch_index_snapshot(st, P<uint64_t>(c->idx->dstate), slot_ctr(s));
     HIPCHK(c, hipGetLastError());
     s.dedup = true;  // bw_wait now reports the index's sticky errors for this batch
@@ -1966,17 +1979,26 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     }
     hipSetDevice(c->device);
     const uint32_t W = (uint32_t)comm_world(comm);
-    const uint64_t max_n = s->max_blobs;
+    const bool ranged = s->ex_n != ~0ull;  // a range of the batch's blobs (bw_chunk_stream_shard)
+    const uint64_t max_n = ranged ? s->ex_n : s->max_blobs;
     const uint64_t nblk = (max_n + 4095) / 4096;
     int rc = 0;
     rc |= ensure(c, s->ex_dig, max_n * 32);
     rc |= ensure(c, s->ex_perm, max_n * 8);
-    rc |= ensure(c, s->ex_msg, 2 * W * 8);
+    rc |= ensure(c, s->ex_msg, 2 * W * 8 + 8);
     rc |= ensure(c, c->bk_blk, (nblk + 1) * W * 8);
     if (rc) return BW_ENOMEM;
-    if (int r = ensure_host(c, s->ex_h, 4 * W * 8)) return r;
-    launch_owner_partition(c->stream, P<uint8_t>(s->digests), slot_ctr(*s) + C_NBLOBS, max_n, W, P<uint8_t>(s->ex_dig),
-                           P<uint64_t>(s->ex_perm), P<uint64_t>(s->ex_msg), P<uint64_t>(c->bk_blk));
+    if (int r = ensure_host(c, s->ex_h, 4 * W * 8 + 8)) return r;
+    const uint64_t* d_n = slot_ctr(*s) + C_NBLOBS;
+    if (ranged) {  // the range's length as a device count (pinned source: the copy is asynchronous)
+        uint64_t* hn = (uint64_t*)s->ex_h.p + 4 * W;
+        *hn = max_n;
+        HIPCHK(c, hipMemcpyAsync(P<uint64_t>(s->ex_msg) + 2 * W, hn, 8, hipMemcpyHostToDevice, c->stream));
+        d_n = P<uint64_t>(s->ex_msg) + 2 * W;
+    }
+    launch_owner_partition(c->stream, P<uint8_t>(s->digests) + (ranged ? 32 * s->ex_first : 0), d_n, max_n, W,
+                           P<uint8_t>(s->ex_dig), P<uint64_t>(s->ex_perm), P<uint64_t>(s->ex_msg),
+                           P<uint64_t>(c->bk_blk));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(s->ex_part, c->stream));
     s->comm = comm;

@@ -35,7 +35,8 @@ struct bw_comm {
     ncclComm_t ctl = nullptr;             // split of `nccl` at initialisation: the per-exchange counts,
                                           // on a stream of its own
     hipStream_t ctl_st = nullptr;
-    uint64_t* ctl_buf = nullptr;          // device, 2 x world u64: the counts received
+    uint64_t* ctl_buf = nullptr;          // device, 6 x world u64: [0, 2W) the counts received,
+                                          // [2W, 4W) / [4W, 6W) an allgather's send / receive
     bw_host_all_to_all host_fn = nullptr;  // or the caller's host transport
     void* user = nullptr;
     void* exq = nullptr;                   // exchanges waiting for their counts (bw_capi.hip)
@@ -199,6 +200,48 @@ int bw::comm_poll(bw_comm* c, hipEvent_t ev, uint64_t since_ns, bool* ready, std
     return BW_OK;
 }
 
+// all[2k, 2k + 1] = rank k's mine[0, 1], now (host-synchronous, deadline-bounded): the settlement
+// rounds of a file split across the ranks (bw_chunk_stream_shard).  RCCL: on the control
+// communicator and stream, after every counts exchange issued before it; host transport: the
+// caller's function.
+int bw::comm_allgather2(bw_comm* c, const uint64_t mine[2], uint64_t* all, std::string& err) {
+    if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
+    const int W = c->world;
+    std::vector<uint64_t> send(2 * W);
+    for (int k = 0; k < W; k++) {
+        send[2 * k] = mine[0];
+        send[2 * k + 1] = mine[1];
+    }
+    if (c->nccl) {
+        hipStream_t st = c->ctl_st;
+        uint64_t* ds = c->ctl_buf + 2 * W;
+        uint64_t* dr = c->ctl_buf + 4 * W;
+        if (hipMemcpyAsync(ds, send.data(), 2 * W * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+            return comm_err(c, err, "allgather staging copy failed");
+        ncclResult_t r = ncclGroupStart();
+        for (int k = 0; k < W && (r == ncclSuccess || r == ncclInProgress); k++) {
+            r = ncclSend(ds + 2 * k, 16, ncclUint8, k, c->ctl, st);
+            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv(dr + 2 * k, 16, ncclUint8, k, c->ctl, st);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r != ncclSuccess && r != ncclInProgress) return fail(c, err, std::string("allgather: ") + ncclGetErrorString(r));
+        if (int rc = settle(c, c->ctl, e, "allgather", err)) return rc;
+        hipEvent_t ev;
+        if (hipMemcpyAsync(all, dr, 2 * W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+            return comm_err(c, err, "allgather staging copy failed");
+        hipEventRecord(ev, st);
+        const int rc = comm_wait_event(c, ev, err);
+        hipEventDestroy(ev);
+        return rc;
+    }
+    if (int rc = c->host_fn(c->user, send.data(), all, 16)) {
+        c->failed = true;
+        return comm_err(c, err, "the host all-to-all returned " + std::to_string(rc) + " (communicator failed)");
+    }
+    return BW_OK;
+}
+
 uint64_t bw::comm_now_ns() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
 }
@@ -311,7 +354,7 @@ extern "C" int bw_comm_init_timeout(int device, int rank, int world, const uint8
     };
     if (hipEventCreateWithFlags(&c->tail, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->ctl_st, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->ctl_buf, 2 * world * 8) != hipSuccess)
+        hipMalloc(&c->ctl_buf, 6 * world * 8) != hipSuccess)
         return bail(BW_EHIP);
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;  // every wait below is ours, with a deadline

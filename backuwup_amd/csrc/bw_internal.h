@@ -258,6 +258,9 @@ void parallel_ranges(uint64_t n, F fn, uint64_t work = 0) {
 
 // ------------------------------------------------------------------ many small messages (bw_capi.hip)
 int ctx_device(const bw_ctx* c);
+// the blobs of batch `ticket` that bw_exchange_dedup sends to their owners: [first, first + n)
+// (default: all of them); bw_chunk_stream_shard's rank keeps only the chunks it owns
+int batch_set_exchange_range(bw_ctx* c, uint64_t ticket, uint64_t first, uint64_t n);
 // Pinned host staging owned by the context (valid until the next call that uses it).
 uint8_t* message_stage(bw_ctx* c, size_t bytes);
 // BLAKE3 of n whole messages lying in `staged` (from message_stage) at offs/lens, in one batch;
@@ -286,6 +289,8 @@ int comm_counts(bw_comm* c, hipEvent_t after, const uint64_t* d_send, uint64_t* 
 // to back in rank order); the host transport pads every section to `pad` elements.  On st.
 int comm_all_to_allv(bw_comm* c, const void* d_send, const uint64_t* scnt, void* d_recv, const uint64_t* rcnt,
                      uint64_t elem, uint64_t pad, hipStream_t st, std::string& err);
+// all[2k, 2k + 1] = rank k's mine[0, 1] (host-synchronous, deadline-bounded; control communicator)
+int comm_allgather2(bw_comm* c, const uint64_t mine[2], uint64_t* all, std::string& err);
 // bw_capi.hip: finish the queued exchanges whose counts arrived, in issue order (until = null: those
 // ready now; else every one up to and including the exchange of slot `until`, waiting for them)
 int exchange_progress(bw_comm* c, const void* until);

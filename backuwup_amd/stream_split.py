@@ -23,9 +23,12 @@ so the chunk straddling S_{r+1} is hashed by rank r+1, which holds it whole in i
 Emitted chunks in rank order are the file's chunks in offset order, i.e. canonical order for
 the digest-prefix exchange (sharded.py).
 
-The resolver is pure logic over a `chunk_fn(start, end) -> cut positions` callback: on the GPU
-it is one bw_process_files_device call over [start, end) (see `device_chunk_fn`); the
-world-size-2/4 gloo tests drive the same class.
+The product path is the C ABI's bw_chunk_stream_shard (backuwup_amd/csrc/bw_stream.hip, round 5),
+which runs these rounds in C over the communicator's control channel (RCCL or the caller's host
+transport) and hands the final chain to bw_exchange_dedup.  This module keeps the same settlement
+as pure logic over a `chunk_fn(start, end) -> cut positions` callback for the world-size-2/4 gloo
+tests (the tests' CPU chunker stands in for the device) and for driving several ranks' windows
+from one process (`device_chunk_fn`).
 """
 import numpy as np
 
@@ -36,6 +39,7 @@ def split_bounds(file_len, world):
 
 
 def window(file_len, rank, world, max_size):
+    """[lo, hi): rank's part of the file in HBM (bw_stream_window computes the same)."""
     s = split_bounds(file_len, world)
     return max(0, s[rank] - max_size), min(file_len, s[rank + 1] + max_size)
 

@@ -360,6 +360,35 @@ int bw_exchange_dedup(bw_ctx* ctx, bw_comm* comm, uint64_t ticket);
 /* Finish the queued exchanges whose counts have arrived (never waits).  BW_ECOMM once aborted. */
 int bw_comm_progress(bw_comm* comm);
 
+/* ---- one long file split across the ranks (SURVEY.md §8e "single long stream") ----
+ * The reference chunks a file serially from its start (a new FastCDC per file, dir_packer.rs:254-266);
+ * here the W ranks of a communicator chunk one file together.  Rank r owns the file bytes [S_r,
+ * S_{r+1}), S_k = file_len * k / W, and holds its window [lo, hi) (bw_stream_window: the owned range
+ * widened by max_size on both sides, clipped to the file) in HBM.  bw_chunk_stream_shard chunks and
+ * hashes the window from a speculative start and settles with the other ranks (rounds of a 16-byte
+ * allgather on the communicator's control communicator; random data settles in one round, data with
+ * no content-defined cut in at most W + 1) where each rank's true chain enters: the chunks every rank
+ * emits are, in rank order, exactly FastCDC::new(file, min, avg, max)'s chunks (boundaries, Chunk.hash
+ * and digests), the chunk straddling a split hashed once, by the rank after it.
+ * out->ticket names the batch (in ctx's ring, submitted with BW_F_NO_DEDUP) that holds this rank's
+ * final chain: bw_wait(ticket) returns the chain's blobs with offsets relative to out->chain_start,
+ * of which [first_blob, first_blob + n_blobs) are the ones this rank emits; bw_exchange_dedup(ctx,
+ * comm, ticket) sends only those to their owners.  d_window = file byte lo in device memory, any
+ * alignment (the library may read up to 15 bytes before it, inside its 16-byte granule).  Every rank
+ * calls it for the same file at the same point in its sequence of calls on the communicator; it
+ * returns once the ranks settled (host-synchronous, deadline-bounded like every wait on peers). */
+typedef struct bw_stream_shard {
+    uint64_t ticket;      /* batch holding this rank's final chain                             */
+    uint64_t first_blob;  /* the chunks this rank emits: blobs [first_blob, first_blob + n_blobs) */
+    uint64_t n_blobs;
+    uint64_t chain_start; /* file offset where the chain starts (its blobs' offsets count from it) */
+    uint32_t rounds;      /* settlement rounds                                                  */
+    uint32_t pad;
+} bw_stream_shard;
+int bw_stream_window(uint64_t file_len, int rank, int world, uint32_t max_size, uint64_t* lo, uint64_t* hi);
+int bw_chunk_stream_shard(bw_ctx* ctx, bw_comm* comm, const uint8_t* d_window, uint64_t file_len,
+                          const bw_params* params, bw_stream_shard* out);
+
 /* ---- tree blobs: split_serialize_tree + add_tree_to_blobs, dir_packer.rs:314-390 ----
  * Tree { kind: TreeKind, name: String, metadata: TreeMetadata { size, mtime, ctime: Option<u64> },
  *        children: Vec<BlobHash>, next_sibling: Option<BlobHash> }   (filesystem/mod.rs:63-77)

@@ -109,6 +109,17 @@ pub mod ffi {
     }
 
     #[repr(C)]
+    #[derive(Clone, Copy, Debug, Default)]
+    pub struct bw_stream_shard {
+        pub ticket: u64,
+        pub first_blob: u64,
+        pub n_blobs: u64,
+        pub chain_start: u64,
+        pub rounds: u32,
+        pub pad: u32,
+    }
+
+    #[repr(C)]
     #[derive(Clone, Copy, Debug)]
     pub struct bw_tree_blob {
         pub tree: u64,
@@ -222,6 +233,10 @@ pub mod ffi {
         pub fn bw_comm_set_capacity(comm: *mut bw_comm, cap: u64) -> c_int;
         pub fn bw_exchange_dedup(ctx: *mut bw_ctx, comm: *mut bw_comm, ticket: u64) -> c_int;
         pub fn bw_comm_progress(comm: *mut bw_comm) -> c_int;
+        pub fn bw_stream_window(file_len: u64, rank: c_int, world: c_int, max_size: u32, lo: *mut u64,
+                                hi: *mut u64) -> c_int;
+        pub fn bw_chunk_stream_shard(ctx: *mut bw_ctx, comm: *mut bw_comm, d_window: *const u8, file_len: u64,
+                                     params: *const bw_params, out: *mut bw_stream_shard) -> c_int;
 
         pub fn bw_tree_serialize(tree: *const bw_tree, next_sibling: *const u8, out: *mut u8, cap: u64,
                                  n_out: *mut u64) -> c_int;
@@ -447,6 +462,19 @@ impl Context {
     }
 
     /// Batch `ticket` (submitted with `BW_F_NO_DEDUP`) through the digest-prefix exchange.
+    /// One long file split across the ranks of `comm` (a VM image on every GPU of the node):
+    /// `window` is this rank's part of it in HBM, file bytes `[lo, hi)` of
+    /// `bw_stream_window(file_len, rank, world, max_size)`.  Returns the batch holding this
+    /// rank's final chain and the range of its blobs this rank emits; in rank order the emitted
+    /// chunks are `FastCDC::new(file, ..)`'s (dir_packer.rs:254-266).  Follow with
+    /// `exchange_dedup(comm, shard.ticket)` and `wait(shard.ticket)`.
+    pub fn chunk_stream_shard(&mut self, comm: &Comm, d_window: *const u8, file_len: u64, params: &ffi::bw_params)
+                              -> Result<ffi::bw_stream_shard> {
+        let mut out = ffi::bw_stream_shard::default();
+        self.check(unsafe { ffi::bw_chunk_stream_shard(self.raw, comm.raw, d_window, file_len, params, &mut out) })?;
+        Ok(out)
+    }
+
     pub fn exchange_dedup(&mut self, comm: &Comm, ticket: u64) -> Result<()> {
         let rc = unsafe { ffi::bw_exchange_dedup(self.raw, comm.raw, ticket) };
         if rc == ffi::BW_ECOMM {

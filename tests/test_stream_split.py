@@ -135,3 +135,96 @@ def test_split_on_device_matches_serial(ctx, oracle, kind, n, world):
     assert [(s, l) for s, l, _ in got] == [(o, l) for _, o, l in want]
     for s, l, d in got[:: max(1, len(got) // 12)]:
         assert d == oracle.blake3(data[s:s + l])
+
+
+# ------------------------------------------------------------------ bw_chunk_stream_shard (C ABI)
+# the settlement behind the C ABI, over a communicator (the caller's host transport
+# here: two processes share the one GPU, which RCCL refuses), followed by bw_exchange_dedup of the
+# emitted range.  Every rank's emitted chunks, in rank order, equal the serial oracle's chunks of the
+# whole file (boundaries, Chunk.hash, digests), and the verdicts equal one global index.
+BK = (262144, 1048576, 3145728)
+SHARD_CASES = [("random", 24 << 20, BK), ("zeros", 14 << 20, BK), ("periodic", 9 << 20, BK),
+               ("random", 300 << 10, BK),  # shorter than one chunk per rank
+               ("random", 300000, SMALL), ("zeros", 200000, SMALL), ("random", 0, BK)]
+
+
+def _shard_worker(rank, world, port, q):
+    import torch
+    from backuwup_amd import Context, make_params
+    from backuwup_amd.comm import Comm, gloo_all_to_all
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = []
+        with Context(0) as c, Comm.host(0, rank, world, gloo_all_to_all()) as comm:
+            c.index_reset(1 << 14)
+            for kind, n, params in SHARD_CASES:
+                data = make_file(kind, n)
+                lo, hi = ss.window(n, rank, world, params[2])
+                win = torch.from_numpy(data[lo:hi].copy()).cuda() if hi > lo else None
+                torch.cuda.synchronize()
+                p = make_params(*params)
+                sh = c.chunk_stream_shard(comm, win.data_ptr() + 0 if win is not None else 0, n, p)
+                if sh["ticket"]:
+                    c.exchange_dedup(comm, sh["ticket"])
+                    res = c.wait(sh["ticket"])
+                    mine = res[sh["first_blob"]:sh["first_blob"] + sh["n_blobs"]]
+                    out.append([(int(sh["chain_start"] + b["offset"]), int(b["length"]), int(b["gear_hash"]),
+                                 bytes(b["digest"]), int(b["is_dup"])) for b in mine] + [("rounds", sh["rounds"])])
+                else:
+                    out.append([("rounds", sh["rounds"])])
+            c.index_check()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2])
+def test_stream_shard_c_abi_two_ranks_one_gpu(world, oracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ix = oracle.Index()  # one backup session: the files in order, each in offset order
+    for c, (kind, n, params) in enumerate(SHARD_CASES):
+        data = make_file(kind, n)
+        chunks = [b for r in range(world) for b in got[r][c] if b[0] != "rounds"]
+        rounds = max(dict([b for b in got[r][c] if b[0] == "rounds"])["rounds"] for r in range(world))
+        if n == 0:
+            assert chunks == []
+            continue
+        want = oracle.process_files(data, [0], [n], *params, small_threshold=0, index=ix)
+        assert [(s, l) for s, l, _, _, _ in chunks] == [(int(o), int(l)) for o, l in zip(want["offset"], want["length"])], (kind, n)
+        assert [g for _, _, g, _, _ in chunks] == [int(x) for x in want["gear_hash"]], (kind, n)
+        assert [d for _, _, _, d, _ in chunks] == [bytes(x) for x in want["digest"]], (kind, n)
+        assert [v for _, _, _, _, v in chunks] == [int(x) for x in want["is_dup"]], (kind, n)
+        if kind == "random" and n > (1 << 20):
+            assert rounds == 1
+        if kind == "zeros":
+            assert rounds >= 2  # the true phase travels from rank 0
+
+
+@pytest.mark.gpu
+def test_stream_shard_c_abi_rccl_world1(ctx, oracle):
+    """World size 1 over RCCL: the settlement is one round, the emitted chunks are the whole file."""
+    import torch
+    from backuwup_amd import make_params
+    from backuwup_amd.comm import Comm, unique_id
+    data = make_file("random", 7 << 20)
+    win = torch.from_numpy(data).cuda()
+    torch.cuda.synchronize()
+    with Comm.rccl(0, 0, 1, unique_id()) as comm:
+        ctx.index_reset(1 << 12)
+        sh = ctx.chunk_stream_shard(comm, win.data_ptr(), data.size, make_params())
+        ctx.exchange_dedup(comm, sh["ticket"])
+        res = ctx.wait(sh["ticket"])
+    want = oracle.process_files(data, [0], [data.size], small_threshold=0)
+    assert sh["rounds"] == 1 and sh["first_blob"] == 0 and sh["n_blobs"] == len(want) == len(res)
+    assert np.array_equal(res["offset"], want["offset"]) and np.array_equal(res["digest"], want["digest"])

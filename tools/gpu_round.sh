@@ -54,9 +54,11 @@ for s in $STEPS; do
     debug) step debug_check 600 python tools/debug_check.py ;;
     exch)  # round 5: the exactly sized, deferred exchange (host transport + RCCL world 1) and the bench's
            # exchange path at world size 1
-      step exch_tests 600 python -u -m pytest tests/test_gpu_pipeline.py -m gpu -k "exchange or shard" -v \
-        -p no:cacheprovider --timeout 300 --timeout-method thread &&
-      step bench_exch 600 python bench.py --exchange --steps 60 --no-cpu-baseline ;;
+      step exch_tests 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_stream_split.py tests/test_gpu_parity.py \
+        -m gpu -k "exchange or shard or split or dropin or coalesced" -v -p no:cacheprovider --timeout 300 \
+        --timeout-method thread &&
+      step bench_exch 600 python bench.py --exchange --steps 60 --no-cpu-baseline &&
+      step bench_split 600 python bench.py --workload c3 --gib 1 --split-files --steps 5 ;;
     zsdiag)  # diagnostic zstd variants: section timers (BW_ZSTD_TIMING) and the step fences dropped
              # (build first: python backuwup_amd/build.py --ztime; build(variant="zsnofence", defines=("-DBW_ZS_NOFENCE",)))
       step zstd_ztime 600 env BW_LIB="$GRAFT_REPO_ROOT/backuwup_amd/libbackuwup_amd_ztime.so" python tools/zstd_bench.py \
