@@ -195,7 +195,8 @@ struct bw_ctx {
     // asynchronous zstd (bw_zstd_submit_device / bw_zstd_wait): each lane runs one batch on its own
     // stream and hash tables, driven by a library thread through the batch's host round trips
     struct ZsLane {
-        hipStream_t st = nullptr;
+        hipStream_t st = nullptr;      // the stream the lane's batch runs on (own_st or the context's)
+        hipStream_t own_st = nullptr;  // created on first use by a lane that runs on a stream of its own
         hipEvent_t ready = nullptr;  // the context stream's work before the submit
         ZstdWork* w = nullptr;
         std::thread th;
@@ -649,7 +650,7 @@ extern "C" void bw_destroy(bw_ctx* c) {
                      &c->ex_rbk, &c->ex_v, &c->ex_rv};
     for (auto& L : c->zs_lanes) {  // batches still in flight finish first
         if (L.th.joinable()) L.th.join();
-        if (L.st && &L != &c->zs_lanes[0]) hipStreamDestroy(L.st);
+        if (L.own_st) hipStreamDestroy(L.own_st);  // (lane 0's own stream leaked)
         if (L.ready) hipEventDestroy(L.ready);
         zstd_work_free(L.w);
         L.w = nullptr;
@@ -2289,11 +2290,14 @@ extern "C" int bw_zstd_submit_device(bw_ctx* c, const uint8_t* d_src, const uint
     }
     hipSetDevice(c->device);
     if (own) {
-        if (!L->st) HIPCHK(c, hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking));
+        if (!L->own_st) HIPCHK(c, hipStreamCreateWithFlags(&L->own_st, hipStreamNonBlocking));
         if (!L->ready) HIPCHK(c, hipEventCreateWithFlags(&L->ready, hipEventDisableTiming));
         HIPCHK(c, hipEventRecord(L->ready, c->stream));
-        HIPCHK(c, hipStreamWaitEvent(L->st, L->ready, 0));
+        HIPCHK(c, hipStreamWaitEvent(L->own_st, L->ready, 0));
+        L->st = L->own_st;
     } else {
+        // lane 0 on the context's stream: its library thread synchronizes that stream, so work the
+        // caller queues there after this submit is waited for too (include/backuwup_gpu.h)
         L->st = c->stream;
     }
     zstd_work_copy_limits(L->w, c->zw);  // the context's BW_OPT_ZSTD_* limits

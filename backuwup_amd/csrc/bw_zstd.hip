@@ -47,8 +47,10 @@ constexpr uint32_t HL_MAX = 17, HS_MAX = 16;
 // A table entry holds a position AND the bytes the match test compares at it (src is immutable,
 // so they are exactly what a load at that position would return): a probe answers the candidate
 // test by itself, one memory round per step fewer than libzstd's position-only tables.  Long
-// table: 16 B {pos, 0, 8 bytes}; short table: 8 B {pos, 4 bytes}.  2.5 MiB per slot.
+// table: 16 B {pos, 0, 8 bytes}; short table: 8 B {pos, 4 bytes}.  2.5 MiB per slot.  The narrow
+// layout (libzstd's u32 positions) takes 768 KiB per slot; each layout has a pool of its own.
 constexpr uint64_t SLOT_WORDS = (1ull << HL_MAX) * 4 + (1ull << HS_MAX) * 2;
+constexpr uint64_t NARROW_WORDS = (1ull << HL_MAX) + (1ull << HS_MAX);
 constexpr uint32_t SEC_HDR = 256;  // sequence-section scratch: header bytes, then the bitstream
 constexpr uint32_t HUF_HDR_CAP = 256;  // table descriptions libzstd keeps are < 129 bytes
 constexpr uint32_t MAXLL = 35, MAXML = 52, MAXOFF = 31, DEFAULT_MAXOFF = 28;
@@ -523,7 +525,7 @@ __device__ void parse_blob(const uint8_t* __restrict__ src, ZBlob* __restrict__ 
                            uint32_t* s_cu, unsigned long long* s_v8) {
     const uint32_t lane = threadIdx.x;
     const uint8_t* s = src + B.src;
-    const ZTab<WIDE> T(tables + (uint64_t)B.slot * SLOT_WORDS);
+    const ZTab<WIDE> T(tables + (uint64_t)B.slot * (WIDE ? SLOT_WORDS : NARROW_WORDS));
     const uint32_t ib = B.base + 1;  // index of s[0] (libzstd: dictLimit)
     const uint32_t hlog = B.hlog, clog = B.clog, maxD = 1u << B.wlog;
     const uint32_t mls = MLS ? MLS : B.mls;  // MLS 0: any length, switched at run time
@@ -1733,15 +1735,19 @@ bool dgrow(DBuf& b, size_t bytes, hipStream_t st, std::string& err) {
 }  // namespace
 
 struct ZstdWork {
-    DBuf blobs, blocks, hist, huf_use, huf_hdr, seqs, lits, sec, tables, active, rerun;
-    std::vector<uint32_t> next_base;  // per slot: the index base its next use starts from
-    std::vector<uint8_t> layout;      // per slot: 0 zero-filled, 1 narrow, 2 wide (a switch clears it)
-    uint32_t n_slots = 0;
-    uint64_t max_slots = 16384;        // hash-table slots (2.5 MiB each): blobs parsed at once
+    DBuf blobs, blocks, hist, huf_use, huf_hdr, seqs, lits, sec, active, rerun;
+    // hash-table slot pools, one per layout (a pool at the wide stride cost 3.3x the memory
+    // of the narrow tables that many-blob sub-batches use): [0] narrow, 768 KiB per slot, up to
+    // max_slots; [1] wide, 2.5 MiB per slot, up to ZS_WIDE_MAX_BLOBS
+    DBuf tables[2];
+    std::vector<uint32_t> next_base[2];  // per slot: the index base its next use starts from
+    uint32_t n_slots[2] = {0, 0};
+    uint64_t max_slots = 16384;        // blobs parsed at once
     uint64_t max_bytes = 8ull << 30;   // input bytes per sub-batch (scratch ~4.2 x this)
     uint32_t* h_rerun = nullptr;       // pinned
     ~ZstdWork() {
-        for (DBuf* b : {&blobs, &blocks, &hist, &huf_use, &huf_hdr, &seqs, &lits, &sec, &tables, &active, &rerun})
+        for (DBuf* b : {&blobs, &blocks, &hist, &huf_use, &huf_hdr, &seqs, &lits, &sec, &tables[0], &tables[1], &active,
+                        &rerun})
             if (b->p) hipFree(b->p);
         if (h_rerun) hipHostFree(h_rerun);
     }
@@ -1800,21 +1806,22 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
         uint64_t i1 = i0, bytes = 0;
         while (i1 < n && i1 - i0 < w->max_slots && (i1 == i0 || bytes + src_len[i1] <= w->max_bytes)) bytes += src_len[i1++];
         const uint32_t nb = (uint32_t)(i1 - i0);
-        if (nb > w->n_slots) {
-            // grow the slot pool (fresh slots are zero: every entry reads as empty)
-            DBuf nt;
-            if (!dgrow(nt, (size_t)nb * SLOT_WORDS * 4, st, err)) return BW_ENOMEM;
-            if (hipMemsetAsync(nt.p, 0, nt.cap, st) != hipSuccess) { err = "hipMemsetAsync failed"; return BW_EHIP; }
-            if (w->tables.p) { hipStreamSynchronize(st); hipFree(w->tables.p); }
-            w->tables = nt;
-            w->n_slots = (uint32_t)(nt.cap / (SLOT_WORDS * 4));
-            w->next_base.assign(w->n_slots, 0);
-            w->layout.assign(w->n_slots, 0);
-        }
         // wide table entries for sub-batches of few blobs (one wave per SIMD: latency-bound), narrow
         // ones when the blobs fill the SIMDs several times over (measured: wide +3 % on 836 blobs of
         // 1 GiB of text, -1..-9 % on 6,808 blobs of 8 GiB; profiles/r04/s10_zsfat, s13_zsab8)
         const bool wide = nb <= ZS_WIDE_MAX_BLOBS;
+        const int L = wide ? 1 : 0;
+        const uint64_t stride = (wide ? SLOT_WORDS : NARROW_WORDS) * 4;
+        if (nb > w->n_slots[L]) {
+            // grow the layout's slot pool (fresh slots are zero: every entry reads as empty)
+            DBuf nt;
+            if (!dgrow(nt, (size_t)nb * stride, st, err)) return BW_ENOMEM;
+            if (hipMemsetAsync(nt.p, 0, nt.cap, st) != hipSuccess) { err = "hipMemsetAsync failed"; return BW_EHIP; }
+            if (w->tables[L].p) { hipStreamSynchronize(st); hipFree(w->tables[L].p); }
+            w->tables[L] = nt;
+            w->n_slots[L] = (uint32_t)(nt.cap / stride);
+            w->next_base[L].assign(w->n_slots[L], 0);
+        }
         hb.resize(nb);
         hk.clear();
         uint64_t seqCap = 0, litCap = 0, secCap = 0;
@@ -1830,17 +1837,15 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
             B.nblocks = (uint32_t)((len + BLOCK - 1) / BLOCK);
             B.slot = j;
             // index range of this use, with room for every rerun (one block flips per rerun)
-            uint32_t& nbase = w->next_base[j];
+            uint32_t& nbase = w->next_base[L][j];
             const uint64_t need = (uint64_t)(B.nblocks + 2) * (len + 2);
-            uint8_t& lay = w->layout[j];
-            const uint8_t want = wide ? 2 : 1;
-            if ((uint64_t)nbase + need >= 0xFFFFFF00ull || (lay && lay != want)) {  // (a switch: the other
-                                                                                     // layout's words are no entries)
-                if (hipMemsetAsync(w->tables.p ? (uint8_t*)w->tables.p + (uint64_t)j * SLOT_WORDS * 4 : nullptr, 0,
-                                   SLOT_WORDS * 4, st) != hipSuccess) { err = "hipMemsetAsync failed"; return BW_EHIP; }
+            if ((uint64_t)nbase + need >= 0xFFFFFF00ull) {  // the index space of the slot is used up: clear it
+                if (hipMemsetAsync((uint8_t*)w->tables[L].p + (uint64_t)j * stride, 0, stride, st) != hipSuccess) {
+                    err = "hipMemsetAsync failed";
+                    return BW_EHIP;
+                }
                 nbase = 0;
             }
-            lay = want;
             B.base = nbase;
             nbase += (uint32_t)need;
             for (uint32_t k = 0; k < B.nblocks; k++) {
@@ -1882,7 +1887,7 @@ int zstd_compress(hipStream_t st, ZstdWork*& w, const uint8_t* d_src, const uint
             if (pass > 32) { err = "zstd: decisions did not converge"; return BW_ESTATE; }
             hipMemsetAsync(dR, 0, 4, st);
             if (nBlocks) {
-                hipLaunchKernelGGL(k_zs_parse, dim3(nBlobs), dim3(64), 0, st, d_src, dB, dK, (uint32_t*)w->tables.p,
+                hipLaunchKernelGGL(k_zs_parse, dim3(nBlobs), dim3(64), 0, st, d_src, dB, dK, (uint32_t*)w->tables[L].p,
                                    (uint64_t*)w->seqs.p, blobList, (int)wide);
                 hipLaunchKernelGGL(k_zs_stats, dim3((uint32_t)nBlocks), dim3(ST_THREADS), 0, st, d_src, dB, dK,
                                    (const uint64_t*)w->seqs.p, (uint8_t*)w->lits.p, (uint8_t*)w->sec.p,

@@ -195,7 +195,8 @@ enum {
                                     2 = aligned 128-byte lines through registers (k_b3_lines, default) */
     BW_OPT_SCAN_WAVES = 6,       /* gear-scan workgroup: 16 waves (default) or 8 (leaves LDS for BLAKE3) */
     BW_OPT_LATENCY_STREAM = 7,   /* 1: the small kernels between the passes on a high-priority stream */
-    BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (2.5 MiB of hash tables each; 16384) */
+    BW_OPT_ZSTD_SLOTS = 8,       /* bw_zstd_*: blobs compressed at once (16384); hash tables 768 KiB per blob,
+                                    2.5 MiB per blob in sub-batches of at most 2,048 blobs */
     BW_OPT_ZSTD_BATCH_BYTES = 9, /* bw_zstd_*: input bytes per internal batch (~4.2x in scratch; 8 GiB) */
     BW_OPT_ORDER_HASH = 10,      /* 1: the scans and the BLAKE3 leaf passes of the contexts sharing an
                                     index run one at a time each, in submission order (a batch's scan
@@ -511,8 +512,11 @@ int bw_zstd_compress(bw_ctx* ctx, const uint8_t* src, const uint64_t* src_off, c
  * one of the context's BW_ZSTD_LANES lanes (each its own hash tables and a stream of its own,
  * ordered after the work already on the context's stream; with fewer than BW_ZSTD_LANES + 2
  * hardware queues per process -- HIP's GPU_MAX_HW_QUEUES, 4 by default -- the first lane runs on
- * the context's stream instead) and returns at once with *ticket; BW_ESTATE when every
- * lane holds a batch (wait for one first).  d_src and d_dst stay untouched by the caller until
+ * the context's stream instead, so its bw_zstd_wait also waits for whatever the caller queued on
+ * that stream after the submit) and returns at once with *ticket; BW_ESTATE when every lane holds
+ * a batch (wait for one first).  Hash tables: per lane, 768 KiB per blob for sub-batches of more
+ * than 2,048 blobs and 2.5 MiB per blob for smaller ones (two pools, each grown to the largest
+ * sub-batch of its layout seen: at most BW_OPT_ZSTD_SLOTS x 768 KiB + 2,048 x 2.5 MiB).  d_src and d_dst stay untouched by the caller until
  * bw_zstd_wait(ticket), which blocks for the batch and writes its n frame sizes to frame_len. */
 #define BW_ZSTD_LANES 3
 int bw_zstd_submit_device(bw_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
