@@ -1962,6 +1962,10 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
         c->err = "ticket " + std::to_string(ticket) + " is not (or no longer) held by the context";
         return BW_ESTATE;
     }
+    if (comm_failed(comm)) {
+        c->err = "the communicator was aborted by an earlier failure";
+        return BW_ECOMM;
+    }
     if (s->dedup || s->ex_state) {
         c->err = "the batch was gated already (submit it with BW_F_NO_DEDUP and exchange it once)";
         return BW_ESTATE;
@@ -1986,30 +1990,35 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     int rc = 0;
     rc |= ensure(c, s->ex_dig, max_n * 32);
     rc |= ensure(c, s->ex_perm, max_n * 8);
-    rc |= ensure(c, s->ex_msg, 2 * W * 8 + 8);
+    rc |= ensure(c, s->ex_msg, 4 * W * 8 + 8);  // [0, 2W) sent, [2W, 4W) received, [4W] a range's length
     rc |= ensure(c, c->bk_blk, (nblk + 1) * W * 8);
     if (rc) return BW_ENOMEM;
     if (int r = ensure_host(c, s->ex_h, 4 * W * 8 + 8)) return r;
+    uint64_t* msg = P<uint64_t>(s->ex_msg);
+    uint64_t* h = (uint64_t*)s->ex_h.p;
     const uint64_t* d_n = slot_ctr(*s) + C_NBLOBS;
     if (ranged) {  // the range's length as a device count (pinned source: the copy is asynchronous)
-        uint64_t* hn = (uint64_t*)s->ex_h.p + 4 * W;
-        *hn = max_n;
-        HIPCHK(c, hipMemcpyAsync(P<uint64_t>(s->ex_msg) + 2 * W, hn, 8, hipMemcpyHostToDevice, c->stream));
-        d_n = P<uint64_t>(s->ex_msg) + 2 * W;
+        h[4 * W] = max_n;
+        HIPCHK(c, hipMemcpyAsync(msg + 4 * W, h + 4 * W, 8, hipMemcpyHostToDevice, c->stream));
+        d_n = msg + 4 * W;
     }
     launch_owner_partition(c->stream, P<uint8_t>(s->digests) + (ranged ? 32 * s->ex_first : 0), d_n, max_n, W,
-                           P<uint8_t>(s->ex_dig), P<uint64_t>(s->ex_perm), P<uint64_t>(s->ex_msg),
-                           P<uint64_t>(c->bk_blk));
+                           P<uint8_t>(s->ex_dig), P<uint64_t>(s->ex_perm), msg, P<uint64_t>(c->bk_blk));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(s->ex_part, c->stream));
     s->comm = comm;
     s->ex_since = comm_now_ns();
     s->ex_rc = 0;
     bool now = false;
-    if (int r = comm_counts(comm, s->ex_part, P<uint64_t>(s->ex_msg), (uint64_t*)s->ex_h.p, s->ex_ready, &now, c->err)) {
+    if (int r = comm_counts(comm, msg, msg + 2 * W, h, c->stream, &now, c->err)) {
         s->ex_state = 3;
         s->ex_rc = r;
         return r;
+    }
+    if (!now) {  // RCCL: the counts to the slot's pinned buffer by a kernel behind the all-to-all
+        launch_copy_u64(c->stream, msg, h, 4 * W);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(s->ex_ready, c->stream));
     }
     s->ex_now = now;
     s->ex_state = 1;

@@ -50,6 +50,8 @@ struct bw_comm {
     // communicator running at once on one GPU can wait on each other forever.
     hipEvent_t tail = nullptr;
     hipStream_t tail_stream = nullptr;
+    hipEvent_t ctl_tail = nullptr;  // likewise for the control communicator (counts, allgathers)
+    hipStream_t ctl_tail_stream = nullptr;
     std::string err;
 };
 
@@ -79,6 +81,16 @@ int fail(bw_comm* c, std::string& err, const std::string& what) {
 
 Clock::time_point deadline_of(const bw_comm* c) { return Clock::now() + std::chrono::milliseconds(c->timeout_ms); }
 
+// Between two polls of a wait on the GPU or the peers: yield for the first 2 ms (an exchange's
+// counts or an RCCL enqueue normally settle within tens of microseconds, and the batch pipeline
+// waits for them), then sleep 50 us.
+void pace(Clock::time_point since) {
+    if (Clock::now() - since < std::chrono::milliseconds(2))
+        std::this_thread::yield();
+    else
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+}
+
 // An error reported by either communicator (ncclInProgress = still enqueuing, not an error).
 ncclResult_t async_state(bw_comm* c) {
     for (ncclComm_t k : {c->nccl, c->ctl}) {
@@ -93,7 +105,7 @@ ncclResult_t async_state(bw_comm* c) {
 // A non-blocking call returned r: wait (to the deadline) until communicator k has finished it.
 int settle(bw_comm* c, ncclComm_t k, ncclResult_t r, const char* what, std::string& err) {
     if (r != ncclSuccess && r != ncclInProgress) return fail(c, err, std::string(what) + ": " + ncclGetErrorString(r));
-    const auto dl = deadline_of(c);
+    const auto t0 = Clock::now(), dl = deadline_of(c);
     for (;;) {
         ncclResult_t s = ncclSuccess;
         if (ncclCommGetAsyncError(k, &s) != ncclSuccess) return fail(c, err, std::string(what) + ": async state");
@@ -101,7 +113,7 @@ int settle(bw_comm* c, ncclComm_t k, ncclResult_t r, const char* what, std::stri
         if (s != ncclInProgress) return fail(c, err, std::string(what) + ": " + ncclGetErrorString(s));
         if (Clock::now() > dl)
             return fail(c, err, std::string(what) + ": no progress within " + std::to_string(c->timeout_ms) + " ms");
-        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        pace(t0);
     }
 }
 
@@ -117,8 +129,8 @@ bool bw::comm_failed(const bw_comm* c) { return c->failed; }
 // event and the communicators' async error state until the deadline; aborts on either.
 int bw::comm_wait_event(bw_comm* c, hipEvent_t ev, std::string& err) {
     if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
-    const auto dl = deadline_of(c);
-    for (uint32_t spin = 0;; spin++) {
+    const auto t0 = Clock::now(), dl = deadline_of(c);
+    for (;;) {
         const hipError_t q = hipEventQuery(ev);
         if (q == hipSuccess) return BW_OK;
         if (q != hipErrorNotReady) return fail(c, err, std::string("hipEventQuery: ") + hipGetErrorString(q));
@@ -130,43 +142,40 @@ int bw::comm_wait_event(bw_comm* c, hipEvent_t ev, std::string& err) {
         if (Clock::now() > dl)
             return fail(c, err, "a collective did not complete within " + std::to_string(c->timeout_ms) +
                                     " ms (a peer failed or stalled)");
-        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(100));
+        pace(t0);
     }
 }
 
 // The per-exchange counts (16 bytes per rank, include/backuwup_gpu.h bw_exchange_dedup): d_send[2r, 2r+1]
-// goes to rank r; h[0, 2W) = d_send, h[2W, 4W) = what every rank sent here.  RCCL: on the control
-// communicator and its own stream, after `after` (the partition that wrote d_send), without host
-// synchronization; `ready` is recorded behind the copies into h, and the data-path operations of
-// the exchange are enqueued once it fired (bw_capi.hip, exchange_progress).  The control
-// communicator is a split of the data one, so a later exchange's counts never queue behind an
-// earlier exchange's transfers on the data communicator, which wait for the host.  Host transport:
-// synchronous, *now = true.
-int bw::comm_counts(bw_comm* c, hipEvent_t after, const uint64_t* d_send, uint64_t* h, hipEvent_t ready, bool* now,
+// goes to rank r, d_recv[2k, 2k+1] = what rank k sent here.  RCCL: on the control communicator,
+// enqueued on st right behind the partition that wrote d_send (no host synchronization); the
+// control communicator's operations wait for each other across streams like the data ones.  It is
+// a split of the data communicator, so a later exchange's counts never queue behind an earlier
+// exchange's transfers, which are enqueued once the host has read those counts
+// (bw_capi.hip, exchange_progress).  Host transport: synchronous through pinned h (4 x world u64:
+// [0, 2W) sent, [2W, 4W) received), *now = true.
+int bw::comm_counts(bw_comm* c, const uint64_t* d_send, uint64_t* d_recv, uint64_t* h, hipStream_t st, bool* now,
                     std::string& err) {
     if (c->failed) return comm_err(c, err, "the communicator was aborted by an earlier failure");
     const int W = c->world;
     *now = false;
     if (c->nccl) {
-        hipStream_t st = c->ctl_st;
-        if (hipStreamWaitEvent(st, after, 0) != hipSuccess) return comm_err(c, err, "hipStreamWaitEvent failed");
+        if (c->ctl_tail_stream && c->ctl_tail_stream != st && hipStreamWaitEvent(st, c->ctl_tail, 0) != hipSuccess)
+            return comm_err(c, err, "hipStreamWaitEvent on the control communicator's last operation failed");
         ncclResult_t r = ncclGroupStart();
         for (int k = 0; k < W && (r == ncclSuccess || r == ncclInProgress); k++) {
             r = ncclSend(d_send + 2 * k, 16, ncclUint8, k, c->ctl, st);
-            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv(c->ctl_buf + 2 * k, 16, ncclUint8, k, c->ctl, st);
+            if (r == ncclSuccess || r == ncclInProgress) r = ncclRecv(d_recv + 2 * k, 16, ncclUint8, k, c->ctl, st);
         }
         const ncclResult_t e = ncclGroupEnd();
         if (r != ncclSuccess && r != ncclInProgress)
             return fail(c, err, std::string("counts all-to-all: ") + ncclGetErrorString(r));
         if (int rc = settle(c, c->ctl, e, "counts all-to-all", err)) return rc;
-        if (hipMemcpyAsync(h, d_send, 2 * W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipMemcpyAsync(h + 2 * W, c->ctl_buf, 2 * W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipEventRecord(ready, st) != hipSuccess)
-            return comm_err(c, err, "counts staging copy failed");
+        if (hipEventRecord(c->ctl_tail, st) != hipSuccess) return comm_err(c, err, "hipEventRecord failed");
+        c->ctl_tail_stream = st;
         return BW_OK;
     }
-    if (hipEventSynchronize(after) != hipSuccess ||
-        hipMemcpy(h, d_send, 2 * W * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(h, d_send, 2 * W * 8, hipMemcpyDeviceToHost) != hipSuccess)
         return comm_err(c, err, "counts staging copy (device to host) failed");
     if (int rc = c->host_fn(c->user, h, h + 2 * W, 16)) {
         c->failed = true;
@@ -214,6 +223,8 @@ int bw::comm_allgather2(bw_comm* c, const uint64_t mine[2], uint64_t* all, std::
     }
     if (c->nccl) {
         hipStream_t st = c->ctl_st;
+        if (c->ctl_tail_stream && c->ctl_tail_stream != st && hipStreamWaitEvent(st, c->ctl_tail, 0) != hipSuccess)
+            return comm_err(c, err, "hipStreamWaitEvent on the control communicator's last operation failed");
         uint64_t* ds = c->ctl_buf + 2 * W;
         uint64_t* dr = c->ctl_buf + 4 * W;
         if (hipMemcpyAsync(ds, send.data(), 2 * W * 8, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -226,6 +237,8 @@ int bw::comm_allgather2(bw_comm* c, const uint64_t mine[2], uint64_t* all, std::
         const ncclResult_t e = ncclGroupEnd();
         if (r != ncclSuccess && r != ncclInProgress) return fail(c, err, std::string("allgather: ") + ncclGetErrorString(r));
         if (int rc = settle(c, c->ctl, e, "allgather", err)) return rc;
+        if (hipEventRecord(c->ctl_tail, st) != hipSuccess) return comm_err(c, err, "hipEventRecord failed");
+        c->ctl_tail_stream = st;
         hipEvent_t ev;
         if (hipMemcpyAsync(all, dr, 2 * W * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
@@ -353,6 +366,7 @@ extern "C" int bw_comm_init_timeout(int device, int rank, int world, const uint8
         return rc;
     };
     if (hipEventCreateWithFlags(&c->tail, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ctl_tail, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->ctl_st, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->ctl_buf, 6 * world * 8) != hipSuccess)
         return bail(BW_EHIP);
@@ -407,6 +421,7 @@ extern "C" void bw_comm_destroy(bw_comm* c) {
         *k = nullptr;
     }
     if (c->tail) hipEventDestroy(c->tail);
+    if (c->ctl_tail) hipEventDestroy(c->ctl_tail);
     if (c->ctl_st) hipStreamDestroy(c->ctl_st);
     if (c->ctl_buf) hipFree(c->ctl_buf);
     if (c->pin_send) hipHostFree(c->pin_send);

@@ -386,6 +386,15 @@ void launch_owner_partition(hipStream_t st, const uint8_t* digests, const uint64
                            n_owners, shift, FLAT, blk, out, perm);
 }
 
+__global__ void k_copy_u64(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+void launch_copy_u64(hipStream_t st, const uint64_t* src, uint64_t* dst, uint32_t n) {
+    if (n) hipLaunchKernelGGL(k_copy_u64, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n);
+}
+
 // Verdicts of my owner sections (partition order) back to blob order, into is_dup and the records.
 __global__ void k_owner_scatter(const uint8_t* __restrict__ verdict, const uint64_t* __restrict__ perm, uint64_t n,
                                 uint8_t* __restrict__ is_dup, uint8_t* __restrict__ packed) {

@@ -200,6 +200,8 @@ void launch_index_snapshot(hipStream_t st, const uint64_t* dstate, uint64_t* ctr
 // msg[2o] = digests for owner o, msg[2o + 1] = the largest section; blk as for the buckets
 void launch_owner_partition(hipStream_t st, const uint8_t* digests, const uint64_t* n_dev, uint64_t max_n,
                             uint32_t n_owners, uint8_t* out, uint64_t* perm, uint64_t* msg, uint64_t* blk);
+// n u64 from device memory into device-accessible pinned host memory, by a kernel on st
+void launch_copy_u64(hipStream_t st, const uint64_t* src, uint64_t* dst, uint32_t n);
 // is_dup[perm[i]] = verdict[i] (and the records' is_dup byte, packed may be null), i < n
 void launch_owner_scatter(hipStream_t st, const uint8_t* verdict, const uint64_t* perm, uint64_t n, uint8_t* is_dup,
                           uint8_t* packed);
@@ -281,9 +283,10 @@ uint64_t comm_now_ns();
 int comm_wait_event(bw_comm* c, hipEvent_t ev, std::string& err);
 // one non-blocking look at ev (enqueued at since_ns): *ready, or BW_ECOMM past the deadline
 int comm_poll(bw_comm* c, hipEvent_t ev, uint64_t since_ns, bool* ready, std::string& err);
-// the exchange's counts, 16 B per rank: h[0, 2W) = d_send, h[2W, 4W) = received (pinned host);
-// RCCL: asynchronous after `after`, `ready` recorded behind it; host transport: synchronous, *now
-int comm_counts(bw_comm* c, hipEvent_t after, const uint64_t* d_send, uint64_t* h, hipEvent_t ready, bool* now,
+// the exchange's counts, 16 B per rank: d_recv[2k, 2k + 1] = rank k's d_send[2r, 2r + 1].  RCCL:
+// enqueued on st (the caller stages d_send/d_recv to the host and records its event); host
+// transport: synchronous, h[0, 2W) = d_send, h[2W, 4W) = received, *now = true
+int comm_counts(bw_comm* c, const uint64_t* d_send, uint64_t* d_recv, uint64_t* h, hipStream_t st, bool* now,
                 std::string& err);
 // variable all-to-all of elem-byte elements: scnt[k] to rank k, rcnt[k] from rank k (sections back
 // to back in rank order); the host transport pads every section to `pad` elements.  On st.
