@@ -734,6 +734,103 @@ void launch_b3_calib(hipStream_t st, uint32_t n_blocks, uint32_t blocks_per_lane
 
 uint32_t b3_calib_blocks_per_cu() { return BW_B3_LINES_MINW; }
 
+// ---- small whole messages straight from pinned host memory (bw_blake3_hash's coalesced batches:
+// the reference's per-file and per-tree blake3::hash calls, dir_packer.rs:286, :320).  One wave per
+// message of <= 64 leaves (64 KiB), one workgroup each.  The wave first pulls the whole message
+// from the caller-side pinned staging into LDS with every lane's 16-byte loads in flight at once
+// (over PCIe: one round of latency instead of one per 64-byte block), then lane i compresses leaf
+// i from LDS, and the leaves merge into the left-balanced tree level by level in registers (pairs
+// from the left, an odd last node carried up: the tree whose left subtree is the largest power of
+// two), ROOT on the last merge or on a single leaf.  offs / lens and the digests live in the same
+// pinned staging: a batch is one launch and one synchronization.  In LDS the 16-byte word w of
+// leaf c sits at c * 1024 + ((w ^ c) & 63) * 16, so the 64 lanes reading word w of their own
+// leaves spread over the banks instead of all hitting one (a 1 KiB stride).
+__device__ __forceinline__ uint32_t msg_lds_at(uint32_t byte) {
+    const uint32_t c = byte >> 10, w = (byte >> 4) & 63;
+    return (c << 10) | (((w ^ c) & 63) << 4) | (byte & 15);
+}
+
+__global__ __launch_bounds__(64) void k_b3_msgs(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
+                                                const uint64_t* __restrict__ lens, uint8_t* __restrict__ out) {
+    extern __shared__ uint4 s_msg[];  // the message, swizzled (whole 1 KiB leaves), zero-padded to 64-byte blocks
+    uint8_t* lds = (uint8_t*)s_msg;
+    const uint32_t msg = blockIdx.x, lane = threadIdx.x;
+    const uint64_t off = offs[msg];
+    const uint32_t len = (uint32_t)lens[msg];
+    const uint32_t len64 = len == 0 ? 64 : (len + 63) & ~63u;  // (an empty message is one zero block)
+    // 16-byte aligned; data == nullptr: offs holds absolute addresses (the callers' pinned copies)
+    const uint4* src = (const uint4*)((uintptr_t)data + off);
+    const uint32_t nw = len64 / 16;
+    // eight 16-byte loads per lane in flight before any is stored: a 64 KiB message is eight rounds
+    // of PCIe latency, not 64
+    for (uint32_t i0 = lane; i0 < nw; i0 += 8 * 64) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t i = i0 + 64 * k;
+            v[k] = i < nw && i * 16 < len ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t i = i0 + 64 * k;
+            if (i >= nw) break;
+            if (i * 16 + 16 > len && i * 16 < len) {  // the word holding the message's end: zero past it
+                uint32_t* w = (uint32_t*)&v[k];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t b0 = i * 16 + 4 * q;
+                    if (b0 >= len) w[q] = 0;
+                    else if (b0 + 4 > len) w[q] &= (1u << (8 * (len - b0))) - 1;
+                }
+            }
+            *(uint4*)(lds + msg_lds_at(i * 16)) = v[k];
+        }
+    }
+    __syncthreads();
+    uint32_t m = len == 0 ? 1 : (len + B3_LEAF_BYTES - 1) / B3_LEAF_BYTES;  // leaves (<= 64)
+    uint32_t cv[8];
+    b3_iv(cv);
+    if (lane < m) {
+        const uint32_t ll = len - lane * B3_LEAF_BYTES < B3_LEAF_BYTES ? len - lane * B3_LEAF_BYTES : B3_LEAF_BYTES;
+        const uint32_t nblk = ll == 0 ? 1 : (ll + 63) / 64;
+        for (uint32_t blk = 0; blk < nblk; blk++) {
+            uint32_t mw[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint4 v = *(const uint4*)(lds + msg_lds_at(lane * B3_LEAF_BYTES + blk * 64 + 16 * q));
+                mw[4 * q] = v.x;
+                mw[4 * q + 1] = v.y;
+                mw[4 * q + 2] = v.z;
+                mw[4 * q + 3] = v.w;
+            }
+            const uint32_t left = ll - blk * 64;
+            uint32_t flags = blk == 0 ? B3_CHUNK_START : 0;
+            if (blk == nblk - 1) flags |= B3_CHUNK_END | (m == 1 ? B3_ROOT : 0);
+            b3_compress(cv, mw, left < 64 ? left : 64, lane, flags);
+        }
+    }
+    while (m > 1) {  // one level: node j <- parent(2j, 2j + 1), or node 2j itself when it is the odd last
+        uint32_t a[8], b[8];
+        b3_shfl8(cv, (int)(2 * lane) & 63, a);
+        b3_shfl8(cv, (int)(2 * lane + 1) & 63, b);
+        if (2 * lane + 1 < m) {
+            b3_parent(a, b, m == 2 ? B3_ROOT : 0, cv);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; w++) cv[w] = a[w];
+        }
+        m = (m + 1) / 2;
+    }
+    if (lane == 0) store_digest(out + 32ull * msg, cv);
+}
+
+void launch_b3_msgs(hipStream_t st, const uint8_t* data, const uint64_t* offs, const uint64_t* lens, uint32_t n,
+                    uint32_t max_len, uint8_t* out) {
+    // whole 1 KiB leaves: the swizzle moves a partial leaf's words anywhere inside its kilobyte
+    const uint32_t lds = std::max<uint32_t>(B3_LEAF_BYTES, (max_len + B3_LEAF_BYTES - 1) & ~(B3_LEAF_BYTES - 1));
+    if (n) hipLaunchKernelGGL(k_b3_msgs, dim3(n), dim3(64), lds, st, data, offs, lens, out);
+}
+
 void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, BlobArrays b, uint64_t max_blobs,
                    uint64_t max_groups, uint32_t* cv_buf, uint32_t* cv_tmp, uint8_t* digests, int max_leaves,
                    hipEvent_t between, int loads, hipStream_t upper, hipEvent_t leaf_done, hipEvent_t mark) {

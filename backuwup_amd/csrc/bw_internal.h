@@ -157,6 +157,12 @@ void launch_blake3(hipStream_t st, const uint8_t* data, const uint64_t* ctr, Blo
 // stamps[2 * block] = shader cycles, stamps[2 * block + 1] = 100 MHz ticks of wave 0.
 void launch_b3_calib(hipStream_t st, uint32_t n_blocks, uint32_t blocks_per_lane, uint32_t* sink, uint64_t* stamps);
 uint32_t b3_calib_blocks_per_cu();  // the leaf pass's occupancy (blocks of 256 per CU)
+// n whole messages of at most 64 KiB each (data + offs[i], lens[i] bytes; all three may be pinned
+// host memory, read over PCIe; offsets 16-byte aligned) -> out[32 i ..] (may be pinned host memory):
+// one wave per message, max_len = the longest (sizes the LDS)
+constexpr uint64_t B3_MSG_MAX = 65536;
+void launch_b3_msgs(hipStream_t st, const uint8_t* data, const uint64_t* offs, const uint64_t* lens, uint32_t n,
+                    uint32_t max_len, uint8_t* out);
 
 // ------------------------------------------------------------------ launchers (bw_dedup.hip)
 // Dedup state (device, persistent across batches): st[0] = log length (next seq),

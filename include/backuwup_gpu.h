@@ -131,12 +131,13 @@ void bw_fastcdc_release(uint64_t handle);
 uint64_t bw_blake3_kept_hits(void);
 
 /* blake3::hash(data) -> 32 bytes, host buffer; always hashes the bytes given.  Messages up to
- * BW_COALESCE_MAX_MSG from concurrent callers (any contexts, any threads) are coalesced: each caller
- * copies its message into the open batch's pinned staging and one launch hashes the batch (one
- * batch in flight per device; the next fills meanwhile), so N threads calling at once cost one round
- * trip, not N.  For such messages the context is only read for its device, so any number of threads
- * may pass the same context; larger messages run on the context itself (one thread at a time). */
-#define BW_COALESCE_MAX_MSG 4194304u
+ * BW_COALESCE_MAX_MSG (a small file, a tree blob) from concurrent callers (any contexts, any
+ * threads) are coalesced: each caller copies its message into pinned memory of its own, the open
+ * batch is launched as one kernel as soon as one of the device's four lanes is free (the next batch
+ * fills meanwhile), so N threads calling at once cost a few round trips, not N.  For such messages
+ * the context is only read for its device, so any number of threads may pass the same context;
+ * larger messages run on the context itself (one thread at a time). */
+#define BW_COALESCE_MAX_MSG 65536u
 int bw_blake3_hash(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
 /* The Rust blake3::hash drop-in's entry (dir_packer.rs:286, :320, :353): as bw_blake3_hash, except
  * that a chunk slice of a live bw_fastcdc_chunks_hashed source is answered from its kept digest.

@@ -35,7 +35,7 @@ pub mod ffi {
     pub const BW_OK: c_int = 0;
     pub const BW_EINVAL: c_int = -1;
     pub const BW_ENOSPC: c_int = -2;
-    pub const BW_COALESCE_MAX_MSG: u64 = 4_194_304;
+    pub const BW_COALESCE_MAX_MSG: u64 = 65_536;
     pub const BW_EHIP: c_int = -3;
     pub const BW_ENOMEM: c_int = -4;
     pub const BW_ECOLLISION: c_int = -5;

@@ -555,9 +555,11 @@ def test_coalesced_hash_many_threads(oracle):
     from backuwup_amd import Context, _lib
     L = _lib.load()
     rng = np.random.default_rng(5)
-    lens = rng.integers(0, 70 << 10, 4000)
+    lens = rng.integers(0, 64 << 10, 4000)  # the one-wave-per-message kernel (<= 64 KiB)
     lens[::7] = rng.integers(60, 140, len(lens[::7]))  # tree-blob sized
-    lens[:3] = [0, 1, 1024]
+    lens[::97] = rng.integers(64 << 10, 200 << 10, len(lens[::97]))  # above 64 KiB: through the caller's context
+    edges = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 3071, 3072, 4097, 32768, 65535, 65536, 65537]
+    lens[:len(edges)] = edges
     blob = splitmix_bytes(31, int(lens.sum()) + 64)
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
     want = [oracle.blake3(blob[o:o + n]) for o, n in zip(offs, lens)]
@@ -566,6 +568,8 @@ def test_coalesced_hash_many_threads(oracle):
     b0, m0 = ctypes.c_uint64(), ctypes.c_uint64()
     L.bw_blake3_coalesce_stats(0, ctypes.byref(b0), ctypes.byref(m0))
     ctxs = [Context(0) for _ in range(4)]  # 16 threads over 4 contexts: small messages only name the device
+    for i in range(len(edges)):  # alone: a batch of one message each, either path
+        assert ctxs[0].blake3_at(blob, int(offs[i]), int(lens[i])) == want[i], lens[i]
 
     def worker(t):
         try:
@@ -585,5 +589,6 @@ def test_coalesced_hash_many_threads(oracle):
     assert got == want
     b1, m1 = ctypes.c_uint64(), ctypes.c_uint64()
     L.bw_blake3_coalesce_stats(0, ctypes.byref(b1), ctypes.byref(m1))
-    assert m1.value - m0.value == len(lens)
+    small = int(np.sum(lens <= 65536)) + sum(1 for e in edges if e <= 65536)  # larger: the caller's context
+    assert m1.value - m0.value == small
     assert b1.value - b0.value < len(lens)  # some launches carried several callers' messages
