@@ -95,7 +95,9 @@ def build(force=False, verbose=False, debug=False, jobs=8, variant=None, defines
 
 
 if __name__ == "__main__":
-    if "--ztime" in sys.argv:  # zstd parse section timers (tools/zstd_bench.py --timing)
+    if "--clock" in sys.argv:  # clock stamps around scan tiles and leaf-pass waves (tools/clock_windows.py)
+        print(build(force="--force" in sys.argv, verbose=True, variant="clock", defines=("-DBW_CLOCK_STAMPS=1",)))
+    elif "--ztime" in sys.argv:  # zstd parse section timers (tools/zstd_bench.py --timing)
         print(build(force="--force" in sys.argv, verbose=True, variant="ztime", defines=("-DBW_ZSTD_TIMING",)))
     else:
         print(build(force="--force" in sys.argv, verbose=True, debug="--debug" in sys.argv))

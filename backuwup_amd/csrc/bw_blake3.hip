@@ -19,6 +19,11 @@
 #include "bw_internal.h"
 
 namespace bw {
+#if BW_CLOCK_STAMPS
+__device__ ClockLog* g_clk_b3 = nullptr;
+void clock_log_register_b3(void* log) { hipMemcpyToSymbol(HIP_SYMBOL(g_clk_b3), &log, sizeof(log)); }
+#endif
+
 
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
@@ -358,6 +363,9 @@ __global__ __launch_bounds__(256, MINW) void k_b3_lines(const uint8_t* __restric
     // are not counted; only whole waves past it leave
     const bool live = g0 < ng;
     if (FUSED ? (ng == 0 || g0 - (threadIdx.x & 63) >= ng) : !live) return;
+#if BW_CLOCK_STAMPS
+    ClockStamp clk((blockIdx.x & 3) == 0 ? g_clk_b3 : nullptr, 1);  // the waves of one block in 4
+#endif
     const uint64_t g = live ? g0 : ng - 1;
     // (a group -> blob map written beside Chunk.hash instead of this search measured 5 % slower on
     // C1 and C2: the 30k-instruction kernel's main loop compiled worse around it, profiles/r03/s13_*)

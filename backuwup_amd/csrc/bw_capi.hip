@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/backuwup_gpu.h"
+#include "bw_device.h"
 #include "bw_internal.h"
 #include "bw_tables.inc"
 
@@ -2030,6 +2031,47 @@ extern "C" int bw_exchange_dedup(bw_ctx* c, bw_comm* comm, uint64_t ticket) {
     // the host transport delivered the counts already: finish now; RCCL: whatever is ready
     return exchange_progress(comm, now ? s : nullptr);
 }
+
+// ------------------------------------------------------------------ clock stamps (diagnostic build)
+#if BW_CLOCK_STAMPS
+namespace bw {
+void clock_log_register_cdc(void* log);
+void clock_log_register_b3(void* log);
+}
+static ClockLog* g_clock_log = nullptr;  // device: the header; its records follow it
+// (re)arm the log of `device` with room for cap records and switch stamping on or off; the kernels
+// of every context of the process stamp into it.  Not in the C ABI header: libbackuwup_amd_clock.so
+// only (tools/clock_windows.py).
+extern "C" int bw_clock_log(int device, uint64_t cap, int on) {
+    hipSetDevice(device);
+    if (!g_clock_log) {
+        if (hipMalloc(&g_clock_log, sizeof(ClockLog) + cap * sizeof(ClockRec)) != hipSuccess) return BW_ENOMEM;
+        ClockLog h{(ClockRec*)(g_clock_log + 1), cap, 0, 0};
+        if (hipMemcpy(g_clock_log, &h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) return BW_EHIP;
+        clock_log_register_cdc(g_clock_log);
+        clock_log_register_b3(g_clock_log);
+    }
+    hipDeviceSynchronize();
+    ClockLog h;
+    if (hipMemcpy(&h, g_clock_log, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return BW_EHIP;
+    if (on && !h.on) h.n = 0;  // a new window
+    h.on = on ? 1 : 0;
+    return hipMemcpy(g_clock_log, &h, sizeof h, hipMemcpyHostToDevice) == hipSuccess ? BW_OK : BW_EHIP;
+}
+// the records (40 B each: kind, pad, t0, t1 at 100 MHz, c0, c1 shader cycles); *n = logged (may
+// exceed cap: the rest were dropped)
+extern "C" int bw_clock_log_read(void* out, uint64_t cap, uint64_t* n) {
+    if (!g_clock_log || !n) return BW_ESTATE;
+    hipDeviceSynchronize();
+    ClockLog h;
+    if (hipMemcpy(&h, g_clock_log, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return BW_EHIP;
+    *n = h.n;
+    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(h.n, h.cap), cap);
+    if (k && out && hipMemcpy(out, g_clock_log + 1, k * sizeof(ClockRec), hipMemcpyDeviceToHost) != hipSuccess)
+        return BW_EHIP;
+    return BW_OK;
+}
+#endif
 
 // ------------------------------------------------------------------ stage timing API
 

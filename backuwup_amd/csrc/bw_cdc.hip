@@ -28,6 +28,11 @@
 #include "bw_internal.h"
 
 namespace bw {
+#if BW_CLOCK_STAMPS
+__device__ ClockLog* g_clk_cdc = nullptr;
+void clock_log_register_cdc(void* log) { hipMemcpyToSymbol(HIP_SYMBOL(g_clk_cdc), &log, sizeof(log)); }
+#endif
+
 
 __constant__ uint64_t c_gear[256] = BW_GEAR_INIT;
 
@@ -185,6 +190,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_scan(const uint8_t* __restrict__ d
     const uint64_t nw = (uint64_t)gridDim.x * WAVES;
 
     for (uint64_t tile = (uint64_t)blockIdx.x * WAVES + wid; tile < n_tiles; tile += nw) {
+#if BW_CLOCK_STAMPS
+        ClockStamp clk((tile & 15) == 0 ? g_clk_cdc : nullptr, 0);  // one tile in 16: the stamps' atomics
+                                                                    // must not slow what they time
+#endif
         if (lane == 0) { *cnt = 0; *fcnt = 0; }
         const uint64_t base = tile * (64ull * STRIP);
         const uint64_t ss = base + (uint64_t)lane * STRIP;

@@ -167,3 +167,43 @@ __device__ __forceinline__ void b3_parent(const uint32_t l[8], const uint32_t r[
     b3_iv(out);
     b3_compress(out, m, 64, 0, B3_PARENT | flags);
 }
+
+// ---------------------------------------------------------------- clock stamps (diagnostic build)
+// BW_CLOCK_STAMPS (libbackuwup_amd_clock.so only, tools/clock_windows.py): lane 0 of a wave stamps
+// the 100 MHz real-time counter (s_memrealtime) and the shader clock counter (s_memtime) around a
+// unit of work -- a scan tile, a leaf-pass wave -- into a device log, so the clock the chip held
+// can be split by what ran beside it (what limits the overlap of the two passes).
+#ifndef BW_CLOCK_STAMPS
+#define BW_CLOCK_STAMPS 0
+#endif
+#if BW_CLOCK_STAMPS
+struct ClockRec {
+    uint32_t kind, pad;  // 0 = k_scan tile, 1 = k_b3_lines wave
+    uint64_t t0, t1, c0, c1;
+};
+struct ClockLog {
+    ClockRec* rec;
+    unsigned long long cap, n;
+    uint32_t on;
+};
+struct ClockStamp {
+    ClockLog* L;
+    uint64_t t0, c0;
+    uint32_t kind;
+    bool on;
+    __device__ ClockStamp(ClockLog* l, uint32_t k) : L(l), t0(0), c0(0), kind(k) {
+        on = L && L->on && (threadIdx.x & 63) == 0;
+        if (on) {
+            t0 = __builtin_amdgcn_s_memrealtime();
+            c0 = __builtin_amdgcn_s_memtime();
+        }
+    }
+    __device__ ~ClockStamp() {
+        if (!on) return;
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long i = atomicAdd(&L->n, 1ull);
+        if (i < L->cap) L->rec[i] = ClockRec{kind, 0, t0, t1, c0, c1};
+    }
+};
+#endif
+

@@ -52,6 +52,13 @@ for s in $STEPS; do
       step bench_c4 600 python bench.py --workload c4 --steps 60 --no-cpu-baseline &&
       step bench_c5 600 python bench.py --workload c5 --steps 3 --no-cpu-baseline ;;
     debug) step debug_check 600 python tools/debug_check.py ;;
+    attrib)  # round 5, VERDICT r4 #4: what limits the overlap of the scan and the leaf pass (build first:
+             # python backuwup_amd/build.py --clock); then the bench at the driver's 20 steps, the
+             # default 320 and 2,000 (18 s), each with its power and clock samples
+      step clock_windows 300 python tools/clock_windows.py --steps 400 --window 24 &&
+      step bench_s20 300 python bench.py --steps 20 --no-cpu-baseline --no-calibrate &&
+      step bench_s320 300 python bench.py --steps 320 --no-cpu-baseline --no-calibrate &&
+      step bench_s2000 600 python bench.py --steps 2000 --no-cpu-baseline --no-calibrate ;;
     exch)  # round 5: the exactly sized, deferred exchange (host transport + RCCL world 1) and the bench's
            # exchange path at world size 1
       step exch_tests 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_stream_split.py tests/test_gpu_parity.py \
