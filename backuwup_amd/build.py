@@ -15,19 +15,22 @@ LIB = os.path.join(HERE, "libbackuwup_amd.so")
 # only when BW_LIB points at it (tools/debug_check.py), never by the product path
 LIB_DEBUG = os.path.join(HERE, "libbackuwup_amd_debug.so")
 SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_comm.hip", "bw_tree.hip", "bw_seal.hip",
-           "bw_pack.hip", "bw_zstd.hip", "bw_dropin.hip", "bw_stream.hip"]
+           "bw_pack.hip", "bw_zstd.hip", "bw_dropin.hip", "bw_stream.hip", "bw_capi_pack.hip"]
+HEADERS = ["backuwup_gpu.h", "backuwup_gpu_pack.h"]  # include/
 ROCM_LIB = "/opt/rocm/lib"
 ARCH = os.environ.get("BW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
 # sources that are not on the chunk -> hash -> dedup path the bench profiles (their kernels never
-# run in the C2 command), so editing them does not make the committed PMC traffic stale
-OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip", "bw_comm.hip", "bw_dropin.hip", "bw_stream.hip")
+# run in the C2 command), so editing them does not make the committed PMC traffic stale; the write
+# side's C ABI (bw_capi_pack.hip, include/backuwup_gpu_pack.h) is outside the digest too
+OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip", "bw_comm.hip", "bw_dropin.hip", "bw_stream.hip",
+            "bw_capi_pack.hip")
 
 
 def source_digest():
-    """sha256 over the hot path's sources (csrc/* minus OFF_PATH, and the C ABI header): identifies
+    """sha256 over the hot path's sources (csrc/* minus OFF_PATH, and the hot path's C ABI header): identifies
     the kernels a profile was taken with (profiles/pmc_traffic.json), so bench.py can tell stale
     evidence."""
     import hashlib
@@ -46,7 +49,7 @@ def _stale(lib=LIB):
         return True
     t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
-    deps.append(os.path.join(HERE, "..", "include", "backuwup_gpu.h"))
+    deps += [os.path.join(HERE, "..", "include", h) for h in HEADERS]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
@@ -66,7 +69,7 @@ def build(force=False, verbose=False, debug=False, jobs=8, variant=None, defines
     if debug:
         flags += ["-DBW_DEBUG", "-DBW_DIAG=1", "-g"]  # asserts + the diagnostic kernel variants
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
-    headers.append(os.path.join(HERE, "..", "include", "backuwup_gpu.h"))
+    headers += [os.path.join(HERE, "..", "include", h) for h in HEADERS]
     newest_hdr = max(os.path.getmtime(h) for h in headers)
 
     def compile_one(src):

@@ -1,7 +1,8 @@
 """The Rust shim crate (rust/backuwup-gpu) against the C ABI it binds, without a Rust toolchain.
 
 There is no rustc in this image, so the crate is not compiled here.  This test reads its
-`extern "C"` block and `#[repr(C)]` structs as text and checks them against include/backuwup_gpu.h:
+`extern "C"` block and `#[repr(C)]` structs as text and checks them against include/backuwup_gpu.h (and the
+backuwup_gpu_pack.h it includes):
 every function the header declares is bound once, with the same name, arity, return type, and per
 argument the same pointer depth, constness of the pointee and integer width; every struct has the
 same fields in the same order with the same types.  The reference call sites it replaces are
@@ -11,13 +12,17 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-HEADER = os.path.join(ROOT, "include", "backuwup_gpu.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("backuwup_gpu.h", "backuwup_gpu_pack.h")]
 CRATE = os.path.join(ROOT, "rust", "backuwup-gpu")
 
 C_BASE = {"int": "i32", "uint8_t": "u8", "uint32_t": "u32", "uint64_t": "u64", "char": "i8", "double": "f64",
           "void": "void"}
 R_BASE = {"c_int": "i32", "i32": "i32", "u8": "u8", "u32": "u32", "u64": "u64", "c_char": "i8", "i8": "i8",
           "f64": "f64", "c_void": "void", "()": "void"}
+
+
+def _header_text():
+    return "\n".join(open(h).read() for h in HEADERS)
 
 
 def _strip_c_comments(txt):
@@ -53,7 +58,7 @@ def r_type(t):
 
 
 def header_functions():
-    txt = _strip_c_comments(open(HEADER).read())
+    txt = _strip_c_comments(_header_text())
     out = {}
     for m in re.finditer(r"^\s*((?:const\s+)?(?:int|void|char|uint\w+)\s*\*?)\s*(bw_\w+)\s*\(([^)]*)\)\s*;", txt,
                          re.M | re.S):
@@ -64,7 +69,7 @@ def header_functions():
 
 
 def header_structs():
-    txt = _strip_c_comments(open(HEADER).read())
+    txt = _strip_c_comments(_header_text())
     out = {}
     for m in re.finditer(r"typedef\s+struct\s+(\w+)\s*\{(.*?)\}\s*(\w+)\s*;", txt, re.S):
         fields = []
@@ -159,7 +164,7 @@ def test_structs_match_header():
 
 def test_host_transport_typedef_matches():
     """bw_host_all_to_all: int (*)(void* user, const void* send, void* recv, uint64_t bytes_per_rank)."""
-    txt = _strip_c_comments(open(HEADER).read())
+    txt = _strip_c_comments(_header_text())
     m = re.search(r"typedef\s+int\s*\(\s*\*\s*bw_host_all_to_all\s*\)\s*\(([^)]*)\)\s*;", txt)
     cparams = [c_type(p) for p in m.group(1).split(",")]
     src = crate_source()
