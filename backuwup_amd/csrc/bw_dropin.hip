@@ -24,9 +24,16 @@
 // live handle do not change (the Rust FastCDC drop-in borrows the mmap immutably for the handle's
 // lifetime).  bw_blake3_hash always hashes the bytes it is given (a rewritten buffer must
 // never be answered from an earlier chunking).
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <memory>
@@ -292,9 +299,245 @@ int coalesced_hash(Combiner* co, const uint8_t* data, uint64_t len, uint8_t out[
     return rc;
 }
 
+// ------------------------------------------------------------------ the hash service
+// The default for messages of <= 64 KiB: a persistent kernel (k_b3_service, bw_blake3.hip) whose
+// workers poll the ring of slots in pinned memory, one ticket each, and store each digest into its
+// slot over a sentinel.  A call is a copy into the caller's pinned staging, a few stores and a wait
+// on its slot: no kernel launch, no event and no library thread between the call and its digest
+// (the coalescer above pays ~20 us of launch, event and thread hand-offs per batch before the
+// kernel's own time).
+//   * Waiting: a caller spins for SVC_SPIN_US, then sleeps on a futex of its slot; one completer
+//     thread per device watches the slots of the sleeping callers and wakes each as its digest lands.
+//     With more callers than cores (tokio starts one worker per core of the machine) the spinning
+//     would otherwise take the cores the other callers need to post.
+//   * An instance ends by itself when nothing was hashed for SVC_IDLE_US, or after SVC_LIFE_US (so a
+//     device synchronization waits at most that long); a caller that finds it ended starts the next
+//     one, and a waiter without its digest checks again every millisecond, which also covers a
+//     message posted just as the workers gave up.
+//   * The stream is created with a CU mask (all CUs), which gives it a hardware queue of its own:
+//     the process's other streams never queue behind the persistent kernel (tools/dropin_lat.cpp
+//     measures a neighbour stream's launches while the service runs).
+// BW_DROPIN_SERVICE=0 in the environment selects the coalescer instead (A/B).
+constexpr uint32_t SVC_IDLE_US = 5000, SVC_LIFE_US = 100000;
+constexpr double SVC_SPIN_US = 40;
+
+long futex(std::atomic<uint32_t>* a, int op, uint32_t v, const timespec* ts = nullptr) {
+    return syscall(SYS_futex, (uint32_t*)a, op, v, ts, nullptr, 0);
+}
+
+struct Service {
+    int device = 0;
+    hipStream_t st = nullptr;
+    B3SvcSlot* ring = nullptr;  // pinned
+    B3SvcCtl* ctl = nullptr;    // pinned
+    B3SvcDev* dev = nullptr;    // device
+    uint32_t* proc = nullptr;   // device
+    std::atomic<uint64_t> next{0};
+    std::unique_ptr<std::atomic<uint64_t>[]> free_at;  // per slot: the ticket that may use it next
+    std::unique_ptr<std::atomic<uint32_t>[]> sleep;    // per slot: 1 = its caller sleeps, 2 = woken
+    std::atomic<uint32_t> sleepers{0};
+    std::atomic<uint32_t> comp_gen{0};  // the completer's futex word (bumped when a caller goes to sleep)
+    std::mutex mu;
+    std::atomic<uint32_t> epoch{0};  // the last instance launched
+    std::atomic<uint64_t> front{0};  // tickets below it have returned to their callers (under mu)
+    std::atomic<uint64_t> launches{0}, messages{0};
+};
+
+std::mutex g_svc_mu;
+Service* g_svc[64] = {};
+std::atomic<int> g_svc_mode{-1};  // -1 unknown, 0 coalescer, 1 service
+const bool g_svc_trace = getenv("BW_SVC_TRACE") != nullptr;  // diagnostics of slow calls on stderr
+
+bool service_enabled() {
+    int m = g_svc_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char* e = getenv("BW_DROPIN_SERVICE");
+        m = (e && e[0] == '0') ? 0 : 1;
+        g_svc_mode.store(m, std::memory_order_relaxed);
+    }
+    return m == 1;
+}
+
+uint32_t svc_dead(const Service* sv) { return __atomic_load_n(&sv->ctl->dead, __ATOMIC_ACQUIRE); }
+
+// the slot holds ticket t's digest: no word equals its sentinel
+inline bool svc_done(const B3SvcSlot* sl, uint64_t t, uint64_t d[4]) {
+    const uint32_t seq = (uint32_t)(t + 1);
+    for (int k = 0; k < 4; k++) {
+        d[k] = __atomic_load_n(&sl->digest[k], __ATOMIC_ACQUIRE);
+        if (d[k] == b3svc_sentinel(seq, k)) return false;
+    }
+    return true;
+}
+
+// start an instance unless one is running (the last launched has not published its end)
+int svc_ensure(Service* sv) {
+    const uint32_t e = sv->epoch.load(std::memory_order_acquire);
+    if (e != 0 && svc_dead(sv) != e) return BW_OK;
+    std::lock_guard<std::mutex> lk(sv->mu);
+    const uint32_t e2 = sv->epoch.load(std::memory_order_relaxed);
+    if (e2 != 0 && svc_dead(sv) != e2) return BW_OK;
+    hipSetDevice(sv->device);
+    (void)hipGetLastError();  // (clear an earlier call's error on this thread)
+    // the first ticket not yet returned to its caller: the new instance reserves from there
+    uint64_t lo = sv->front.load(std::memory_order_relaxed);
+    const uint64_t hi = sv->next.load(std::memory_order_acquire);
+    while (lo < hi && sv->free_at[lo % B3_SVC_RING].load(std::memory_order_acquire) > lo) lo++;
+    sv->front.store(lo, std::memory_order_relaxed);
+    launch_b3_service(sv->st, sv->ring, sv->ctl, sv->dev, sv->proc, e2 + 1, (uint32_t)lo, SVC_IDLE_US, SVC_LIFE_US);
+    if (const hipError_t e = hipGetLastError()) {
+        if (g_svc_trace) fprintf(stderr, "[bw svc] launch failed: %s\n", hipGetErrorString(e));
+        return BW_EHIP;
+    }
+    sv->epoch.store(e2 + 1, std::memory_order_release);
+    sv->launches.fetch_add(1, std::memory_order_relaxed);
+    if (g_svc_trace) fprintf(stderr, "[bw svc] launched epoch %u\n", e2 + 1);
+    return BW_OK;
+}
+
+// wakes the sleeping callers whose digests landed; sleeps itself while no caller sleeps
+void svc_completer(Service* sv) {
+    uint64_t lo = 0;  // tickets below lo have returned to their callers
+    for (;;) {
+        const uint32_t gen = sv->comp_gen.load(std::memory_order_acquire);
+        if (sv->sleepers.load(std::memory_order_acquire) == 0) {
+            futex(&sv->comp_gen, FUTEX_WAIT_PRIVATE, gen);
+            continue;
+        }
+        const uint64_t hi = sv->next.load(std::memory_order_acquire);
+        while (lo < hi && sv->free_at[lo % B3_SVC_RING].load(std::memory_order_acquire) > lo) lo++;
+        for (uint64_t t = lo; t < hi; t++) {
+            const uint32_t i = (uint32_t)(t % B3_SVC_RING);
+            uint64_t d[4];
+            if (sv->sleep[i].load(std::memory_order_acquire) == 1 && svc_done(sv->ring + i, t, d)) {
+                uint32_t one = 1;
+                if (sv->sleep[i].compare_exchange_strong(one, 2)) futex(&sv->sleep[i], FUTEX_WAKE_PRIVATE, 1);
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// process exit: end the running instance and wait (bounded) for its grid to drain
+void svc_atexit() {
+    for (int d = 0; d < 64; d++)
+        if (Service* sv = g_svc[d]) {
+            __atomic_store_n(&sv->ctl->stop, 1u, __ATOMIC_RELEASE);
+            hipSetDevice(d);
+            // (an instance ends within microseconds of the stop word, or at its life limit)
+            for (int i = 0; i < 4000 && hipStreamQuery(sv->st) == hipErrorNotReady; i++) usleep(500);
+        }
+}
+
+Service* service(int device) {
+    if (device < 0 || device >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(g_svc_mu);
+    if (!g_svc[device]) {
+        auto* sv = new Service();  // lives as long as the process
+        sv->device = device;
+        hipSetDevice(device);
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+            return nullptr;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
+        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1;
+        if (hipExtStreamCreateWithCUMask(&sv->st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+        if (hipHostMalloc((void**)&sv->ring, sizeof(B3SvcSlot) * B3_SVC_RING, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&sv->ctl, sizeof(B3SvcCtl), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void**)&sv->dev, sizeof(B3SvcDev)) != hipSuccess ||
+            hipMalloc((void**)&sv->proc, sizeof(uint32_t) * B3_SVC_RING) != hipSuccess)
+            return nullptr;
+        memset(sv->ring, 0, sizeof(B3SvcSlot) * B3_SVC_RING);
+        memset(sv->ctl, 0, sizeof(B3SvcCtl));
+        if (hipMemset(sv->dev, 0, sizeof(B3SvcDev)) != hipSuccess ||
+            hipMemset(sv->proc, 0, sizeof(uint32_t) * B3_SVC_RING) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            return nullptr;
+        sv->free_at.reset(new std::atomic<uint64_t>[B3_SVC_RING]);
+        sv->sleep.reset(new std::atomic<uint32_t>[B3_SVC_RING]);
+        for (uint32_t i = 0; i < B3_SVC_RING; i++) {
+            sv->free_at[i].store(i);
+            sv->sleep[i].store(0);
+        }
+        std::thread(svc_completer, sv).detach();
+        static std::once_flag once;
+        std::call_once(once, [] { atexit(svc_atexit); });
+        g_svc[device] = sv;
+    }
+    return g_svc[device];
+}
+
+int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    TlStage& ts = t_stage;
+    if (ts.cap < len + 16) {  // this thread's pinned copy of its message
+        if (ts.p) hipHostFree(ts.p);
+        ts.p = nullptr;
+        ts.cap = 0;
+        const uint64_t want = std::max<uint64_t>(65536 + 64, len + 16);
+        if (hipHostMalloc((void**)&ts.p, want, hipHostMallocDefault) != hipSuccess) return BW_ENOMEM;
+        ts.cap = want;
+    }
+    if (len) memcpy(ts.p, data, len);
+    const uint64_t t = sv->next.fetch_add(1, std::memory_order_relaxed);
+    const uint32_t i = (uint32_t)(t % B3_SVC_RING), seq = (uint32_t)(t + 1);
+    while (sv->free_at[i].load(std::memory_order_acquire) != t) std::this_thread::yield();  // (a full ring)
+    B3SvcSlot* sl = sv->ring + i;
+    for (int k = 0; k < 4; k++) __atomic_store_n(&sl->digest[k], b3svc_sentinel(seq, k), __ATOMIC_RELAXED);
+    __atomic_store_n(&sl->ptr, (uint64_t)(uintptr_t)ts.p, __ATOMIC_RELAXED);
+    __atomic_store_n(&sl->lenseq, len | ((uint64_t)seq << 32), __ATOMIC_RELEASE);
+    int rc = svc_ensure(sv);
+    uint64_t d[4];
+    if (rc == BW_OK && !svc_done(sl, t, d)) {
+        const auto t0 = std::chrono::steady_clock::now();
+        auto us_now = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); };
+        bool ok = false;
+        for (uint32_t it = 0; !ok; it++) {  // spin
+            __builtin_ia32_pause();
+            if (svc_done(sl, t, d)) ok = true;
+            else if ((it & 63) == 63 && us_now() > SVC_SPIN_US) break;
+        }
+        if (!ok) {  // sleep until the completer wakes this slot; re-check the instance every millisecond
+            sv->sleep[i].store(1, std::memory_order_release);
+            sv->sleepers.fetch_add(1, std::memory_order_acq_rel);
+            sv->comp_gen.fetch_add(1, std::memory_order_acq_rel);
+            futex(&sv->comp_gen, FUTEX_WAKE_PRIVATE, 1);
+            double next_trace = 2000;
+            while (!svc_done(sl, t, d)) {
+                const timespec ts1 = {0, 1000000};
+                if (sv->sleep[i].load(std::memory_order_acquire) == 1) futex(&sv->sleep[i], FUTEX_WAIT_PRIVATE, 1, &ts1);
+                if (svc_done(sl, t, d)) break;
+                sv->sleep[i].store(1, std::memory_order_release);  // (woken early, or a timeout)
+                const double us = us_now();
+                if ((rc = svc_ensure(sv)) != BW_OK) break;
+                if (g_svc_trace && us > next_trace) {
+                    fprintf(stderr, "[bw svc] ticket %llu waiting %.0f us: epoch %u dead %u\n", (unsigned long long)t, us,
+                            sv->epoch.load(), svc_dead(sv));
+                    next_trace = us * 2;
+                }
+                if (us > 10e6) {  // ten seconds: the device is not answering
+                    if (g_svc_trace) fprintf(stderr, "[bw svc] ticket %llu: no digest after 10 s\n", (unsigned long long)t);
+                    rc = BW_EHIP;
+                    break;
+                }
+            }
+            sv->sleep[i].store(0, std::memory_order_release);
+            sv->sleepers.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    sv->messages.fetch_add(1, std::memory_order_relaxed);
+    if (rc != BW_OK) return rc;  // (the slot stays taken: a late digest must not land in a reused slot)
+    memcpy(out, d, 32);
+    sv->free_at[i].store(t + B3_SVC_RING, std::memory_order_release);
+    return BW_OK;
+}
+
 int hash_one(bw_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[32]) {
-    if (len <= CO_MAX_MSG)
-        if (Combiner* co = combiner(ctx_device(c))) return coalesced_hash(co, data, len, out);
+    if (len <= CO_MAX_MSG) {
+        if (service_enabled()) {
+            if (Service* sv = service(ctx_device(c))) return service_hash(sv, data, len, out);
+        } else if (Combiner* co = combiner(ctx_device(c))) {
+            return coalesced_hash(co, data, len, out);
+        }
+    }
     const uint64_t off = 0;
     static const uint8_t empty[16] = {0};
     return bw_blake3_hash_many(c, len ? data : empty, len, &off, &len, 1, out);
@@ -375,10 +618,23 @@ extern "C" uint64_t bw_blake3_kept_hits(void) { return g_kept_hits.load(); }
 
 extern "C" int bw_blake3_coalesce_stats(int device, uint64_t* batches, uint64_t* messages) {
     if (device < 0 || device >= 64) return BW_EINVAL;
-    std::lock_guard<std::mutex> lk(g_co_mu);
-    const Combiner* co = g_co[device];
-    if (batches) *batches = co ? co->batches.load() : 0;
-    if (messages) *messages = co ? co->messages.load() : 0;
+    uint64_t b = 0, m = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_co_mu);
+        if (const Combiner* co = g_co[device]) {
+            b += co->batches.load();
+            m += co->messages.load();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_svc_mu);
+        if (const Service* sv = g_svc[device]) {
+            b += sv->launches.load();
+            m += sv->messages.load();
+        }
+    }
+    if (batches) *batches = b;
+    if (messages) *messages = m;
     return BW_OK;
 }
 
