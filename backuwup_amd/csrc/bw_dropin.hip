@@ -28,6 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <linux/futex.h>
+#include <sched.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -321,6 +322,28 @@ int coalesced_hash(Combiner* co, const uint8_t* data, uint64_t len, uint8_t out[
 constexpr uint32_t SVC_IDLE_US = 5000, SVC_LIFE_US = 100000;
 constexpr double SVC_SPIN_US = 40;
 
+// CPUs this process may run on at once: its affinity mask, capped by a cgroup v2 CPU quota (a
+// container that lends 16 of a machine's cores shows all of them in the mask).  A caller only spins
+// while fewer callers than that are waiting; past it, a spinning caller takes a core that another
+// caller needs to post its message.
+int usable_cpus() {
+    static const int n = [] {
+        cpu_set_t set;
+        int c = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 16;
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            long period = 0;
+            if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+                const long quota = atol(q);
+                if (quota > 0) c = std::min<int>(c, (int)std::max<long>(1, (quota + period - 1) / period));
+            }
+            fclose(f);
+        }
+        return std::max(1, c);
+    }();
+    return n;
+}
+
 long futex(std::atomic<uint32_t>* a, int op, uint32_t v, const timespec* ts = nullptr) {
     return syscall(SYS_futex, (uint32_t*)a, op, v, ts, nullptr, 0);
 }
@@ -336,6 +359,7 @@ struct Service {
     std::unique_ptr<std::atomic<uint64_t>[]> free_at;  // per slot: the ticket that may use it next
     std::unique_ptr<std::atomic<uint32_t>[]> sleep;    // per slot: 1 = its caller sleeps, 2 = woken
     std::atomic<uint32_t> sleepers{0};
+    std::atomic<int> waiting{0};  // callers between their post and their digest
     std::atomic<uint32_t> comp_gen{0};  // the completer's futex word (bumped when a caller goes to sleep)
     std::mutex mu;
     std::atomic<uint32_t> epoch{0};  // the last instance launched
@@ -490,7 +514,8 @@ int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]
         const auto t0 = std::chrono::steady_clock::now();
         auto us_now = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); };
         bool ok = false;
-        for (uint32_t it = 0; !ok; it++) {  // spin
+        const bool spin = sv->waiting.fetch_add(1, std::memory_order_acq_rel) < usable_cpus();
+        for (uint32_t it = 0; spin && !ok; it++) {
             __builtin_ia32_pause();
             if (svc_done(sl, t, d)) ok = true;
             else if ((it & 63) == 63 && us_now() > SVC_SPIN_US) break;
@@ -522,6 +547,7 @@ int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]
             sv->sleep[i].store(0, std::memory_order_release);
             sv->sleepers.fetch_sub(1, std::memory_order_acq_rel);
         }
+        sv->waiting.fetch_sub(1, std::memory_order_acq_rel);
     }
     sv->messages.fetch_add(1, std::memory_order_relaxed);
     if (rc != BW_OK) return rc;  // (the slot stays taken: a late digest must not land in a reused slot)
