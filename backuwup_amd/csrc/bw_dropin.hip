@@ -9,16 +9,14 @@
 //     a reader lock) with a per-thread cache of the last source hit, so callers on many threads do
 //     not serialize on one mutex and a lookup does not scan every open file.
 //   * whole-file blobs and tree blobs (dir_packer.rs:267-271 -> :286, :274 -> :320/:353): one small
-//     message per call.  Concurrent calls of at most 64 KiB from many threads are coalesced: each
-//     caller copies its message into pinned memory of its own (the copies run in parallel on the
-//     callers' threads) and adds it to the open batch; a library thread launches the open batch as
-//     soon as one of four lanes (streams) is free, and a second one waits for the launched batches
-//     and wakes their callers, so under load a batch holds what the other threads brought while the
-//     lanes were busy (group commit).  A batch is one kernel that reads the messages from the
-//     callers' pinned copies over PCIe and writes the digests into the batch's pinned table
-//     (k_b3_msgs).  Larger messages run through the caller's own context (the batch pipeline, in
-//     parallel across the callers' contexts): gathered into the one launcher thread they measured
-//     30 GB/s on C1 against 55 through the callers' own contexts.
+//     message per call.  Messages of at most 64 KiB go to the device's hash service (below): the
+//     caller copies its message into pinned memory of its own and posts it into a ring of slots that
+//     a persistent kernel's workers poll, and the digest comes back into the slot -- no launch per
+//     call.  (The round-5 coalescer, kept as the BW_DROPIN_SERVICE=0 alternative, batched concurrent
+//     calls into launches over four lanes; it paid ~20 us of launch, event and thread hand-offs per
+//     batch.)  Larger messages run through the caller's own context (the batch pipeline, in parallel
+//     across the callers' contexts): gathered into one library thread they measured 30 GB/s on C1
+//     against 55 through the callers' own contexts.
 //
 // Only bw_blake3_hash_dropin consults the kept digests: its caller guarantees that the bytes under a
 // live handle do not change (the Rust FastCDC drop-in borrows the mmap immutably for the handle's

@@ -131,19 +131,25 @@ void bw_fastcdc_release(uint64_t handle);
 uint64_t bw_blake3_kept_hits(void);
 
 /* blake3::hash(data) -> 32 bytes, host buffer; always hashes the bytes given.  Messages up to
- * BW_COALESCE_MAX_MSG (a small file, a tree blob) from concurrent callers (any contexts, any
- * threads) are coalesced: each caller copies its message into pinned memory of its own, the open
- * batch is launched as one kernel as soon as one of the device's four lanes is free (the next batch
- * fills meanwhile), so N threads calling at once cost a few round trips, not N.  For such messages
- * the context is only read for its device, so any number of threads may pass the same context;
- * larger messages run on the context itself (one thread at a time). */
+ * BW_COALESCE_MAX_MSG (a small file, a tree blob) go to the device's hash service: each caller
+ * copies its message into pinned memory of its own and posts it into a ring of slots that a
+ * persistent kernel's workers poll; the digest lands in the slot, where the caller spins briefly and
+ * then sleeps until a library thread wakes it.  No kernel launch per call: ~8 us for a tree blob,
+ * ~24 us for 16 KiB on one thread, and concurrent callers (any contexts, any threads) are served in
+ * parallel.  The service's instance ends by itself after 5 ms without messages (or 100 ms of life;
+ * the next call starts another), on a hardware queue of its own, so the process's streams never
+ * wait for it; a device-wide synchronization may wait up to that long.  BW_DROPIN_SERVICE=0 in the
+ * environment selects the earlier batching path (launches coalesced over four lanes).  For such
+ * messages the context is only read for its device, so any number of threads may pass the same
+ * context; larger messages run on the context itself (one thread at a time). */
 #define BW_COALESCE_MAX_MSG 65536u
 int bw_blake3_hash(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
 /* The Rust blake3::hash drop-in's entry (dir_packer.rs:286, :320, :353): as bw_blake3_hash, except
  * that a chunk slice of a live bw_fastcdc_chunks_hashed source is answered from its kept digest.
  * Only for callers that guarantee those bytes are unchanged while the handle lives. */
 int bw_blake3_hash_dropin(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
-/* coalesced launches and the messages they carried on `device` since the process started */
+/* launches (hash-service instances, or coalesced batches) and the messages they carried on
+ * `device` since the process started */
 int bw_blake3_coalesce_stats(int device, uint64_t* batches, uint64_t* messages);
 /* n independent messages data[offsets[i] .. offsets[i]+lengths[i]) -> out[32*i..] */
 int bw_blake3_hash_many(bw_ctx* ctx, const uint8_t* data, uint64_t data_len,

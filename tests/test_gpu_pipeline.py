@@ -748,6 +748,73 @@ def test_exchange_peer_failure_returns_ecomm():
     assert rc2 == BW_ECOMM and dt2 < 1, got[0]
 
 
+def _dying_rccl_peer_worker(rank, world, uid, q):
+    """One GPU per rank over RCCL: rank 1 leaves after the first exchange (os._exit, no goodbye);
+    rank 0's next exchange (the control communicator's counts, then the data all-to-all) must fail
+    with BW_ECOMM within the deadline, and bw_comm_destroy must return."""
+    import os
+    import time
+    import torch
+    from backuwup_amd._lib import BW_ECOMM
+    from backuwup_amd.comm import Comm
+    torch.cuda.set_device(rank)
+    data, offs, lens = small_files(800, seed=58)
+    res = []
+    with Context(rank) as c:
+        comm = Comm.rccl(rank, rank, world, uid, timeout_ms=8000)
+        c.index_reset(1 << 14)
+        for batch in range(2):
+            b = _slices(data, offs, lens, [((2 * batch + rank) * 200, (2 * batch + rank + 1) * 200)])[0]
+            t_dev = torch.from_numpy(b[0]).cuda()
+            tk = c.submit_device(t_dev.data_ptr(), b[0].size, b[1], b[2], make_params(flags=BW_F_NO_DEDUP))
+            if batch == 1 and rank == 1:
+                q.put((rank, "left"))
+                q.close()
+                q.join_thread()
+                os._exit(0)
+            t0 = time.time()
+            try:
+                c.exchange_dedup(comm, tk)
+                c.wait(tk)
+                res.append("ok")
+            except BwError as e:
+                res.append((e.rc, round(time.time() - t0, 1), comm.status()))
+        t1 = time.time()
+        comm.close()
+        res.append(round(time.time() - t1, 1))
+    q.put((rank, res))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def test_rccl_peer_failure_mid_session_returns_ecomm():
+    """RCCL with two ranks on two GPUs (skipped with fewer): a peer that dies after the first
+    exchange makes the survivor's next bw_exchange_dedup / bw_wait return BW_ECOMM within the 8 s
+    deadline (non-blocking communicators, the polled waits, ncclCommAbort), and destroying the failed
+    communicator returns promptly."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
+    import torch.multiprocessing as mp
+    from backuwup_amd._lib import BW_ECOMM
+    from backuwup_amd.comm import unique_id
+    uid = unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dying_rccl_peer_worker, args=(r, 2, uid, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got[1] == "left"
+    first, (rc, dt, status), t_close = got[0]
+    assert first == "ok"
+    assert rc == BW_ECOMM and status == BW_ECOMM and dt < 30, got[0]
+    assert t_close < 10, got[0]
+
+
 _NEVER_JOINED = """
 import sys, time
 sys.path.insert(0, %r)
