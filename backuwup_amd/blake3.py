@@ -37,8 +37,9 @@ def _immutable(data):
 
 
 def hash(data, ctx=None):  # noqa: A001 - mirrors blake3::hash
-    """blake3::hash(data) -> 32 bytes (the crate's Hash converted with .into()).  Calls from many
-    threads at once are coalesced into one launch by the library (bw_blake3_hash)."""
+    """blake3::hash(data) -> 32 bytes (the crate's Hash converted with .into()).  A message of at
+    most 64 KiB goes to the library's hash service, a persistent kernel that serves the calls of
+    every thread without a launch per call (bw_blake3_hash)."""
     buf = _as_bytes_view(data)
     ctx = ctx or default_context()
     return ctx.blake3_dropin(buf) if _immutable(data) else ctx.blake3(buf)

@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "libbackuwup_amd.so")
 # only when BW_LIB points at it (tools/debug_check.py), never by the product path
 LIB_DEBUG = os.path.join(HERE, "libbackuwup_amd_debug.so")
 SOURCES = ["bw_capi.hip", "bw_cdc.hip", "bw_blake3.hip", "bw_dedup.hip", "bw_comm.hip", "bw_tree.hip", "bw_seal.hip",
-           "bw_pack.hip", "bw_zstd.hip", "bw_dropin.hip", "bw_stream.hip", "bw_capi_pack.hip"]
+           "bw_pack.hip", "bw_zstd.hip", "bw_dropin.hip", "bw_stream.hip", "bw_capi_pack.hip", "bw_b3_small.hip"]
 HEADERS = ["backuwup_gpu.h", "backuwup_gpu_pack.h"]  # include/
 ROCM_LIB = "/opt/rocm/lib"
 ARCH = os.environ.get("BW_OFFLOAD_ARCH", "gfx950")
@@ -24,9 +24,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # sources that are not on the chunk -> hash -> dedup path the bench profiles (their kernels never
 # run in the C2 command), so editing them does not make the committed PMC traffic stale; the write
-# side's C ABI (bw_capi_pack.hip, include/backuwup_gpu_pack.h) is outside the digest too
+# side's C ABI (bw_capi_pack.hip, include/backuwup_gpu_pack.h) and the drop-ins' small-message
+# hashing (bw_b3_small.hip) are outside the digest too
 OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip", "bw_comm.hip", "bw_dropin.hip", "bw_stream.hip",
-            "bw_capi_pack.hip")
+            "bw_capi_pack.hip", "bw_b3_small.hip", "bw_b3_small.h")
 
 
 def source_digest():

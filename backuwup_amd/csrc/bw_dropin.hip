@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "bw_internal.h"
+#include "bw_b3_small.h"
 
 using namespace bw;
 

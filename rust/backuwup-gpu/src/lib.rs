@@ -626,8 +626,8 @@ impl Drop for Comm {
 // core (client/src/main.rs:43, 256 on an MI355X node), so the threads share a small pool
 // (BACKUWUP_GPU_CONTEXTS, default 16) instead of holding one context each; a thread takes the
 // first free one from its own starting point and only blocks when all are busy.  blake3::hash
-// of small messages needs none of them for long: the library coalesces concurrent calls into one
-// launch of its own (bw_blake3_hash).
+// of small messages needs none of them: it goes to the library's hash service (a persistent kernel
+// serving every thread's calls, bw_blake3_hash).
 static POOL: std::sync::OnceLock<Vec<std::sync::Mutex<Context>>> = std::sync::OnceLock::new();
 static NEXT_SLOT: std::sync::atomic::AtomicUsize = std::sync::atomic::AtomicUsize::new(0);
 thread_local! {
@@ -748,12 +748,12 @@ pub mod blake3 {
 
     /// `blake3::hash(input)` -- standard unkeyed BLAKE3, 32-byte output, computed on the GPU.  A
     /// chunk of a live `FastCDC` drop-in is answered from the digest its construction kept (safe
-    /// Rust cannot change those bytes while the `FastCDC` borrows them); concurrent calls from many
-    /// threads share one launch.
+    /// Rust cannot change those bytes while the `FastCDC` borrows them); a small message from any
+    /// thread goes to the library's hash service (no launch per call).
     pub fn hash(input: &[u8]) -> Hash {
         if input.len() as u64 <= crate::ffi::BW_COALESCE_MAX_MSG {
-            // coalesced: the library only reads the context's device, so no pool slot is held while
-            // the call waits for its batch (holding one would cap a batch at the pool's size)
+            // the hash service: the library only reads the context's device, so no pool slot is held
+            // while the call waits for its digest (holding one would cap the calls in flight)
             let raw = super::with_default(|c| c.raw);
             let mut h = [0u8; 32];
             let rc = unsafe { crate::ffi::bw_blake3_hash_dropin(raw, input.as_ptr(), input.len() as u64, h.as_mut_ptr()) };

@@ -4,7 +4,8 @@
 #      context each, and at 64 / 256 threads (tokio's default is one worker per core) with one
 #      context each and with the Rust shim's pool of 16 contexts; HBM per context.
 #   C4 (tools/dropin_c4.cpp): 1 M small files, blake3::hash of each file and of its Tree blob, at
-#      16 / 64 / 256 threads over a pool of 16 contexts (concurrent calls coalesced by the library).
+#      16 / 64 / 256 threads over a pool of 16 contexts (small calls served by the library's hash
+#      service; BW_DROPIN_SERVICE=0 selects the round-5 coalescer).
 #   CPU on the same files: bench.py's cpu_baseline (C1; C4 with --cpu-trees).
 # Build first (CPU): see the two tools' headers.  DROPIN_PARTS picks parts (default "c1 c4 cpu").
 set -o pipefail
