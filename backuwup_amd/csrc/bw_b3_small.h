@@ -14,18 +14,25 @@ void launch_b3_msgs(hipStream_t st, const uint8_t* data, const uint64_t* offs, c
                     uint32_t max_len, uint8_t* out);
 
 // The small-message hash service (bw_dropin.hip drives it): a persistent kernel whose workers take
-// messages posted into a ring of slots in pinned host memory and write each digest into its slot.
-//   host -> GPU: digest words = the ticket's sentinel (b3svc_sentinel), ptr (the message, pinned,
-//                16-byte aligned), then lenseq = len | (ticket + 1) << 32
-//   GPU -> host: the digest over the sentinel (four 8-byte stores; the host takes the slot as done
-//                once no word equals its sentinel: a digest word matches with probability 2^-64)
-struct alignas(64) B3SvcSlot {
+// messages posted into a ring of request slots and write each digest into a response slot.
+//   host -> GPU (B3SvcReq): ptr (the message, 16-byte aligned), then lenseq = len | (ticket + 1) << 32.
+//     With a large BAR the requests and the callers' message copies live in HBM (fine-grained,
+//     written by the CPU through the BAR: no PCIe read on the GPU's side); otherwise in pinned host
+//     memory.
+//   GPU -> host (B3SvcResp, pinned): the digest over the ticket's sentinel (b3svc_sentinel; four
+//     8-byte stores; the host takes the slot as done once no word equals its sentinel: a digest word
+//     matches with probability 2^-64)
+struct alignas(64) B3SvcReq {
     uint64_t lenseq;
     uint64_t ptr;
-    uint64_t pad[2];
-    uint64_t digest[4];
+    uint64_t pad[6];
 };
-static_assert(sizeof(B3SvcSlot) == 64, "one cache line per slot");
+static_assert(sizeof(B3SvcReq) == 64, "one cache line per slot");
+struct alignas(64) B3SvcResp {
+    uint64_t digest[4];
+    uint64_t pad[4];
+};
+static_assert(sizeof(B3SvcResp) == 64, "one cache line per slot");
 __host__ __device__ inline uint64_t b3svc_sentinel(uint32_t seq, int k) {
     return (0x9E3779B97F4A7C15ull * seq) ^ (0xD1B54A32D192ED03ull * (uint64_t)(k + 1));
 }
@@ -49,7 +56,7 @@ constexpr uint32_t B3_SVC_WORKERS = 64;   // workgroups of 256 (one message each
 // one instance (epoch >= 1) on st, reserving tickets from `start` on; ends when nothing was hashed for
 // idle_us, after life_us, or on ctl->stop.  proc: B3_SVC_RING words in device memory (ticket + 1 once
 // hashed)
-void launch_b3_service(hipStream_t st, B3SvcSlot* ring, B3SvcCtl* ctl, B3SvcDev* dev, uint32_t* proc,
+void launch_b3_service(hipStream_t st, B3SvcReq* req, B3SvcResp* resp, B3SvcCtl* ctl, B3SvcDev* dev, uint32_t* proc,
                        uint32_t epoch, uint32_t start, uint32_t idle_us, uint32_t life_us);
 
 }  // namespace bw

@@ -87,6 +87,12 @@ __device__ __forceinline__ void b3q_compress(uint32_t& ca, uint32_t& cb, const u
     for (int r = 0; r < 7; r++)
 #pragma unroll
         for (int k = 0; k < 4; k++) mw[r][k] = *(const uint32_t*)(blk + of.o[r][k]);
+    // all 28 reads in flight at once, one wait: left to itself the compiler waits for each round's
+    // words just before the round, exposing the LDS latency four times per compression
+#pragma unroll
+    for (int r = 0; r < 7; r++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) asm volatile("" : "+v"(mw[r][k]));
     uint32_t a = ca, b = cb, c = cj, d = dj;
 #pragma unroll
     for (int r = 0; r < 7; r++) {
@@ -215,7 +221,8 @@ void launch_b3_msgs(hipStream_t st, const uint8_t* data, const uint64_t* offs, c
 constexpr uint32_t B3Q_SVC_MSG_LDS = (uint32_t)(B3_MSG_MAX / B3_LEAF_BYTES) * B3Q_LEAF_STRIDE + 64 * 32;
 
 // ---- the small-message hash service: one persistent instance per device (bw_dropin.hip).  Callers
-// post messages into a ring of slots in pinned host memory (bw_internal.h: B3SvcSlot), one ticket
+// post messages into a ring of request slots (bw_b3_small.h: B3SvcReq; in HBM written through the
+// BAR, or in pinned host memory), one ticket
 // each.  Every worker workgroup reserves the next ticket (a fetch-add in HBM: no races between the
 // workers), polls that ticket's slot over PCIe until the caller has posted it, hashes the message
 // (b3q_message) and stores the digest over the slot's sentinel, where the caller spins.  No launch,
@@ -228,7 +235,8 @@ constexpr uint32_t B3Q_SVC_MSG_LDS = (uint32_t)(B3_MSG_MAX / B3_LEAF_BYTES) * B3
 //     out publishes the epoch in ctl->dead, and the host starts the next instance when a caller needs
 //     one.  Control flow around the barriers is wave-uniform: wave 0 polls with all its lanes (values
 //     made uniform by readfirstlane, lane 0 alone reserves), the other waves wait at the barrier.
-__global__ __launch_bounds__(256) void k_b3_service(B3SvcSlot* ring, B3SvcCtl* ctl, B3SvcDev* dev, uint32_t* proc,
+__global__ __launch_bounds__(256) void k_b3_service(B3SvcReq* req, B3SvcResp* resp, B3SvcCtl* ctl, B3SvcDev* dev,
+                                                    uint32_t* proc,
                                                     uint32_t epoch, uint32_t start, uint32_t idle_ticks,
                                                     uint32_t life_ticks) {
     extern __shared__ uint4 s_msg[];
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(256) void k_b3_service(B3SvcSlot* ring, B3SvcCtl* c
                 // not comparable to the tick), restarting whenever any worker hashed a message
                 uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
                 uint32_t seen = __hip_atomic_load(&dev->progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                B3SvcSlot* sl = ring + (t % B3_SVC_RING);
+                B3SvcReq* sl = req + (t % B3_SVC_RING);
                 bool leave = false;
                 for (uint32_t it = 0;; it++) {
                     const uint64_t h = __hip_atomic_load(&sl->lenseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(256) void k_b3_service(B3SvcSlot* ring, B3SvcCtl* c
         const uint8_t* dig = b3q_message((const uint8_t*)(uintptr_t)*s_ptr, s_w[1], (uint8_t*)s_msg, tid, 256);
         if (tid < 64) {
             if (lane < 4)  // the digest over the sentinel, 8 bytes per store (each word lands whole)
-                __hip_atomic_store(&ring[t % B3_SVC_RING].digest[lane], ((const uint64_t*)dig)[lane], __ATOMIC_RELAXED,
+                __hip_atomic_store(&resp[t % B3_SVC_RING].digest[lane], ((const uint64_t*)dig)[lane], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
             if (lane == 0) {
                 __hip_atomic_store(&proc[t % B3_SVC_RING], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -341,12 +349,12 @@ __global__ __launch_bounds__(256) void k_b3_service(B3SvcSlot* ring, B3SvcCtl* c
     }
 }
 
-void launch_b3_service(hipStream_t st, B3SvcSlot* ring, B3SvcCtl* ctl, B3SvcDev* dev, uint32_t* proc,
+void launch_b3_service(hipStream_t st, B3SvcReq* req, B3SvcResp* resp, B3SvcCtl* ctl, B3SvcDev* dev, uint32_t* proc,
                        uint32_t epoch, uint32_t start, uint32_t idle_us, uint32_t life_us) {
     static const hipError_t attr = hipFuncSetAttribute((const void*)k_b3_service,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, B3Q_SVC_MSG_LDS + 32);
     (void)attr;
-    hipLaunchKernelGGL(k_b3_service, dim3(B3_SVC_WORKERS), dim3(256), B3Q_SVC_MSG_LDS + 32, st, ring, ctl, dev, proc,
+    hipLaunchKernelGGL(k_b3_service, dim3(B3_SVC_WORKERS), dim3(256), B3Q_SVC_MSG_LDS + 32, st, req, resp, ctl, dev, proc,
                        epoch, start, idle_us * 100u, life_us * 100u);
 }
 

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <linux/futex.h>
+#include <immintrin.h>
 #include <sched.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -300,12 +301,15 @@ int coalesced_hash(Combiner* co, const uint8_t* data, uint64_t len, uint8_t out[
 }
 
 // ------------------------------------------------------------------ the hash service
-// The default for messages of <= 64 KiB: a persistent kernel (k_b3_service, bw_blake3.hip) whose
-// workers poll the ring of slots in pinned memory, one ticket each, and store each digest into its
-// slot over a sentinel.  A call is a copy into the caller's pinned staging, a few stores and a wait
-// on its slot: no kernel launch, no event and no library thread between the call and its digest
-// (the coalescer above pays ~20 us of launch, event and thread hand-offs per batch before the
-// kernel's own time).
+// The default for messages of <= 64 KiB: a persistent kernel (k_b3_service, bw_b3_small.hip) whose
+// workers poll a ring of request slots, one ticket each, and store each digest into a response slot
+// in pinned memory over a sentinel.  With a large BAR (every MI355X host) the caller copies its
+// message and writes its request straight into HBM through the BAR (fine-grained device memory;
+// ~40 GB/s for a 64 KiB copy), so the GPU never reads over PCIe: a 64 KiB call went from 37 to 24 us.
+// A call is a copy, a few stores and a wait on its slot: no kernel launch, no event and no library
+// thread between the call and its digest (the coalescer above pays ~20 us of launch, event and
+// thread hand-offs per batch before the kernel's own time).  BW_SVC_HOST_RING=1 keeps the requests
+// and copies in pinned host memory.
 //   * Waiting: a caller spins for SVC_SPIN_US, then sleeps on a futex of its slot; one completer
 //     thread per device watches the slots of the sleeping callers and wakes each as its digest lands.
 //     With more callers than cores (tokio starts one worker per core of the machine) the spinning
@@ -350,7 +354,9 @@ long futex(std::atomic<uint32_t>* a, int op, uint32_t v, const timespec* ts = nu
 struct Service {
     int device = 0;
     hipStream_t st = nullptr;
-    B3SvcSlot* ring = nullptr;  // pinned
+    B3SvcReq* req = nullptr;    // HBM through the BAR (vram), else pinned
+    B3SvcResp* resp = nullptr;  // pinned
+    bool vram = false;          // requests and message copies in HBM, written by the CPU (large BAR)
     B3SvcCtl* ctl = nullptr;    // pinned
     B3SvcDev* dev = nullptr;    // device
     uint32_t* proc = nullptr;   // device
@@ -384,7 +390,7 @@ bool service_enabled() {
 uint32_t svc_dead(const Service* sv) { return __atomic_load_n(&sv->ctl->dead, __ATOMIC_ACQUIRE); }
 
 // the slot holds ticket t's digest: no word equals its sentinel
-inline bool svc_done(const B3SvcSlot* sl, uint64_t t, uint64_t d[4]) {
+inline bool svc_done(const B3SvcResp* sl, uint64_t t, uint64_t d[4]) {
     const uint32_t seq = (uint32_t)(t + 1);
     for (int k = 0; k < 4; k++) {
         d[k] = __atomic_load_n(&sl->digest[k], __ATOMIC_ACQUIRE);
@@ -407,7 +413,8 @@ int svc_ensure(Service* sv) {
     const uint64_t hi = sv->next.load(std::memory_order_acquire);
     while (lo < hi && sv->free_at[lo % B3_SVC_RING].load(std::memory_order_acquire) > lo) lo++;
     sv->front.store(lo, std::memory_order_relaxed);
-    launch_b3_service(sv->st, sv->ring, sv->ctl, sv->dev, sv->proc, e2 + 1, (uint32_t)lo, SVC_IDLE_US, SVC_LIFE_US);
+    launch_b3_service(sv->st, sv->req, sv->resp, sv->ctl, sv->dev, sv->proc, e2 + 1, (uint32_t)lo, SVC_IDLE_US,
+                      SVC_LIFE_US);
     if (const hipError_t e = hipGetLastError()) {
         if (g_svc_trace) fprintf(stderr, "[bw svc] launch failed: %s\n", hipGetErrorString(e));
         return BW_EHIP;
@@ -432,7 +439,7 @@ void svc_completer(Service* sv) {
         for (uint64_t t = lo; t < hi; t++) {
             const uint32_t i = (uint32_t)(t % B3_SVC_RING);
             uint64_t d[4];
-            if (sv->sleep[i].load(std::memory_order_acquire) == 1 && svc_done(sv->ring + i, t, d)) {
+            if (sv->sleep[i].load(std::memory_order_acquire) == 1 && svc_done(sv->resp + i, t, d)) {
                 uint32_t one = 1;
                 if (sv->sleep[i].compare_exchange_strong(one, 2)) futex(&sv->sleep[i], FUTEX_WAKE_PRIVATE, 1);
             }
@@ -465,12 +472,19 @@ Service* service(int device) {
         std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
         if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1;
         if (hipExtStreamCreateWithCUMask(&sv->st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
-        if (hipHostMalloc((void**)&sv->ring, sizeof(B3SvcSlot) * B3_SVC_RING, hipHostMallocDefault) != hipSuccess ||
+        int large_bar = 0;
+        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device);
+        const char* hr = getenv("BW_SVC_HOST_RING");
+        sv->vram = large_bar && !(hr && hr[0] == '1');
+        if ((sv->vram ? hipExtMallocWithFlags((void**)&sv->req, sizeof(B3SvcReq) * B3_SVC_RING, hipDeviceMallocFinegrained)
+                      : hipHostMalloc((void**)&sv->req, sizeof(B3SvcReq) * B3_SVC_RING, hipHostMallocDefault)) != hipSuccess ||
+            hipHostMalloc((void**)&sv->resp, sizeof(B3SvcResp) * B3_SVC_RING, hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void**)&sv->ctl, sizeof(B3SvcCtl), hipHostMallocDefault) != hipSuccess ||
             hipMalloc((void**)&sv->dev, sizeof(B3SvcDev)) != hipSuccess ||
             hipMalloc((void**)&sv->proc, sizeof(uint32_t) * B3_SVC_RING) != hipSuccess)
             return nullptr;
-        memset(sv->ring, 0, sizeof(B3SvcSlot) * B3_SVC_RING);
+        memset(sv->resp, 0, sizeof(B3SvcResp) * B3_SVC_RING);
+        if (hipMemset(sv->req, 0, sizeof(B3SvcReq) * B3_SVC_RING) != hipSuccess) return nullptr;
         memset(sv->ctl, 0, sizeof(B3SvcCtl));
         if (hipMemset(sv->dev, 0, sizeof(B3SvcDev)) != hipSuccess ||
             hipMemset(sv->proc, 0, sizeof(uint32_t) * B3_SVC_RING) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
@@ -489,24 +503,45 @@ Service* service(int device) {
     return g_svc[device];
 }
 
+// this thread's copy of its message for the service: in HBM (written through the BAR) or pinned
+struct TlVStage {
+    uint8_t* p = nullptr;
+    uint64_t cap = 0;
+    bool vram = false;
+    ~TlVStage() {
+        if (p) vram ? (void)hipFree(p) : (void)hipHostFree(p);
+    }
+};
+thread_local TlVStage t_vstage;
+
 int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]) {
-    TlStage& ts = t_stage;
-    if (ts.cap < len + 16) {  // this thread's pinned copy of its message
-        if (ts.p) hipHostFree(ts.p);
+    TlVStage& ts = t_vstage;
+    if (ts.cap < len + 16 || ts.vram != sv->vram) {
+        if (ts.p) ts.vram ? (void)hipFree(ts.p) : (void)hipHostFree(ts.p);
         ts.p = nullptr;
         ts.cap = 0;
         const uint64_t want = std::max<uint64_t>(65536 + 64, len + 16);
-        if (hipHostMalloc((void**)&ts.p, want, hipHostMallocDefault) != hipSuccess) return BW_ENOMEM;
+        if ((sv->vram ? hipExtMallocWithFlags((void**)&ts.p, want, hipDeviceMallocFinegrained)
+                      : hipHostMalloc((void**)&ts.p, want, hipHostMallocDefault)) != hipSuccess) {
+            ts.p = nullptr;
+            return BW_ENOMEM;
+        }
         ts.cap = want;
+        ts.vram = sv->vram;
     }
     if (len) memcpy(ts.p, data, len);
+    _mm_sfence();  // (the copy reaches HBM before the request that names it: writes through the BAR are
+                   // write-combined and only ordered by a fence)
     const uint64_t t = sv->next.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(t % B3_SVC_RING), seq = (uint32_t)(t + 1);
     while (sv->free_at[i].load(std::memory_order_acquire) != t) std::this_thread::yield();  // (a full ring)
-    B3SvcSlot* sl = sv->ring + i;
+    B3SvcResp* sl = sv->resp + i;
+    B3SvcReq* rq = sv->req + i;
     for (int k = 0; k < 4; k++) __atomic_store_n(&sl->digest[k], b3svc_sentinel(seq, k), __ATOMIC_RELAXED);
-    __atomic_store_n(&sl->ptr, (uint64_t)(uintptr_t)ts.p, __ATOMIC_RELAXED);
-    __atomic_store_n(&sl->lenseq, len | ((uint64_t)seq << 32), __ATOMIC_RELEASE);
+    __atomic_store_n(&rq->ptr, (uint64_t)(uintptr_t)ts.p, __ATOMIC_RELAXED);
+    _mm_sfence();
+    __atomic_store_n(&rq->lenseq, len | ((uint64_t)seq << 32), __ATOMIC_RELEASE);
+    _mm_sfence();
     int rc = svc_ensure(sv);
     uint64_t d[4];
     if (rc == BW_OK && !svc_done(sl, t, d)) {
