@@ -30,10 +30,18 @@ OFF_PATH = ("bw_zstd.hip", "bw_seal.hip", "bw_pack.hip", "bw_tree.hip", "bw_comm
             "bw_capi_pack.hip", "bw_b3_small.hip", "bw_b3_small.h")
 
 
+def _code_only(text):
+    """The source without its comments and blank space: documentation edits do not change what ran."""
+    import re
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", " ", text)
+    return " ".join(text.split())
+
+
 def source_digest():
-    """sha256 over the hot path's sources (csrc/* minus OFF_PATH, and the hot path's C ABI header): identifies
-    the kernels a profile was taken with (profiles/pmc_traffic.json), so bench.py can tell stale
-    evidence."""
+    """sha256 over the code (comments stripped) of the hot path's sources (csrc/* minus OFF_PATH,
+    and the hot path's C ABI header): identifies the kernels a profile was taken with
+    (profiles/pmc_traffic.json), so bench.py can tell stale evidence."""
     import hashlib
     h = hashlib.sha256()
     files = [f for f in sorted(os.listdir(CSRC)) if f not in OFF_PATH] + ["../../include/backuwup_gpu.h"]
@@ -41,7 +49,7 @@ def source_digest():
         path = os.path.normpath(os.path.join(CSRC, f))
         if os.path.isfile(path) and not f.endswith((".tmp", ".o")):
             h.update(f.encode())
-            h.update(open(path, "rb").read())
+            h.update(_code_only(open(path, encoding="utf-8", errors="replace").read()).encode())
     return h.hexdigest()
 
 

@@ -314,15 +314,15 @@ int coalesced_hash(Combiner* co, const uint8_t* data, uint64_t len, uint8_t out[
 //     thread per device watches the slots of the sleeping callers and wakes each as its digest lands.
 //     With more callers than cores (tokio starts one worker per core of the machine) the spinning
 //     would otherwise take the cores the other callers need to post.
-//   * An instance ends by itself when nothing was hashed for SVC_IDLE_US, or after SVC_LIFE_US (so a
-//     device synchronization waits at most that long); a caller that finds it ended starts the next
-//     one, and a waiter without its digest checks again every millisecond, which also covers a
-//     message posted just as the workers gave up.
+//   * An instance ends by itself when nothing was hashed for SVC_IDLE_US (5 ms), or after
+//     SVC_LIFE_US (500 ms; so a device synchronization waits at most that long); a caller that finds
+//     it ended starts the next one, and a waiter without its digest checks again every millisecond,
+//     which also covers a message posted just as the workers gave up.
 //   * The stream is created with a CU mask (all CUs), which gives it a hardware queue of its own:
 //     the process's other streams never queue behind the persistent kernel (tools/dropin_lat.cpp
 //     measures a neighbour stream's launches while the service runs).
 // BW_DROPIN_SERVICE=0 in the environment selects the coalescer instead (A/B).
-constexpr uint32_t SVC_IDLE_US = 5000, SVC_LIFE_US = 100000;
+constexpr uint32_t SVC_IDLE_US = 5000, SVC_LIFE_US = 500000;
 constexpr double SVC_SPIN_US = 40;
 
 // CPUs this process may run on at once: its affinity mask, capped by a cgroup v2 CPU quota (a

@@ -136,7 +136,7 @@ uint64_t bw_blake3_kept_hits(void);
  * persistent kernel's workers poll; the digest lands in the slot, where the caller spins briefly and
  * then sleeps until a library thread wakes it.  No kernel launch per call: ~8 us for a tree blob,
  * ~24 us for 16 KiB on one thread, and concurrent callers (any contexts, any threads) are served in
- * parallel.  The service's instance ends by itself after 5 ms without messages (or 100 ms of life;
+ * parallel.  The service's instance ends by itself after 5 ms without messages (or 500 ms of life;
  * the next call starts another), on a hardware queue of its own, so the process's streams never
  * wait for it; a device-wide synchronization may wait up to that long.  BW_DROPIN_SERVICE=0 in the
  * environment selects the earlier batching path (launches coalesced over four lanes).  For such

@@ -546,6 +546,51 @@ def test_dropin_call_sites_many_threads(oracle):
     assert L.bw_blake3_kept_hits() - hits0 == sum(len(w) for w in want)
 
 
+def test_hash_service_instances_and_ring_wrap(oracle):
+    """The hash service's persistent instance ends by itself when idle (5 ms) and the next call
+    starts another; tickets wrap the 4,096-slot ring many times over; every digest equals the
+    oracle's, across instance boundaries and from several threads (bw_b3_small.hip k_b3_service)."""
+    import threading
+    import time
+    from backuwup_amd import Context, _lib
+    L = _lib.load()
+    rng = np.random.default_rng(9)
+    blob = splitmix_bytes(77, 1 << 20)
+    b0, m0 = ctypes.c_uint64(), ctypes.c_uint64()
+    L.bw_blake3_coalesce_stats(0, ctypes.byref(b0), ctypes.byref(m0))
+    with Context(0) as c:
+        for rep in range(3):  # idle gaps: each burst finds the last instance ended
+            o, n = int(rng.integers(0, 1 << 19)), int(rng.integers(0, 65536))
+            assert c.blake3_at(blob, o, n) == oracle.blake3(blob[o:o + n]), (rep, n)
+            time.sleep(0.03)
+        offs = rng.integers(0, (1 << 20) - 2048, 12000)
+        lens = rng.integers(0, 2048, 12000)
+        want = [oracle.blake3(blob[o:o + n]) for o, n in zip(offs, lens)]
+        got = [None] * len(offs)
+        errors = []
+
+        def worker(t):
+            try:
+                for i in range(t, len(offs), 8):
+                    got[i] = c.blake3_at(blob, int(offs[i]), int(lens[i]))
+                    if i % 3001 == 0:
+                        time.sleep(0.012)  # some instances end mid-run
+            except Exception as e:  # reported below
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=240)
+    assert not errors, errors
+    assert got == want
+    b1, m1 = ctypes.c_uint64(), ctypes.c_uint64()
+    L.bw_blake3_coalesce_stats(0, ctypes.byref(b1), ctypes.byref(m1))
+    assert m1.value - m0.value == 12003
+    assert b1.value - b0.value >= 3  # at least one instance per idle-separated burst
+
+
 def test_coalesced_hash_many_threads(oracle):
     """the reference calls blake3::hash once per small file and once per tree blob,
     from every tokio worker at once (dir_packer.rs:166, :286, :320).  Sixteen threads hash thousands

@@ -49,7 +49,7 @@ with open("/tmp/c4_table.bin", "wb") as f:
     np.asarray(l, np.uint64).tofile(f)
 print("files", len(o), "unique bytes", u, "file bytes", int(np.sum(l)))
 PY
-  run dropin_c4 900 stdbuf -oL ./build_ab/dropin_c4 /tmp/c4_table.bin ${DROPIN_C4_THREADS:-16,64,256} 16 1 || exit 1
+  run dropin_c4 900 stdbuf -oL ./build_ab/dropin_c4 /tmp/c4_table.bin ${DROPIN_C4_THREADS:-16,64,256} 16 ${DROPIN_C4_REPS:-1} || exit 1
 fi
 if [[ " $PARTS " == *" cpu "* ]]; then
   run bench_c1_cpu 600 python3 bench.py --workload c1 --steps 300 || exit 1
