@@ -534,7 +534,11 @@ int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]
                    // write-combined and only ordered by a fence)
     const uint64_t t = sv->next.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(t % B3_SVC_RING), seq = (uint32_t)(t + 1);
-    while (sv->free_at[i].load(std::memory_order_acquire) != t) std::this_thread::yield();  // (a full ring)
+    // (a full ring: 4,096 calls in flight; a slot whose call failed stays taken, so bound the wait)
+    for (auto t0 = std::chrono::steady_clock::now(); sv->free_at[i].load(std::memory_order_acquire) != t;) {
+        std::this_thread::yield();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return BW_EHIP;
+    }
     B3SvcResp* sl = sv->resp + i;
     B3SvcReq* rq = sv->req + i;
     for (int k = 0; k < 4; k++) __atomic_store_n(&sl->digest[k], b3svc_sentinel(seq, k), __ATOMIC_RELAXED);
