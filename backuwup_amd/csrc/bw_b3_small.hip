@@ -167,8 +167,10 @@ __device__ __forceinline__ const uint8_t* b3q_message(const uint8_t* __restrict_
         *(uint32_t*)(nodes + q * 32 + 4 * j) = ca;
         *(uint32_t*)(nodes + q * 32 + 16 + 4 * j) = cb;
     }
-    for (uint32_t m = leaves; m > 1; m = (m + 1) / 2) {  // one level: node p <- parent(2p, 2p + 1)
-        __syncthreads();
+    // one level: node p <- parent(2p, 2p + 1), the odd last node moved up as it is.  While a level
+    // has more than 16 parents its quads span several waves (workgroup barriers); from 32 nodes down
+    // wave 0 alone finishes the tree (LDS operations of one wave run in order: no barrier)
+    auto level = [&](uint32_t m, bool wave_only) {
         const uint32_t half = m / 2;
         uint32_t na = 0, nb = 0;
         if (q < half) {
@@ -176,16 +178,26 @@ __device__ __forceinline__ const uint8_t* b3q_message(const uint8_t* __restrict_
             nb = b3q_iv(4 + j);
             const uint32_t dj = j < 2 ? 0u : j == 2 ? 64u : (B3_PARENT | (m == 2 ? B3_ROOT : 0));
             b3q_compress(na, nb, nodes + q * 64, of, ivj, dj);
-        } else if (q == half && (m & 1)) {  // the odd last node moves up as it is
+        } else if (q == half && (m & 1)) {
             na = *(const uint32_t*)(nodes + (m - 1) * 32 + 4 * j);
             nb = *(const uint32_t*)(nodes + (m - 1) * 32 + 16 + 4 * j);
         }
-        __syncthreads();
+        if (wave_only) __builtin_amdgcn_wave_barrier();
+        else __syncthreads();
         if (q < half || (q == half && (m & 1))) {
             *(uint32_t*)(nodes + q * 32 + 4 * j) = na;
             *(uint32_t*)(nodes + q * 32 + 16 + 4 * j) = nb;
         }
+        if (wave_only) __builtin_amdgcn_wave_barrier();
+    };
+    uint32_t m = leaves;
+    for (; m > 32; m = (m + 1) / 2) {
+        __syncthreads();
+        level(m, false);
     }
+    __syncthreads();
+    if (tid < 64)
+        for (; m > 1; m = (m + 1) / 2) level(m, true);
     __syncthreads();
     return nodes;  // the root chaining value = the digest: nodes[0, 32)
 }

@@ -425,8 +425,11 @@ int svc_ensure(Service* sv) {
     return BW_OK;
 }
 
-// wakes the sleeping callers whose digests landed; sleeps itself while no caller sleeps
-void svc_completer(Service* sv) {
+// wakes the sleeping callers whose digests landed (tickets t with t % SVC_COMPLETERS == k); sleeps
+// itself while no caller sleeps.  Several of them: at 256 callers one thread making every wake-up
+// system call (~600 k a second) was the limit.
+constexpr int SVC_COMPLETERS = 4;
+void svc_completer(Service* sv, int k) {
     uint64_t lo = 0;  // tickets below lo have returned to their callers
     for (;;) {
         const uint32_t gen = sv->comp_gen.load(std::memory_order_acquire);
@@ -436,7 +439,7 @@ void svc_completer(Service* sv) {
         }
         const uint64_t hi = sv->next.load(std::memory_order_acquire);
         while (lo < hi && sv->free_at[lo % B3_SVC_RING].load(std::memory_order_acquire) > lo) lo++;
-        for (uint64_t t = lo; t < hi; t++) {
+        for (uint64_t t = lo + ((k - lo % SVC_COMPLETERS) + SVC_COMPLETERS) % SVC_COMPLETERS; t < hi; t += SVC_COMPLETERS) {
             const uint32_t i = (uint32_t)(t % B3_SVC_RING);
             uint64_t d[4];
             if (sv->sleep[i].load(std::memory_order_acquire) == 1 && svc_done(sv->resp + i, t, d)) {
@@ -495,7 +498,7 @@ Service* service(int device) {
             sv->free_at[i].store(i);
             sv->sleep[i].store(0);
         }
-        std::thread(svc_completer, sv).detach();
+        for (int k = 0; k < SVC_COMPLETERS; k++) std::thread(svc_completer, sv, k).detach();
         static std::once_flag once;
         std::call_once(once, [] { atexit(svc_atexit); });
         g_svc[device] = sv;
@@ -562,7 +565,7 @@ int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]
             sv->sleep[i].store(1, std::memory_order_release);
             sv->sleepers.fetch_add(1, std::memory_order_acq_rel);
             sv->comp_gen.fetch_add(1, std::memory_order_acq_rel);
-            futex(&sv->comp_gen, FUTEX_WAKE_PRIVATE, 1);
+            futex(&sv->comp_gen, FUTEX_WAKE_PRIVATE, SVC_COMPLETERS);
             double next_trace = 2000;
             while (!svc_done(sl, t, d)) {
                 const timespec ts1 = {0, 1000000};

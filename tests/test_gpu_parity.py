@@ -591,6 +591,50 @@ def test_hash_service_instances_and_ring_wrap(oracle):
     assert b1.value - b0.value >= 3  # at least one instance per idle-separated burst
 
 
+_ALT_PATH = """
+import sys, threading
+sys.path.insert(0, %r)
+import numpy as np
+from backuwup_amd import Context
+from backuwup_amd.synth import splitmix_bytes
+blob = splitmix_bytes(79, 1 << 20)
+rng = np.random.default_rng(11)
+offs = rng.integers(0, (1 << 20) - 70000, 600)
+lens = rng.integers(0, 65537, 600)
+lens[:6] = [0, 1, 64, 1024, 65535, 65536]
+got = [None] * len(offs)
+with Context(0) as c:
+    def worker(t):
+        for i in range(t, len(offs), 4):
+            got[i] = c.blake3_at(blob, int(offs[i]), int(lens[i])).hex()
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+print("@@", ",".join("%%d:%%d:%%s" %% (o, n, g) for o, n, g in zip(offs, lens, got)))
+"""
+
+
+@pytest.mark.parametrize("env", [{"BW_SVC_HOST_RING": "1"}, {"BW_DROPIN_SERVICE": "0"}])
+def test_small_hash_alternative_paths(oracle, env):
+    """The hash service with its requests in pinned host memory (the path of a host without a large
+    BAR), and the launched-batch coalescer (BW_DROPIN_SERVICE=0): each in a child process (the
+    library reads the choice once per process), 600 messages from 4 threads, equal to the oracle."""
+    import os
+    import subprocess
+    import sys
+    from backuwup_amd.synth import splitmix_bytes
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _ALT_PATH % root], capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, **env))
+    line = [l for l in out.stdout.splitlines() if l.startswith("@@ ")]
+    assert line, (out.stdout[-2000:], out.stderr[-2000:])
+    blob = splitmix_bytes(79, 1 << 20)
+    for item in line[0][3:].split(","):
+        o, n, g = item.split(":")
+        o, n = int(o), int(n)
+        assert bytes.fromhex(g) == oracle.blake3(blob[o:o + n]), (env, o, n)
+
+
 def test_coalesced_hash_many_threads(oracle):
     """the reference calls blake3::hash once per small file and once per tree blob,
     from every tokio worker at once (dir_packer.rs:166, :286, :320).  Sixteen threads hash thousands
