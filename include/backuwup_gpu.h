@@ -132,11 +132,12 @@ uint64_t bw_blake3_kept_hits(void);
 
 /* blake3::hash(data) -> 32 bytes, host buffer; always hashes the bytes given.  Messages up to
  * BW_COALESCE_MAX_MSG (a small file, a tree blob) go to the device's hash service: each caller
- * copies its message into pinned memory of its own and posts it into a ring of slots that a
- * persistent kernel's workers poll; the digest lands in the slot, where the caller spins briefly and
- * then sleeps until a library thread wakes it.  No kernel launch per call: ~8 us for a tree blob,
- * ~24 us for 16 KiB on one thread, and concurrent callers (any contexts, any threads) are served in
- * parallel.  The service's instance ends by itself after 5 ms without messages (or 500 ms of life;
+ * copies its message into a staging buffer of its own and posts a request into a ring of slots that
+ * a persistent kernel's workers poll (with a large BAR both sit in HBM, written by the CPU through
+ * the BAR; otherwise in pinned host memory, or so with BW_SVC_HOST_RING=1); the digest lands in a
+ * response slot in pinned memory, where the caller spins briefly and then sleeps until a library
+ * thread wakes it.  No kernel launch per call: ~7 us for a tree blob, ~20 us for 16 KiB on one
+ * thread, and concurrent callers (any contexts, any threads) are served in parallel.  The service's instance ends by itself after 5 ms without messages (or 500 ms of life;
  * the next call starts another), on a hardware queue of its own, so the process's streams never
  * wait for it; a device-wide synchronization may wait up to that long.  BW_DROPIN_SERVICE=0 in the
  * environment selects the earlier batching path (launches coalesced over four lanes).  For such
