@@ -651,9 +651,11 @@ def _two_rank_c_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
-    """bw_exchange_dedup with two processes on the one GPU: every verdict equals one global index
-    over the canonical order (batch, rank, position), including a repeated batch (all duplicates)."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle, world):
+    """bw_exchange_dedup with two (four) processes on the one GPU: every verdict equals one global
+    index over the canonical order (batch, rank, position), including a repeated batch (all
+    duplicates) and batches whose sizes differ between the ranks and grow and shrink."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -662,17 +664,17 @@ def test_exchange_dedup_c_abi_two_ranks_one_gpu(oracle):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_two_rank_c_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_two_rank_c_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in range(2))
+    got = dict(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     data, offs, lens = small_files(6000, seed=56)
     ix = oracle.Index()
     for batch in range(4):
-        for r in range(2):
+        for r in range(world):
             lo, hi, dig, dup = got[r][batch]
             want = oracle.process_files(*_slices(data, offs, lens, [(lo, hi)])[0], index=ix)
             assert np.array_equal(dig, want["digest"]) and np.array_equal(dup, want["is_dup"]), (batch, r)

@@ -180,7 +180,7 @@ def _shard_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_stream_shard_c_abi_two_ranks_one_gpu(world, oracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
