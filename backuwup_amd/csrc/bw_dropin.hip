@@ -39,6 +39,7 @@
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -315,12 +316,15 @@ int coalesced_hash(Combiner* co, const uint8_t* data, uint64_t len, uint8_t out[
 //     With more callers than cores (tokio starts one worker per core of the machine) the spinning
 //     would otherwise take the cores the other callers need to post.
 //   * An instance ends by itself when nothing was hashed for SVC_IDLE_US (5 ms), or after
-//     SVC_LIFE_US (500 ms; so a device synchronization waits at most that long); a caller that finds
-//     it ended starts the next one, and a waiter without its digest checks again every millisecond,
-//     which also covers a message posted just as the workers gave up.
-//   * The stream is created with a CU mask (all CUs), which gives it a hardware queue of its own:
-//     the process's other streams never queue behind the persistent kernel (tools/dropin_lat.cpp
-//     measures a neighbour stream's launches while the service runs).
+//     SVC_LIFE_US (500 ms); a caller that finds it ended starts the next one, and a waiter without
+//     its digest checks again every millisecond, which also covers a message posted just as the
+//     workers gave up.  A device-wide synchronization (hipDeviceSynchronize, torch.cuda.synchronize)
+//     waits for the running instance: under steady calls up to its life.  BW_SVC_LIFE_US (1,000 to
+//     500,000) shortens that bound for an application that synchronizes the device while hashing;
+//     50 ms cost C4 0-7 % (profiles/r05/s25_svc_stream).
+//   * The stream is a non-blocking stream of the least priority (service(), below): the process's
+//     other streams never queue behind the persistent kernel, and the legacy null stream does not
+//     wait for it (tools/dropin_lat.cpp measures both while the service runs).
 // BW_DROPIN_SERVICE=0 in the environment selects the coalescer instead (A/B).
 constexpr uint32_t SVC_IDLE_US = 5000, SVC_LIFE_US = 500000;
 constexpr double SVC_SPIN_US = 40;
@@ -413,8 +417,11 @@ int svc_ensure(Service* sv) {
     const uint64_t hi = sv->next.load(std::memory_order_acquire);
     while (lo < hi && sv->free_at[lo % B3_SVC_RING].load(std::memory_order_acquire) > lo) lo++;
     sv->front.store(lo, std::memory_order_relaxed);
-    launch_b3_service(sv->st, sv->req, sv->resp, sv->ctl, sv->dev, sv->proc, e2 + 1, (uint32_t)lo, SVC_IDLE_US,
-                      SVC_LIFE_US);
+    static const uint32_t life = [] {  // BW_SVC_LIFE_US (see above)
+        const char* e = getenv("BW_SVC_LIFE_US");
+        return e && atoi(e) > 0 ? (uint32_t)std::min(std::max(atoi(e), 1000), (int)SVC_LIFE_US) : SVC_LIFE_US;
+    }();
+    launch_b3_service(sv->st, sv->req, sv->resp, sv->ctl, sv->dev, sv->proc, e2 + 1, (uint32_t)lo, SVC_IDLE_US, life);
     if (const hipError_t e = hipGetLastError()) {
         if (g_svc_trace) fprintf(stderr, "[bw svc] launch failed: %s\n", hipGetErrorString(e));
         return BW_EHIP;
@@ -474,7 +481,25 @@ Service* service(int device) {
             return nullptr;
         std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
         if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1;
-        if (hipExtStreamCreateWithCUMask(&sv->st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+        // The persistent kernel needs a stream that neither holds up other work nor is held up by it
+        // (profiles/r05/s25_svc_stream): a plain stream shares one of the process's few hardware
+        // queues (GPU_MAX_HW_QUEUES) with other streams, whose kernels then wait behind the running
+        // instance (up to its 500 ms life); a CU-masked stream gets a queue of its own but is a
+        // blocking stream, so every legacy-null-stream call (a bare hipMemcpy, PyTorch's default
+        // stream) waits for the instance to end.  A non-blocking stream of the least priority has
+        // both: the runtime keeps a queue pool per priority, and nothing else here asks for "low".
+        // BW_SVC_STREAM=cumask|plain selects the other two (A/B only).
+        const char* sk = getenv("BW_SVC_STREAM");
+        const std::string skind = sk ? sk : "low";
+        int least = 0, greatest = 0;
+        if (skind == "cumask" ? hipExtStreamCreateWithCUMask(&sv->st, (uint32_t)mask.size(), mask.data()) != hipSuccess
+            : skind == "plain"
+                ? hipStreamCreateWithFlags(&sv->st, hipStreamNonBlocking) != hipSuccess
+                : hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                      hipStreamCreateWithPriority(&sv->st, hipStreamNonBlocking, least) != hipSuccess)
+            return nullptr;
+        if (getenv("BW_SVC_TRACE"))
+            fprintf(stderr, "[svc] stream %s (priority range %d..%d)\n", skind.c_str(), least, greatest);
         int large_bar = 0;
         hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device);
         const char* hr = getenv("BW_SVC_HOST_RING");

@@ -137,9 +137,11 @@ uint64_t bw_blake3_kept_hits(void);
  * the BAR; otherwise in pinned host memory, or so with BW_SVC_HOST_RING=1); the digest lands in a
  * response slot in pinned memory, where the caller spins briefly and then sleeps until a library
  * thread wakes it.  No kernel launch per call: ~7 us for a tree blob, ~20 us for 16 KiB on one
- * thread, and concurrent callers (any contexts, any threads) are served in parallel.  The service's instance ends by itself after 5 ms without messages (or 500 ms of life;
- * the next call starts another), on a hardware queue of its own, so the process's streams never
- * wait for it; a device-wide synchronization may wait up to that long.  BW_DROPIN_SERVICE=0 in the
+ * thread, and concurrent callers (any contexts, any threads) are served in parallel.  The service's
+ * instance ends by itself after 5 ms without messages (or 500 ms of life; the next call starts
+ * another).  It runs on a non-blocking stream of the least priority, so neither the process's
+ * streams nor the legacy null stream wait for it; a device-wide synchronization does, up to the
+ * life (BW_SVC_LIFE_US=1000..500000 shortens it).  BW_DROPIN_SERVICE=0 in the
  * environment selects the earlier batching path (launches coalesced over four lanes).  For such
  * messages the context is only read for its device, so any number of threads may pass the same
  * context; larger messages run on the context itself (one thread at a time). */

@@ -591,6 +591,52 @@ def test_hash_service_instances_and_ring_wrap(oracle):
     assert b1.value - b0.value >= 3  # at least one instance per idle-separated burst
 
 
+def test_hash_service_leaves_null_stream_free(oracle):
+    """While callers keep the hash service's persistent instance running, work on the legacy null
+    stream (a bare hipMemcpy, PyTorch's default stream) is not held up until the instance ends: the
+    service's stream is a non-blocking one (bw_dropin.hip service(); a CU-masked stream, a blocking
+    one, held such calls up to the instance's 500 ms life, profiles/r05/s25_svc_stream)."""
+    import threading
+    import time
+    import torch
+    from backuwup_amd import Context
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime already loaded (torch's and the library's)
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    blob = splitmix_bytes(78, 1 << 16)
+    x = torch.arange(16, dtype=torch.int32, device="cuda:0")
+    host = (ctypes.c_int32 * 16)()
+    stop = threading.Event()
+    errors = []
+    with Context(0) as c:
+        want = oracle.blake3(blob[:4096])
+
+        def caller():
+            try:
+                while not stop.is_set():
+                    if c.blake3_at(blob, 0, 4096) != want:
+                        errors.append("digest")
+                        return
+            except Exception as e:  # reported below
+                errors.append(repr(e))
+
+        th = threading.Thread(target=caller)
+        th.start()
+        try:
+            time.sleep(0.05)  # an instance is running
+            worst = 0.0
+            for _ in range(40):
+                t = time.perf_counter()
+                assert hip.hipMemcpy(host, ctypes.c_void_p(x.data_ptr()), 64, 2) == 0  # device to host
+                assert int(torch.ones(4, device="cuda:0").sum()) == 4  # the default stream
+                worst = max(worst, time.perf_counter() - t)
+        finally:
+            stop.set()
+            th.join(timeout=60)
+    assert not errors, errors
+    assert list(host) == list(range(16))
+    assert worst < 0.1, f"a null-stream call waited {worst * 1e3:.1f} ms behind the hash service"
+
+
 _ALT_PATH = """
 import sys, threading
 sys.path.insert(0, %r)

@@ -188,10 +188,38 @@ int main(int argc, char** argv) {
             hipStreamSynchronize(x);
             v.push_back(us_since(t));
         }
+        // the legacy null stream (PyTorch's default stream, a bare hipMemcpy): it waits for every
+        // blocking stream, so a persistent kernel on a blocking stream would hold it up to the
+        // kernel's exit
+        std::vector<double> vn, vm, vd;
+        int* dw = nullptr;
+        hipMalloc((void**)&dw, 64);
+        int hw = 0;
+        for (int i = 0; i < 200; i++) {
+            auto t = clk::now();
+            k_empty<<<1, 64, 0, 0>>>(nullptr);
+            hipStreamSynchronize(0);
+            vn.push_back(us_since(t));
+            t = clk::now();
+            hipMemcpy(&hw, dw, 4, hipMemcpyDeviceToHost);
+            vm.push_back(us_since(t));
+            if (i % 10 == 0) {  // a device-wide synchronization waits for the running instance
+                t = clk::now();
+                hipDeviceSynchronize();
+                vd.push_back(us_since(t));
+            }
+        }
         run = false;
         for (auto& x : th) x.join();
         report("neighbour stream launch+sync", v);
         printf("   max %.1f us\n", v.back());
+        report("null stream launch+sync", vn);
+        printf("   max %.1f us\n", vn.back());
+        report("null stream hipMemcpy 4 B", vm);
+        printf("   max %.1f us\n", vm.back());
+        report("hipDeviceSynchronize", vd);
+        printf("   max %.1f us\n", vd.back());
+        hipFree(dw);
         for (auto& x : ss) hipStreamDestroy(x);
     }
     bw_destroy(ctx);
