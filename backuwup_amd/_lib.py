@@ -13,7 +13,7 @@ BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -
 BW_ECRYPTO, BW_EFORMAT, BW_ECOMM = -7, -8, -9
 BW_COMM_ID_BYTES = 128
 BW_COMM_DEFAULT_TIMEOUT_MS = 120000
-BW_ZSTD_LANES = 3  # include/backuwup_gpu.h: asynchronous zstd batches in flight per context
+BW_ZSTD_LANES = 6  # include/backuwup_gpu.h: asynchronous zstd batches in flight per context
 BW_F_NO_HASH, BW_F_NO_DEDUP, BW_F_SERIAL_RESOLVE = 1, 2, 4
 BW_OPT_DEPTH, BW_OPT_SCAN_SMALL_BYTES, BW_OPT_CAND_CAP, BW_OPT_STAGE_CHUNK, BW_OPT_B3_LOADS = 1, 2, 3, 4, 5
 BW_OPT_SCAN_WAVES, BW_OPT_LATENCY_STREAM, BW_OPT_ZSTD_SLOTS, BW_OPT_ZSTD_BATCH_BYTES = 6, 7, 8, 9

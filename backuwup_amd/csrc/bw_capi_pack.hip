@@ -166,17 +166,25 @@ extern "C" int bw_zstd_submit_device(bw_ctx* c, const uint8_t* d_src, const uint
             L = &x;
             break;
         }
-    // Every lane on a stream of its own when the process has hardware queues for them: HIP maps a
-    // process's streams onto GPU_MAX_HW_QUEUES queues (4 by default), and two lanes sharing one run
-    // one after the other.  With the default, lane 0 runs on the context's stream instead, and the
-    // other lanes' submit-time wait on that stream then also covers lane 0's batch.  Measured on
-    // 1 GiB text batches, three lanes: own streams 1.64-1.66 GB/s with 4 queues and 2.91 with 8;
-    // lane 0 on the context's stream 2.29-2.31 either way (profiles/r04/s17_lanesab, s18_lanesq8).
+    // Every lane on a stream of its own, each on a hardware queue of its own where the runtime has
+    // one: HIP maps a process's streams of one priority onto GPU_MAX_HW_QUEUES queues (4 by
+    // default), and two lanes sharing a queue run one after the other.  The runtime keeps a queue
+    // pool per priority, so lanes 0-3 take high-priority streams (a pool nothing else in the library
+    // uses, except BW_OPT_LATENCY_STREAM) and lanes 4-5 normal ones.  1 GiB text batches from one
+    // host thread with the default 4 queues (profiles/r05/s28_zstd_lanes .. s31): 3 lanes 2.86-2.90
+    // GB/s (round 4's normal-priority lanes, lane 0 on the context's stream: 2.32), 4 lanes 3.52-3.56,
+    // 5 lanes 4.04, 6 lanes 4.43-4.56; 8 lanes 3.46 (two share the context's queues; 5.01 with 8
+    // queues).  BW_ZSTD_LANE_PRIO=normal restores round 4's placement (A/B): with fewer than
+    // BW_ZSTD_LANES + 2 queues lane 0 then runs on the context's stream.
     static const int hw_queues = [] {
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         return q && atoi(q) > 0 ? atoi(q) : 4;
     }();
-    const bool own = L != &c->zs_lanes[0] || hw_queues >= BW_ZSTD_LANES + 2;  // + the context's, the caller's
+    static const bool lane_high = [] {
+        const char* e = getenv("BW_ZSTD_LANE_PRIO");
+        return !(e && !strcmp(e, "normal"));
+    }();
+    const bool own = lane_high || L != &c->zs_lanes[0] || hw_queues >= BW_ZSTD_LANES + 2;  // + the context's, the caller's
     if (!L) {
         c->err = "every zstd lane holds a batch (BW_ZSTD_LANES = " + std::to_string(BW_ZSTD_LANES) +
                  "): bw_zstd_wait for one first";
@@ -184,7 +192,12 @@ extern "C" int bw_zstd_submit_device(bw_ctx* c, const uint8_t* d_src, const uint
     }
     hipSetDevice(c->device);
     if (own) {
-        if (!L->own_st) HIPCHK(c, hipStreamCreateWithFlags(&L->own_st, hipStreamNonBlocking));
+        if (!L->own_st) {
+            int least = 0, greatest = 0;
+            HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+            const bool hi = lane_high && L - c->zs_lanes < 4;  // (the high pool's default 4 queues)
+            HIPCHK(c, hipStreamCreateWithPriority(&L->own_st, hipStreamNonBlocking, hi ? greatest : 0));
+        }
         if (!L->ready) HIPCHK(c, hipEventCreateWithFlags(&L->ready, hipEventDisableTiming));
         HIPCHK(c, hipEventRecord(L->ready, c->stream));
         HIPCHK(c, hipStreamWaitEvent(L->own_st, L->ready, 0));

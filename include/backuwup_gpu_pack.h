@@ -88,15 +88,15 @@ int bw_zstd_compress(bw_ctx* ctx, const uint8_t* src, const uint64_t* src_off, c
 /* Asynchronous form: one call lasts as long as its largest blob's serial parse, so a packer keeps
  * several batches in flight.  bw_zstd_submit_device copies the offset tables, starts the batch on
  * one of the context's BW_ZSTD_LANES lanes (each its own hash tables and a stream of its own,
- * ordered after the work already on the context's stream; with fewer than BW_ZSTD_LANES + 2
- * hardware queues per process -- HIP's GPU_MAX_HW_QUEUES, 4 by default -- the first lane runs on
- * the context's stream instead, so its bw_zstd_wait also waits for whatever the caller queued on
- * that stream after the submit) and returns at once with *ticket; BW_ESTATE when every lane holds
+ * ordered after the work already on the context's stream: lanes 0-3 high-priority streams, which
+ * the runtime serves from a hardware-queue pool of their own, lanes 4-5 normal ones; 1 GiB text
+ * batches from one host thread, HIP's default 4 queues per pool: 4 lanes 3.5 GB/s, 6 lanes 4.4-4.6)
+ * and returns at once with *ticket; BW_ESTATE when every lane holds
  * a batch (wait for one first).  Hash tables: per lane, 768 KiB per blob for sub-batches of more
  * than 2,048 blobs and 2.5 MiB per blob for smaller ones (two pools, each grown to the largest
  * sub-batch of its layout seen: at most BW_OPT_ZSTD_SLOTS x 768 KiB + 2,048 x 2.5 MiB).  d_src and d_dst stay untouched by the caller until
  * bw_zstd_wait(ticket), which blocks for the batch and writes its n frame sizes to frame_len. */
-#define BW_ZSTD_LANES 3
+#define BW_ZSTD_LANES 6
 int bw_zstd_submit_device(bw_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint64_t* src_len,
                           uint64_t n, uint8_t* d_dst, const uint64_t* dst_off, uint64_t* ticket);
 int bw_zstd_wait(bw_ctx* ctx, uint64_t ticket, uint64_t* frame_len);
