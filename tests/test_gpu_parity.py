@@ -604,6 +604,7 @@ def test_hash_service_leaves_null_stream_free(oracle):
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     blob = splitmix_bytes(78, 1 << 16)
     x = torch.arange(16, dtype=torch.int32, device="cuda:0")
+    assert int(torch.ones(4, device="cuda:0").sum()) == 4  # (first-use code loading, before the timing)
     host = (ctypes.c_int32 * 16)()
     stop = threading.Event()
     errors = []
