@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BW_LIB") or os.path.join(HERE, "libbackuwup_amd.so")
 
 BW_OK, BW_EINVAL, BW_ENOSPC, BW_EHIP, BW_ENOMEM, BW_ECOLLISION, BW_ESTATE = 0, -1, -2, -3, -4, -5, -6
-BW_ECRYPTO, BW_EFORMAT, BW_ECOMM = -7, -8, -9
+BW_ECRYPTO, BW_EFORMAT, BW_ECOMM, BW_EAGAIN = -7, -8, -9, -10
 BW_COMM_ID_BYTES = 128
 BW_COMM_DEFAULT_TIMEOUT_MS = 120000
 BW_ZSTD_LANES = 6  # include/backuwup_gpu.h: asynchronous zstd batches in flight per context
@@ -175,7 +175,10 @@ SIGNATURES = [
     ("bw_fastcdc_release", None, [ctypes.c_uint64]),
     ("bw_blake3_kept_hits", ctypes.c_uint64, []),
     ("bw_blake3_hash_dropin", ctypes.c_int, [vp, vp, ctypes.c_uint64, u8p]),
+    ("bw_blake3_hash_dropin_device", ctypes.c_int, [ctypes.c_int, vp, ctypes.c_uint64, u8p]),
     ("bw_blake3_coalesce_stats", ctypes.c_int, [ctypes.c_int, u64p, u64p]),
+    ("bw_blake3_service_faults", ctypes.c_int, [ctypes.c_int, u64p, u64p, u64p]),
+    ("bw_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     ("bw_profile_read", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
     ("bw_profile_intervals", ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, u64p]),
     ("bw_calibrate_b3", ctypes.c_int, [vp, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),

@@ -8,7 +8,6 @@ is a synchronous round trip).
 """
 import numpy as np
 
-from .context import default_context
 
 OUT_LEN = 32
 
@@ -39,9 +38,14 @@ def _immutable(data):
 def hash(data, ctx=None):  # noqa: A001 - mirrors blake3::hash
     """blake3::hash(data) -> 32 bytes (the crate's Hash converted with .into()).  A message of at
     most 64 KiB goes to the library's hash service, a persistent kernel that serves the calls of
-    every thread without a launch per call (bw_blake3_hash)."""
+    every thread without a launch per call.  Without `ctx` the call goes through the drop-in pool
+    (backuwup_amd/pool.py: this thread's home device of every GPU of the node, the Rust crate's
+    policy); with one, through that context (bw_blake3_hash_dropin / bw_blake3_hash)."""
     buf = _as_bytes_view(data)
-    ctx = ctx or default_context()
+    if ctx is None:
+        from .pool import default_pool
+        p = default_pool()
+        return p.hash_dropin(data) if _immutable(data) else p.with_context(lambda c: c.blake3(buf))
     return ctx.blake3_dropin(buf) if _immutable(data) else ctx.blake3(buf)
 
 
@@ -55,4 +59,7 @@ def hash_many(data, offsets, lengths, ctx=None):
         raise ValueError("blake3.hash_many: %d offsets but %d lengths" % (offs.size, lens.size))
     if offs.size and int((offs + lens).max()) > buf.size:
         raise ValueError("blake3.hash_many: a message runs past the end of the data")
-    return (ctx or default_context()).blake3_many(buf, offs, lens)
+    if ctx is None:
+        from .pool import default_pool
+        return default_pool().with_context(lambda c: c.blake3_many(buf, offs, lens))
+    return ctx.blake3_many(buf, offs, lens)

@@ -33,6 +33,9 @@ struct alignas(64) B3SvcResp {
     uint64_t pad[4];
 };
 static_assert(sizeof(B3SvcResp) == 64, "one cache line per slot");
+// bit 31 of lenseq's length word: the host cancelled this ticket (its caller gave up and the slot
+// was reclaimed); a worker that reserves it moves on without hashing or writing the response slot
+constexpr uint32_t B3SVC_CANCEL = 1u << 31;
 __host__ __device__ inline uint64_t b3svc_sentinel(uint32_t seq, int k) {
     return (0x9E3779B97F4A7C15ull * seq) ^ (0xD1B54A32D192ED03ull * (uint64_t)(k + 1));
 }
@@ -47,7 +50,7 @@ struct B3SvcDev {            // device memory, kept across instances
     uint32_t pad0;
     uint32_t started;        // the epoch whose first wave reset `next` (the workers wait for it)
     uint32_t quit;           // the epoch whose workers are leaving
-    uint32_t exited;         // workers of the running instance that left
+    uint32_t exited;         // workers that left, over every instance (never reset; mod 2^32)
     uint32_t progress;       // messages hashed (a waiting worker's idle clock restarts when it moves)
     uint32_t pad[2];
 };

@@ -265,7 +265,6 @@ __global__ __launch_bounds__(256) void k_b3_service(B3SvcReq* req, B3SvcResp* re
         const uint32_t f = start;
         if (lane == 0) {
             __hip_atomic_store(&dev->next, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&dev->exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&dev->started, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -298,13 +297,22 @@ __global__ __launch_bounds__(256) void k_b3_service(B3SvcReq* req, B3SvcResp* re
                 uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
                 uint32_t seen = __hip_atomic_load(&dev->progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 B3SvcReq* sl = req + (t % B3_SVC_RING);
-                bool leave = false;
+                bool leave = false, skip = false;
                 for (uint32_t it = 0;; it++) {
                     const uint64_t h = __hip_atomic_load(&sl->lenseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(h >> 32));
-                    if (seq == t + 1) {
+                    const uint32_t lw = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)h);
+                    // (int)(seq - (t + 1)): 0 = this ticket's request, < 0 = the slot's earlier ticket
+                    // (not posted yet), > 0 = a later ticket already holds the slot (this one was
+                    // served or abandoned and its slot reclaimed by the host)
+                    const int ahead = (int)(seq - (t + 1));
+                    if (ahead > 0 || (ahead == 0 && (lw & B3SVC_CANCEL))) {
+                        skip = true;  // an abandoned ticket the host cancelled: nobody waits for it
+                        break;
+                    }
+                    if (ahead == 0) {
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the message is fresh host memory
-                        ln = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)h);
+                        ln = lw;
                         pt = __hip_atomic_load(&sl->ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         go = 1;
                         break;
@@ -333,6 +341,7 @@ __global__ __launch_bounds__(256) void k_b3_service(B3SvcReq* req, B3SvcResp* re
                     if (lane == 0) __hip_atomic_store(&dev->quit, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
+                (void)skip;  // (go stays 0: reserve the next ticket)
             }
             if (lane == 0) {
                 s_w[0] = go;
@@ -357,8 +366,13 @@ __global__ __launch_bounds__(256) void k_b3_service(B3SvcReq* req, B3SvcResp* re
         __syncthreads();
     }
     if (tid == 0) {  // the last worker out tells the host
+        // `exited` counts every worker of every instance since the service was created and is never
+        // reset: instances run one after another on one stream, epochs are 1, 2, 3, ..., so the last
+        // worker of epoch e is the (gridDim.x * e)-th exit (mod 2^32).  (Round 5 reset the count in
+        // block 0: a worker that timed out at hard_end before block 0 ran was then not counted, the
+        // end was never published, and the host believed a finished instance was still running.)
         const uint32_t n = __hip_atomic_fetch_add(&dev->exited, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (n + 1 == gridDim.x) {
+        if (n + 1 == gridDim.x * epoch) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             __hip_atomic_store(&ctl->dead, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }

@@ -362,6 +362,8 @@ extern "C" const char* bw_strerror(int rc) {
         case BW_ESTATE: return "invalid call order";
         case BW_ECRYPTO: return "AES-GCM authentication failed";
         case BW_EFORMAT: return "malformed bincode data";
+        case BW_ECOMM: return "the exchange transport failed (communicator aborted)";
+        case BW_EAGAIN: return "the hash service could not take the call; retry through a context";
         default: return "unknown error";
     }
 }
@@ -1631,7 +1633,12 @@ struct ExQueue {
     std::vector<ExPending> q;  // FIFO (front = index 0)
 };
 
+// Created once per communicator under a lock: two contexts exchanging on one
+// communicator from two threads must share one FIFO, or the issue order stops being the same on
+// every rank.
+std::mutex g_exq_create_mu;
 ExQueue* exq_of(bw_comm* comm, bool create) {
+    std::lock_guard<std::mutex> lk(g_exq_create_mu);
     void*& p = comm_exq(comm);
     if (!p && create) p = new ExQueue();
     return (ExQueue*)p;

@@ -355,6 +355,29 @@ long futex(std::atomic<uint32_t>* a, int op, uint32_t v, const timespec* ts = nu
     return syscall(SYS_futex, (uint32_t*)a, op, v, ts, nullptr, 0);
 }
 
+// The calling thread's current device for the scope, then back: the drop-ins run on the caller's
+// threads (tokio workers, a torch thread), whose current device must not change under them.
+struct DeviceGuard {
+    int old = -1, want = 0;
+    explicit DeviceGuard(int d) : want(d) {
+        if (hipGetDevice(&old) != hipSuccess) old = -1;
+        if (old != d) hipSetDevice(d);
+    }
+    ~DeviceGuard() {
+        if (old >= 0 && old != want) hipSetDevice(old);
+    }
+};
+
+int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// A caller gives up on its ticket after SVC_WAIT_US without its slot or its digest (the GPU did not
+// run the service for that long: a neighbour holding every CU, a device fault) and returns BW_EAGAIN;
+// the ticket is then abandoned, never left unreturned (svc_reclaim).
+constexpr double SVC_WAIT_US = 10e6;
+
 struct Service {
     int device = 0;
     hipStream_t st = nullptr;
@@ -374,6 +397,19 @@ struct Service {
     std::atomic<uint32_t> epoch{0};  // the last instance launched
     std::atomic<uint64_t> front{0};  // tickets below it have returned to their callers (under mu)
     std::atomic<uint64_t> launches{0}, messages{0};
+    // tickets whose callers gave up: ticket -> whether its request was posted.  Each is
+    // handed back by svc_reclaim, so `front` and the slot's next ticket never wait for it
+    std::mutex ab_mu;
+    std::map<uint64_t, bool> abandoned;
+    std::atomic<uint32_t> ab_pending{0};
+    std::atomic<uint64_t> n_abandoned{0}, n_reclaimed{0}, n_recovered{0};
+    std::atomic<int64_t> probe_at{0};  // the last stream query (at most one per millisecond)
+    // message copies of threads that exited, reused by later threads (freeing device
+    // memory synchronizes the device, which waits for the running instance, up to its life)
+    std::mutex stage_mu;
+    std::vector<uint8_t*> stage_pool;
+    std::atomic<uint64_t> calls{0};
+    uint64_t fault_after = UINT64_MAX;  // BW_SVC_FAULT_AFTER=n (tests): call n gives up right after posting
 };
 
 std::mutex g_svc_mu;
@@ -403,15 +439,69 @@ inline bool svc_done(const B3SvcResp* sl, uint64_t t, uint64_t d[4]) {
     return true;
 }
 
-// start an instance unless one is running (the last launched has not published its end)
-int svc_ensure(Service* sv) {
+// Hand the slots of abandoned tickets on.  Ticket t is reclaimed once it holds its slot (free_at ==
+// t) and no worker can still write its response slot: it was never posted (its caller gave up
+// waiting for the slot), its digest has landed, or no instance runs (`idle`).  Its request is marked
+// cancelled first, so a worker of a later instance that reserves it moves on; then the slot goes to
+// ticket t + RING and `front` may pass t.
+void svc_reclaim(Service* sv, bool idle) {
+    if (sv->ab_pending.load(std::memory_order_acquire) == 0) return;
+    std::lock_guard<std::mutex> lk(sv->ab_mu);
+    for (bool moved = true; moved;) {  // (a reclaimed slot may pass to another abandoned ticket)
+        moved = false;
+        for (auto it = sv->abandoned.begin(); it != sv->abandoned.end();) {
+            const uint64_t t = it->first;
+            const uint32_t i = (uint32_t)(t % B3_SVC_RING);
+            uint64_t d[4];
+            if (sv->free_at[i].load(std::memory_order_acquire) != t ||
+                (it->second && !idle && !svc_done(sv->resp + i, t, d))) {
+                ++it;
+                continue;
+            }
+            __atomic_store_n(&sv->req[i].lenseq, ((uint64_t)(uint32_t)(t + 1) << 32) | B3SVC_CANCEL, __ATOMIC_RELEASE);
+            _mm_sfence();  // (through the BAR: the cancel lands before the slot's next request)
+            sv->free_at[i].store(t + B3_SVC_RING, std::memory_order_release);
+            it = sv->abandoned.erase(it);
+            sv->ab_pending.fetch_sub(1, std::memory_order_acq_rel);
+            sv->n_reclaimed.fetch_add(1, std::memory_order_relaxed);
+            moved = true;
+        }
+    }
+}
+
+void svc_abandon(Service* sv, uint64_t t, bool posted) {
+    std::lock_guard<std::mutex> lk(sv->ab_mu);
+    sv->abandoned.emplace(t, posted);
+    sv->ab_pending.fetch_add(1, std::memory_order_acq_rel);
+    sv->n_abandoned.fetch_add(1, std::memory_order_relaxed);
+    if (g_svc_trace) fprintf(stderr, "[bw svc] ticket %llu abandoned (%s)\n", (unsigned long long)t, posted ? "posted" : "unposted");
+}
+
+// Start an instance unless one is running (the last launched has not published its end).  With
+// `probe` (the waiting callers, every millisecond) also ask the runtime whether the instance's grid
+// is still on its stream: an instance that finished without publishing its end would otherwise
+// strand every posted ticket (round 5's exit count could miss workers that left before block 0 ran;
+// the count is cumulative now, so this is a second line of defence, counted in n_recovered).
+int svc_ensure(Service* sv, bool probe = false) {
     const uint32_t e = sv->epoch.load(std::memory_order_acquire);
-    if (e != 0 && svc_dead(sv) != e) return BW_OK;
+    if (e != 0 && svc_dead(sv) != e) {
+        if (!probe) return BW_OK;
+        const int64_t now = steady_ns();
+        int64_t last = sv->probe_at.load(std::memory_order_relaxed);
+        if (now - last < 1000000 || !sv->probe_at.compare_exchange_strong(last, now)) return BW_OK;
+        if (hipStreamQuery(sv->st) != hipSuccess) return BW_OK;  // still running
+        std::lock_guard<std::mutex> lk(sv->mu);
+        if (sv->epoch.load(std::memory_order_relaxed) != e || svc_dead(sv) == e) return BW_OK;
+        __atomic_store_n(&sv->ctl->dead, e, __ATOMIC_RELEASE);
+        sv->n_recovered.fetch_add(1, std::memory_order_relaxed);
+        if (g_svc_trace) fprintf(stderr, "[bw svc] epoch %u finished without publishing its end\n", e);
+    }
     std::lock_guard<std::mutex> lk(sv->mu);
     const uint32_t e2 = sv->epoch.load(std::memory_order_relaxed);
     if (e2 != 0 && svc_dead(sv) != e2) return BW_OK;
-    hipSetDevice(sv->device);
+    DeviceGuard g(sv->device);
     (void)hipGetLastError();  // (clear an earlier call's error on this thread)
+    svc_reclaim(sv, true);  // no instance runs: every abandoned ticket holding its slot is handed on
     // the first ticket not yet returned to its caller: the new instance reserves from there
     uint64_t lo = sv->front.load(std::memory_order_relaxed);
     const uint64_t hi = sv->next.load(std::memory_order_acquire);
@@ -463,19 +553,26 @@ void svc_atexit() {
     for (int d = 0; d < 64; d++)
         if (Service* sv = g_svc[d]) {
             __atomic_store_n(&sv->ctl->stop, 1u, __ATOMIC_RELEASE);
-            hipSetDevice(d);
             // (an instance ends within microseconds of the stop word, or at its life limit)
             for (int i = 0; i < 4000 && hipStreamQuery(sv->st) == hipErrorNotReady; i++) usleep(500);
         }
 }
 
+int device_count() {
+    static const int n = [] {
+        int c = 0;
+        return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+    }();
+    return n;
+}
+
 Service* service(int device) {
-    if (device < 0 || device >= 64) return nullptr;
+    if (device < 0 || device >= 64 || device >= device_count()) return nullptr;
     std::lock_guard<std::mutex> lk(g_svc_mu);
     if (!g_svc[device]) {
         auto* sv = new Service();  // lives as long as the process
         sv->device = device;
-        hipSetDevice(device);
+        DeviceGuard g(device);
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
             return nullptr;
@@ -498,8 +595,8 @@ Service* service(int device) {
                 : hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
                       hipStreamCreateWithPriority(&sv->st, hipStreamNonBlocking, least) != hipSuccess)
             return nullptr;
-        if (getenv("BW_SVC_TRACE"))
-            fprintf(stderr, "[svc] stream %s (priority range %d..%d)\n", skind.c_str(), least, greatest);
+        if (g_svc_trace)
+            fprintf(stderr, "[svc] device %d stream %s (priority range %d..%d)\n", device, skind.c_str(), least, greatest);
         int large_bar = 0;
         hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device);
         const char* hr = getenv("BW_SVC_HOST_RING");
@@ -523,6 +620,7 @@ Service* service(int device) {
             sv->free_at[i].store(i);
             sv->sleep[i].store(0);
         }
+        if (const char* f = getenv("BW_SVC_FAULT_AFTER")) sv->fault_after = strtoull(f, nullptr, 10);
         for (int k = 0; k < SVC_COMPLETERS; k++) std::thread(svc_completer, sv, k).detach();
         static std::once_flag once;
         std::call_once(once, [] { atexit(svc_atexit); });
@@ -531,54 +629,88 @@ Service* service(int device) {
     return g_svc[device];
 }
 
-// this thread's copy of its message for the service: in HBM (written through the BAR) or pinned
-struct TlVStage {
-    uint8_t* p = nullptr;
-    uint64_t cap = 0;
-    bool vram = false;
-    ~TlVStage() {
-        if (p) vram ? (void)hipFree(p) : (void)hipHostFree(p);
+// This thread's copy area for its messages to each device's service: in that device's HBM (written
+// through the BAR) or pinned, 64 KiB + 64 (every message the service takes fits, so it is never
+// reallocated).  Allocated on the service's device (a tokio thread's current device is
+// 0 whatever service it calls), one per (thread, device), and given back to the service's pool when
+// the thread exits instead of freed (hipFree would synchronize the device).
+constexpr uint64_t SVC_STAGE_BYTES = B3_MSG_MAX + 64;
+struct TlVStages {
+    uint8_t* p[64] = {};
+    Service* sv[64] = {};
+    ~TlVStages() {
+        for (int d = 0; d < 64; d++)
+            if (p[d]) {
+                std::lock_guard<std::mutex> lk(sv[d]->stage_mu);
+                sv[d]->stage_pool.push_back(p[d]);
+            }
     }
 };
-thread_local TlVStage t_vstage;
+thread_local TlVStages t_vstages;
 
-int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]) {
-    TlVStage& ts = t_vstage;
-    if (ts.cap < len + 16 || ts.vram != sv->vram) {
-        if (ts.p) ts.vram ? (void)hipFree(ts.p) : (void)hipHostFree(ts.p);
-        ts.p = nullptr;
-        ts.cap = 0;
-        const uint64_t want = std::max<uint64_t>(65536 + 64, len + 16);
-        if ((sv->vram ? hipExtMallocWithFlags((void**)&ts.p, want, hipDeviceMallocFinegrained)
-                      : hipHostMalloc((void**)&ts.p, want, hipHostMallocDefault)) != hipSuccess) {
-            ts.p = nullptr;
-            return BW_ENOMEM;
+uint8_t* svc_stage(Service* sv) {
+    TlVStages& ts = t_vstages;
+    const int d = sv->device;
+    if (ts.p[d]) return ts.p[d];
+    {
+        std::lock_guard<std::mutex> lk(sv->stage_mu);
+        if (!sv->stage_pool.empty()) {
+            ts.p[d] = sv->stage_pool.back();
+            sv->stage_pool.pop_back();
         }
-        ts.cap = want;
-        ts.vram = sv->vram;
     }
-    if (len) memcpy(ts.p, data, len);
+    if (!ts.p[d]) {
+        DeviceGuard g(d);
+        uint8_t* p = nullptr;
+        if ((sv->vram ? hipExtMallocWithFlags((void**)&p, SVC_STAGE_BYTES, hipDeviceMallocFinegrained)
+                      : hipHostMalloc((void**)&p, SVC_STAGE_BYTES, hipHostMallocDefault)) != hipSuccess)
+            return nullptr;
+        ts.p[d] = p;
+    }
+    ts.sv[d] = sv;
+    return ts.p[d];
+}
+
+// One message (<= 64 KiB) through the device's service.  BW_EAGAIN when the service could not take
+// it (no staging memory, no instance could be launched, or no slot / digest within SVC_WAIT_US); the
+// ticket is then abandoned and reclaimed, never left taken.
+int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    uint8_t* stage = svc_stage(sv);
+    if (!stage) return BW_EAGAIN;
+    if (len) memcpy(stage, data, len);
     _mm_sfence();  // (the copy reaches HBM before the request that names it: writes through the BAR are
                    // write-combined and only ordered by a fence)
+    const uint64_t call = sv->calls.fetch_add(1, std::memory_order_relaxed);
     const uint64_t t = sv->next.fetch_add(1, std::memory_order_relaxed);
     const uint32_t i = (uint32_t)(t % B3_SVC_RING), seq = (uint32_t)(t + 1);
-    // (a full ring: 4,096 calls in flight; a slot whose call failed stays taken, so bound the wait)
-    for (auto t0 = std::chrono::steady_clock::now(); sv->free_at[i].load(std::memory_order_acquire) != t;) {
+    const auto t0 = std::chrono::steady_clock::now();
+    auto us_now = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); };
+    // the slot is free once its previous ticket returned or was reclaimed (a full ring: 4,096 calls
+    // in flight)
+    for (uint32_t it = 0; sv->free_at[i].load(std::memory_order_acquire) != t; it++) {
         std::this_thread::yield();
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return BW_EHIP;
+        if ((it & 255) != 255) continue;
+        svc_reclaim(sv, false);  // the slot's holder may be an abandoned ticket whose digest landed
+        if (svc_ensure(sv, true) != BW_OK || us_now() > SVC_WAIT_US) {
+            std::lock_guard<std::mutex> lk(sv->ab_mu);
+            if (sv->free_at[i].load(std::memory_order_acquire) == t) break;  // handed over just now
+            sv->abandoned.emplace(t, false);
+            sv->ab_pending.fetch_add(1, std::memory_order_acq_rel);
+            sv->n_abandoned.fetch_add(1, std::memory_order_relaxed);
+            return BW_EAGAIN;
+        }
     }
     B3SvcResp* sl = sv->resp + i;
     B3SvcReq* rq = sv->req + i;
     for (int k = 0; k < 4; k++) __atomic_store_n(&sl->digest[k], b3svc_sentinel(seq, k), __ATOMIC_RELAXED);
-    __atomic_store_n(&rq->ptr, (uint64_t)(uintptr_t)ts.p, __ATOMIC_RELAXED);
+    __atomic_store_n(&rq->ptr, (uint64_t)(uintptr_t)stage, __ATOMIC_RELAXED);
     _mm_sfence();
     __atomic_store_n(&rq->lenseq, len | ((uint64_t)seq << 32), __ATOMIC_RELEASE);
     _mm_sfence();
     int rc = svc_ensure(sv);
+    if (call == sv->fault_after) rc = BW_EAGAIN;  // (tests: give up right after posting)
     uint64_t d[4];
     if (rc == BW_OK && !svc_done(sl, t, d)) {
-        const auto t0 = std::chrono::steady_clock::now();
-        auto us_now = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); };
         bool ok = false;
         const bool spin = sv->waiting.fetch_add(1, std::memory_order_acq_rel) < usable_cpus();
         for (uint32_t it = 0; spin && !ok; it++) {
@@ -598,15 +730,14 @@ int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]
                 if (svc_done(sl, t, d)) break;
                 sv->sleep[i].store(1, std::memory_order_release);  // (woken early, or a timeout)
                 const double us = us_now();
-                if ((rc = svc_ensure(sv)) != BW_OK) break;
+                if ((rc = svc_ensure(sv, true)) != BW_OK) break;
                 if (g_svc_trace && us > next_trace) {
                     fprintf(stderr, "[bw svc] ticket %llu waiting %.0f us: epoch %u dead %u\n", (unsigned long long)t, us,
                             sv->epoch.load(), svc_dead(sv));
                     next_trace = us * 2;
                 }
-                if (us > 10e6) {  // ten seconds: the device is not answering
-                    if (g_svc_trace) fprintf(stderr, "[bw svc] ticket %llu: no digest after 10 s\n", (unsigned long long)t);
-                    rc = BW_EHIP;
+                if (us > SVC_WAIT_US) {  // the device is not running the service
+                    rc = BW_EAGAIN;
                     break;
                 }
             }
@@ -616,20 +747,32 @@ int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]
         sv->waiting.fetch_sub(1, std::memory_order_acq_rel);
     }
     sv->messages.fetch_add(1, std::memory_order_relaxed);
-    if (rc != BW_OK) return rc;  // (the slot stays taken: a late digest must not land in a reused slot)
+    if (rc != BW_OK) {  // never left taken: a late digest may still land, so svc_reclaim waits for it
+        svc_abandon(sv, t, true);
+        return BW_EAGAIN;
+    }
     memcpy(out, d, 32);
     sv->free_at[i].store(t + B3_SVC_RING, std::memory_order_release);
     return BW_OK;
 }
 
-int hash_one(bw_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[32]) {
-    if (len <= CO_MAX_MSG) {
-        if (service_enabled()) {
-            if (Service* sv = service(ctx_device(c))) return service_hash(sv, data, len, out);
-        } else if (Combiner* co = combiner(ctx_device(c))) {
-            return coalesced_hash(co, data, len, out);
-        }
+// A message through the device's small-message path (the service, or the coalescer under
+// BW_DROPIN_SERVICE=0) without any context: BW_EAGAIN when that path cannot take it (over 64 KiB,
+// unavailable, or gave up), so the caller retries through a context it holds.
+int small_call(int device, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    if (len > CO_MAX_MSG) return BW_EAGAIN;
+    if (service_enabled()) {
+        Service* sv = service(device);
+        return sv ? service_hash(sv, data, len, out) : BW_EAGAIN;
     }
+    Combiner* co = device < device_count() ? combiner(device) : nullptr;
+    return co ? coalesced_hash(co, data, len, out) : BW_EAGAIN;
+}
+
+// The caller holds `c`: what the small-message path cannot take runs on c's own launch path.
+int hash_one(bw_ctx* c, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    const int rc = small_call(ctx_device(c), data, len, out);
+    if (rc != BW_EAGAIN) return rc;
     const uint64_t off = 0;
     static const uint8_t empty[16] = {0};
     return bw_blake3_hash_many(c, len ? data : empty, len, &off, &len, 1, out);
@@ -739,4 +882,33 @@ extern "C" int bw_blake3_hash_dropin(bw_ctx* c, const uint8_t* data, uint64_t le
     if (!c || !out || (len && !data)) return BW_EINVAL;
     if (len && kept_lookup(data, len, out)) return BW_OK;
     return hash_one(c, data, len, out);
+}
+
+extern "C" int bw_blake3_hash_dropin_device(int device, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    if (!out || (len && !data) || device < 0 || device >= 64) return BW_EINVAL;
+    if (len && kept_lookup(data, len, out)) return BW_OK;
+    return small_call(device, data, len, out);
+}
+
+extern "C" int bw_blake3_service_faults(int device, uint64_t* abandoned, uint64_t* reclaimed, uint64_t* recovered) {
+    if (device < 0 || device >= 64) return BW_EINVAL;
+    uint64_t a = 0, r = 0, v = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_svc_mu);
+        if (const Service* sv = g_svc[device]) {
+            a = sv->n_abandoned.load();
+            r = sv->n_reclaimed.load();
+            v = sv->n_recovered.load();
+        }
+    }
+    if (abandoned) *abandoned = a;
+    if (reclaimed) *reclaimed = r;
+    if (recovered) *recovered = v;
+    return BW_OK;
+}
+
+extern "C" int bw_device_count(int* n) {
+    if (!n) return BW_EINVAL;
+    *n = device_count();
+    return BW_OK;
 }

@@ -12,9 +12,9 @@ outside the crate's asserted ranges raise ValueError (the crate panics).
 """
 from collections import namedtuple
 
+from . import _lib
 from ._lib import BW_EINVAL, BwError
 from .blake3 import _as_bytes_view, _immutable
-from .context import default_context
 
 MINIMUM_MIN = 64
 MINIMUM_MAX = 1_048_576
@@ -36,15 +36,20 @@ class FastCDC:
                 and MAXIMUM_MIN <= max_size <= MAXIMUM_MAX):
             raise ChunkParameterError("fastcdc size parameters out of range: %d/%d/%d"
                                       % (min_size, avg_size, max_size))
-        ctx = ctx or default_context()
-        self._kept, self._ctx = 0, ctx
+        if ctx is None:  # the drop-in pool over the node's GPUs (backuwup_amd/pool.py)
+            from .pool import default_pool
+            run = default_pool().with_context
+        else:
+            def run(fn):
+                return fn(ctx)
+        self._kept, self._L = 0, _lib.load()
         try:
             buf = _as_bytes_view(source)
             if buf.size and buf.flags.c_contiguous and _immutable(source):
-                cuts, self._kept = ctx.fastcdc_chunks_hashed(buf, min_size, avg_size, max_size)
+                cuts, self._kept = run(lambda c: c.fastcdc_chunks_hashed(buf, min_size, avg_size, max_size))
                 self._buf = buf  # the kept digests name this memory: keep it alive with them
             else:
-                cuts = ctx.fastcdc_chunks(source, min_size, avg_size, max_size)
+                cuts = run(lambda c: c.fastcdc_chunks(source, min_size, avg_size, max_size))
             self._chunks = [Chunk(*c) for c in cuts]
         except BwError as e:
             if e.rc == BW_EINVAL:
@@ -55,7 +60,7 @@ class FastCDC:
     def __del__(self):  # the crate's FastCDC borrows the source; its digests go with the object
         kept, self._kept = getattr(self, "_kept", 0), 0
         if kept:
-            self._ctx.fastcdc_release(kept)
+            self._L.bw_fastcdc_release(kept)
 
     def __iter__(self):
         return iter(self._chunks)

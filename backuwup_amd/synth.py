@@ -202,6 +202,50 @@ def small_files_table(n_files, seed=3, lo=4096, hi=65536, dup_fraction=0.30):
     return int(sizes.sum()), uniq_off[src], sizes[src].astype(np.uint64)
 
 
+# ------------------------------------------------------------------ whole-result fingerprints
+# The canonical record of one blob, packed little-endian with no padding: the fields the reference's
+# path decides (dir_packer.rs:246-286 boundaries and digests, blob_index.rs:130-148 verdicts).  The
+# sha256 over a batch's records in canonical order pins the WHOLE result of a configuration
+# (tests/golden/c{2,3,4}_full.json, made on the CPU by tests/golden/make_full_configs.py).
+CANON_DTYPE = np.dtype([("file", "<u8"), ("offset", "<u8"), ("length", "<u8"), ("gear_hash", "<u8"),
+                        ("digest", "u1", (32,)), ("is_dup", "u1")], align=False)
+assert CANON_DTYPE.itemsize == 65
+
+
+class ResultDigest:
+    """Incremental fingerprint of a result array (any dtype with the CANON_DTYPE fields): blob
+    count, duplicate count and bytes, and sha256 over the canonical records (plus one over the
+    digests alone, which localises a mismatch to hashing or to boundaries/verdicts)."""
+
+    def __init__(self):
+        import hashlib
+        self.records, self.digests = hashlib.sha256(), hashlib.sha256()
+        self.n = self.n_dup = self.bytes = self.dup_bytes = 0
+
+    def update(self, blobs, file_base=0):
+        rec = np.zeros(len(blobs), dtype=CANON_DTYPE)
+        for f in ("offset", "length", "gear_hash", "digest", "is_dup"):
+            rec[f] = blobs[f]
+        rec["file"] = np.asarray(blobs["file"], dtype=np.uint64) + np.uint64(file_base)
+        self.records.update(rec.tobytes())
+        self.digests.update(np.ascontiguousarray(rec["digest"]).tobytes())
+        lens = rec["length"].astype(np.uint64)
+        dup = rec["is_dup"] != 0
+        self.n += len(rec)
+        self.n_dup += int(dup.sum())
+        self.bytes += int(lens.sum())
+        self.dup_bytes += int(lens[dup].sum())
+        return self
+
+    def summary(self):
+        return {"blobs": self.n, "dup_blobs": self.n_dup, "bytes": self.bytes, "dup_bytes": self.dup_bytes,
+                "sha256_records": self.records.hexdigest(), "sha256_digests": self.digests.hexdigest()}
+
+
+def result_digest(blobs):
+    return ResultDigest().update(blobs).summary()
+
+
 def _text_piece(rng, nbytes, vocab, ws, wl1, pw):
     """nbytes of words drawn from a Zipf-weighted vocabulary (vectorized gather)."""
     nw = int(nbytes / float(wl1 @ pw) * 1.05) + 16

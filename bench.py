@@ -331,10 +331,14 @@ def main():
             _lib.check(rc, c.h)
         return t_out.value
 
+    first_res = [None]  # the session's first batch (fresh index): the whole-result parity check's input
+
     def wait(c, t):
         rc = L.bw_wait(c.h, t, c_out, c_cap, c_n)
         if rc:
             _lib.check(rc, c.h)
+        if first_res[0] is None:
+            first_res[0] = out_buf[:n_out.value].copy()
 
     def step():
         k = step_no[0] % len(ctxs)
@@ -356,12 +360,14 @@ def main():
     ctx.index_reset(index_hint)
     for _ in range(args.warmup):
         step()
+    if first_res[0] is None and not args.no_check:
+        step()  # (--warmup 0: one untimed batch for the parity check)
     drain()
     torch.cuda.synchronize()
 
     check = None
     if not args.no_check:
-        check = parity_spot_check(args.workload, ctx, data, file_off, file_len, rank)
+        check = parity_spot_check(args, ctx, data, file_off, file_len, rank, first_res[0])
         log("rank %d: parity spot check %s" % (rank, check))
         if not check["bit_exact"]:
             raise SystemExit("parity check failed")
@@ -1107,12 +1113,50 @@ def pmc_traffic(args, kernel):
     return pmc["kernels"][kernel]["hbm_bytes_per_launch"], prov, round(path_bytes / (args.gib * (1 << 30)), 3)
 
 
-def parity_spot_check(workload, ctx, data, file_off, file_len, rank):
-    """Bit-exactness against the CPU oracle on the first ~64 MiB of blobs (C2) or on a sample of
-    files (other workloads), from the last warm-up batch's results."""
+def whole_result_fixture(args, rank):
+    """The committed oracle fixture of this rank's whole first batch, if one exists for exactly this
+    workload (tests/golden/c{2,3,4}_full.json: bench.py's rank-0 corpora at their default sizes)."""
+    name = {"c2": "c2", "c3": "c3", "c4": "c4"}.get(args.workload)
+    path = os.path.join(ROOT, "tests", "golden", "%s_full.json" % name) if name else None
+    if rank != 0 or not path or not os.path.exists(path):
+        return None, path
+    fx = json.load(open(path))
+    same = {"c2": args.gib * (1 << 30) == fx.get("bytes"),
+            "c3": args.gib * (1 << 30) == fx.get("base_bytes"),
+            "c4": args.files == fx.get("files")}[name]
+    return (fx if same else None), path
+
+
+def parity_spot_check(args, ctx, data, file_off, file_len, rank, first=None):
+    """Bit-exactness of the session's first batch (fresh index).  WHOLE result: where the oracle's
+    fixture of this exact corpus is committed (C2 16 GiB, C3 4 GiB x 16, C4 1 M files; rank 0), the
+    sha256 over every blob's (file, offset, length, gear_hash, digest, is_dup) must equal it.  Plus a
+    live oracle run here: the first ~64 MiB of blobs (C2) or a sample of files (other workloads)."""
+    from backuwup_amd import synth
+    out = {}
+    res = first if first is not None else ctx.results()
+    fx, path = whole_result_fixture(args, rank)
+    if fx is not None and first is not None:
+        have = synth.result_digest(res)
+        keys = ("blobs", "dup_blobs", "bytes", "dup_bytes", "sha256_digests", "sha256_records")
+        ok = all(have[k] == fx[k] for k in keys)
+        out["whole_result_detail"] = {
+            "bit_exact": ok, "fixture": os.path.relpath(path, ROOT), "blobs": have["blobs"],
+            "dup_blobs": have["dup_blobs"], "sha256_records": have["sha256_records"],
+            "scope": "every blob of the first batch against the oracle's fixture of the same corpus"}
+    spot = spot_check(args.workload, res, data, file_off, file_len, rank)
+    out.update(spot)
+    whole = out.get("whole_result_detail")
+    # true only when the whole first batch was compared and equal; false when no fixture applies
+    out["whole_result"] = bool(whole and whole["bit_exact"])
+    out["bit_exact"] = bool(spot["bit_exact"] and (whole is None or whole["bit_exact"]))
+    return out
+
+
+def spot_check(workload, res, data, file_off, file_len, rank):
+    """The oracle run live on the first ~64 MiB of blobs (C2) or on a sample of files."""
     import numpy as np
     from oracle import oracle
-    res = ctx.results()
     if workload == "c2":
         n = int(file_len[0])
         ends = np.cumsum(res["length"].astype(np.int64))

@@ -48,7 +48,11 @@ enum {
     BW_ESTATE = -6,     /* call order violated (e.g. bw_results before a batch was submitted)   */
     BW_ECRYPTO = -7,    /* an AES-GCM tag did not verify (PackfileError::CryptoError)           */
     BW_EFORMAT = -8,    /* bincode deserialization failed (PackfileError::SerializationError)   */
-    BW_ECOMM = -9       /* the exchange transport failed (RCCL, or the caller's host all-to-all) */
+    BW_ECOMM = -9,      /* the exchange transport failed (RCCL, or the caller's host all-to-all) */
+    BW_EAGAIN = -10     /* bw_blake3_hash_dropin_device only: the device's hash service could not
+                           take this call (message over BW_COALESCE_MAX_MSG, service unavailable,
+                           or no digest within its bound); nothing was changed, retry the message
+                           through a context (bw_blake3_hash_many)                                 */
 };
 
 /* fastcdc::v2020 size bounds (asserted by FastCDC::with_level) */
@@ -151,9 +155,23 @@ int bw_blake3_hash(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[3
  * that a chunk slice of a live bw_fastcdc_chunks_hashed source is answered from its kept digest.
  * Only for callers that guarantee those bytes are unchanged while the handle lives. */
 int bw_blake3_hash_dropin(bw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t out[32]);
+/* The same without a context, for callers that hold none (the Rust blake3::hash drop-in: each thread
+ * names the device it hashes on, INTEGRATION.md "every GPU of the node"): the kept digests first,
+ * then messages up to BW_COALESCE_MAX_MSG through `device`'s hash service.  Returns BW_EAGAIN, with
+ * nothing changed, where bw_blake3_hash_dropin would have used its context: a larger message, a
+ * service that is unavailable, or a call that got no slot or digest within 10 s (its ticket is then
+ * cancelled and its ring slot handed on, so later calls are unaffected).  The caller then hashes the
+ * message through a context it holds (bw_blake3_hash_many). */
+int bw_blake3_hash_dropin_device(int device, const uint8_t* data, uint64_t len, uint8_t out[32]);
 /* launches (hash-service instances, or coalesced batches) and the messages they carried on
  * `device` since the process started */
 int bw_blake3_coalesce_stats(int device, uint64_t* batches, uint64_t* messages);
+/* hash-service calls on `device` that gave up (BW_EAGAIN) and whose tickets were abandoned; of
+ * those, tickets already handed back; and instances found finished without having published their
+ * end (the host then marks them ended itself) */
+int bw_blake3_service_faults(int device, uint64_t* abandoned, uint64_t* reclaimed, uint64_t* recovered);
+/* visible HIP devices (the Rust drop-ins' pool spreads over them) */
+int bw_device_count(int* n);
 /* n independent messages data[offsets[i] .. offsets[i]+lengths[i]) -> out[32*i..] */
 int bw_blake3_hash_many(bw_ctx* ctx, const uint8_t* data, uint64_t data_len,
                         const uint64_t* offsets, const uint64_t* lengths, uint64_t n,

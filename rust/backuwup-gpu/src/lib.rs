@@ -12,8 +12,8 @@
 //!
 //! A maintainer swaps `use fastcdc::v2020::FastCDC;` for `use backuwup_gpu::fastcdc::v2020::FastCDC;`
 //! and `blake3::hash` for `backuwup_gpu::blake3::hash` in `dir_packer.rs`; nothing else changes.
-//! The drop-ins run on a per-thread default context (device `BACKUWUP_GPU_DEVICE`, default 0),
-//! because the reference's calls carry no context.  Each is one synchronous GPU round trip; the
+//! The drop-ins run on a pool of contexts over every GPU of the node (`BACKUWUP_GPU_DEVICES`,
+//! default all), each thread with a home device, because the reference's calls carry no context.  Each is one synchronous GPU round trip; the
 //! batched session ([`Context::submit_host`] / [`Context::wait`] with a shared [`Index`]) is the
 //! integration a packer should use ("A backup session").
 //!
@@ -43,6 +43,7 @@ pub mod ffi {
     pub const BW_ECRYPTO: c_int = -7;
     pub const BW_EFORMAT: c_int = -8;
     pub const BW_ECOMM: c_int = -9;
+    pub const BW_EAGAIN: c_int = -10;
 
     pub const BW_F_NO_HASH: u32 = 1;
     pub const BW_F_NO_DEDUP: u32 = 2;
@@ -174,7 +175,11 @@ pub mod ffi {
         pub fn bw_blake3_kept_hits() -> u64;
         pub fn bw_blake3_hash(ctx: *mut bw_ctx, data: *const u8, len: u64, out: *mut u8) -> c_int;
         pub fn bw_blake3_hash_dropin(ctx: *mut bw_ctx, data: *const u8, len: u64, out: *mut u8) -> c_int;
+        pub fn bw_blake3_hash_dropin_device(device: c_int, data: *const u8, len: u64, out: *mut u8) -> c_int;
         pub fn bw_blake3_coalesce_stats(device: c_int, batches: *mut u64, messages: *mut u64) -> c_int;
+        pub fn bw_blake3_service_faults(device: c_int, abandoned: *mut u64, reclaimed: *mut u64,
+                                        recovered: *mut u64) -> c_int;
+        pub fn bw_device_count(n: *mut c_int) -> c_int;
         pub fn bw_blake3_hash_many(ctx: *mut bw_ctx, data: *const u8, data_len: u64, offsets: *const u64,
                                    lengths: *const u64, n: u64, out: *mut u8) -> c_int;
 
@@ -623,26 +628,72 @@ impl Drop for Comm {
 }
 
 // The drop-ins' contexts: the reference's calls carry none, and tokio runs one worker thread per
-// core (client/src/main.rs:43, 256 on an MI355X node), so the threads share a small pool
-// (BACKUWUP_GPU_CONTEXTS, default 16) instead of holding one context each; a thread takes the
-// first free one from its own starting point and only blocks when all are busy.  blake3::hash
-// of small messages needs none of them: it goes to the library's hash service (a persistent kernel
-// serving every thread's calls, bw_blake3_hash).
-static POOL: std::sync::OnceLock<Vec<std::sync::Mutex<Context>>> = std::sync::OnceLock::new();
+// core (client/src/main.rs:43, 256 on an MI355X node), so the threads share a pool of contexts
+// instead of holding one each.  The pool spans every GPU of the node: the devices
+// are BACKUWUP_GPU_DEVICES ("all", the default, or a list such as "0,1,2,3"; a device may repeat),
+// or the single BACKUWUP_GPU_DEVICE of earlier versions; BACKUWUP_GPU_CONTEXTS contexts per listed
+// device (default 16).  Thread k (in order of first use) gets home device k mod n: its FastCDC::new
+// takes the first free context from its home slot on (contexts alternate devices, so a thread that
+// finds its own device's contexts busy moves to the next device's), and its blake3::hash of a small
+// message goes to its home device's hash service.  Files are independent (CDC restarts per file,
+// dir_packer.rs:254) and the dedup gate stays the caller's (add_blob), so spreading the calls over
+// the devices changes no result.
+struct Pool {
+    devices: Vec<i32>,
+    contexts: Vec<std::sync::Mutex<Context>>,  // context j is on devices[j % devices.len()]
+}
+
+static POOL: std::sync::OnceLock<Pool> = std::sync::OnceLock::new();
 static NEXT_SLOT: std::sync::atomic::AtomicUsize = std::sync::atomic::AtomicUsize::new(0);
 thread_local! {
     static SLOT: RefCell<Option<usize>> = RefCell::new(None);
 }
 
+/// The devices the drop-ins use (see above).
+pub fn pool_devices() -> Vec<i32> {
+    let listed = std::env::var("BACKUWUP_GPU_DEVICES").ok();
+    match listed.as_deref().map(str::trim) {
+        Some(v) if !v.is_empty() && v != "all" => {
+            v.split(',').map(|d| d.trim().parse().expect("BACKUWUP_GPU_DEVICES: device numbers")).collect()
+        }
+        _ => {
+            if listed.is_none() {
+                if let Some(d) = std::env::var("BACKUWUP_GPU_DEVICE").ok().and_then(|v| v.parse().ok()) {
+                    return vec![d];
+                }
+            }
+            let mut n: c_int = 0;
+            let rc = unsafe { ffi::bw_device_count(&mut n) };
+            assert!(rc == ffi::BW_OK && n > 0, "no MI355X for backuwup-gpu");
+            (0..n).collect()
+        }
+    }
+}
+
+fn pool() -> &'static Pool {
+    POOL.get_or_init(|| {
+        let devices = pool_devices();
+        let per = std::env::var("BACKUWUP_GPU_CONTEXTS").ok().and_then(|v| v.parse().ok()).unwrap_or(16usize).max(1);
+        let contexts = (0..per * devices.len())
+            .map(|j| std::sync::Mutex::new(Context::new(devices[j % devices.len()]).expect("no MI355X for backuwup-gpu")))
+            .collect();
+        Pool { devices, contexts }
+    })
+}
+
+fn home_slot() -> usize {
+    SLOT.with(|s| *s.borrow_mut().get_or_insert_with(|| NEXT_SLOT.fetch_add(1, std::sync::atomic::Ordering::Relaxed)))
+}
+
+/// The device this thread's small `blake3::hash` calls go to.
+fn home_device() -> i32 {
+    let p = pool();
+    p.devices[home_slot() % p.devices.len()]
+}
+
 fn with_default<R>(f: impl FnOnce(&mut Context) -> R) -> R {
-    let pool = POOL.get_or_init(|| {
-        let dev = std::env::var("BACKUWUP_GPU_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0);
-        let n = std::env::var("BACKUWUP_GPU_CONTEXTS").ok().and_then(|v| v.parse().ok()).unwrap_or(16usize).max(1);
-        (0..n).map(|_| std::sync::Mutex::new(Context::new(dev).expect("no MI355X for backuwup-gpu"))).collect()
-    });
-    let start = SLOT.with(|s| {
-        *s.borrow_mut().get_or_insert_with(|| NEXT_SLOT.fetch_add(1, std::sync::atomic::Ordering::Relaxed))
-    }) % pool.len();
+    let pool = &pool().contexts;
+    let start = home_slot() % pool.len();
     for k in 0..pool.len() {
         if let Ok(mut c) = pool[(start + k) % pool.len()].try_lock() {
             return f(&mut c);
@@ -748,18 +799,24 @@ pub mod blake3 {
 
     /// `blake3::hash(input)` -- standard unkeyed BLAKE3, 32-byte output, computed on the GPU.  A
     /// chunk of a live `FastCDC` drop-in is answered from the digest its construction kept (safe
-    /// Rust cannot change those bytes while the `FastCDC` borrows them); a small message from any
-    /// thread goes to the library's hash service (no launch per call).
+    /// Rust cannot change those bytes while the `FastCDC` borrows them); a small message goes to
+    /// the hash service of this thread's home device (no launch per call, no context held while
+    /// it waits).  What the service does not take -- a message over 64 KiB, or a call it could not
+    /// serve in time (`BW_EAGAIN`: the ticket is cancelled and its slot handed on, later calls are
+    /// unaffected) -- is hashed through a pool context's own launch path.  Only a failed GPU (the
+    /// launch path's error) ends in a panic: the crate's `hash` has no error to return.
     pub fn hash(input: &[u8]) -> Hash {
-        if input.len() as u64 <= crate::ffi::BW_COALESCE_MAX_MSG {
-            // the hash service: the library only reads the context's device, so no pool slot is held
-            // while the call waits for its digest (holding one would cap the calls in flight)
-            let raw = super::with_default(|c| c.raw);
-            let mut h = [0u8; 32];
-            let rc = unsafe { crate::ffi::bw_blake3_hash_dropin(raw, input.as_ptr(), input.len() as u64, h.as_mut_ptr()) };
-            assert_eq!(rc, crate::ffi::BW_OK, "GPU hashing failed");
+        let mut h = [0u8; 32];
+        let rc = unsafe {
+            crate::ffi::bw_blake3_hash_dropin_device(super::home_device(), input.as_ptr(), input.len() as u64,
+                                                     h.as_mut_ptr())
+        };
+        if rc == crate::ffi::BW_OK {
             return Hash(h);
         }
-        Hash(super::with_default(|c| c.blake3_hash_dropin(input)).expect("GPU hashing failed"))
+        assert_eq!(rc, crate::ffi::BW_EAGAIN, "bw_blake3_hash_dropin_device: invalid call");
+        let len = input.len() as u64;
+        let d = super::with_default(|c| c.blake3_hash_many(input, &[0], &[len])).expect("the GPU failed");
+        Hash(d[0])
     }
 }

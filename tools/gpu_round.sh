@@ -34,6 +34,11 @@ for s in $STEPS; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu --maxfail 20 -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python __graft_entry__.py ;;
+    sel) step pytest_sel 600 python -u -m pytest ${PYTEST_SEL:-tests/test_gpu_dropin_pool.py} -m gpu -v -p no:cacheprovider \
+           --timeout 240 --timeout-method thread ;;
+    full) step pytest_full 600 python -u -m pytest tests/test_gpu_full_configs.py -m gpu -v -p no:cacheprovider \
+           --timeout 300 --timeout-method thread ;;
+    bench20) step bench20 300 python bench.py --steps 20 --no-cpu-baseline ;;
     collide) step collide 120 ./build_ab/collide "$OUT/blake3_prefix_collision.json" 14 32768 1 ;;
     slab) step slab 900 bash tools/gpu_slab.sh ;;
     dropin) step dropin 1100 bash tools/gpu_dropin.sh ;;

@@ -8,7 +8,7 @@ for i in $(seq 1 ${GPU_TRIES:-40}); do
   # .last_call.json and any .graft_* marker included) goes to profiles/<round>/calls/<time>/; files
   # over 8 MiB (raw traces) are listed there by size instead of copied
   if [ -n "$(ls -A gpurun_out 2>/dev/null)" ]; then
-    d=profiles/${GPU_ROUND:-r05}/calls/$(date +%Y%m%d_%H%M%S); mkdir -p "$d"
+    d=profiles/${GPU_ROUND:-r06}/calls/$(date +%Y%m%d_%H%M%S); mkdir -p "$d"
     (cd gpurun_out && find . -type f -size -8M -exec cp --parents {} "../$d" \;)
     (cd gpurun_out && find . -type f -size +8M -printf '%s %p\n') > "$d/_large_files.txt"
     rm -rf gpurun_out/* gpurun_out/.[!.]*
