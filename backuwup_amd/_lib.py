@@ -129,6 +129,8 @@ SIGNATURES = [
     ("bw_comm_set_timeout", ctypes.c_int, [vp, ctypes.c_uint32]),
     ("bw_comm_status", ctypes.c_int, [vp]),
     ("bw_comm_init_host", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.POINTER(vp)]),
+    ("bw_comm_init_all", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(vp)]),
+    ("bw_comm_init_local", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(vp)]),
     ("bw_comm_destroy", None, [vp]),
     ("bw_comm_last_error", ctypes.c_char_p, [vp]),
     ("bw_comm_set_capacity", ctypes.c_int, [vp, ctypes.c_uint64]),

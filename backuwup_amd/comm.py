@@ -72,6 +72,28 @@ class Comm:
         check(L.bw_comm_init_host(device, rank, world, cb, None, ctypes.byref(h)))
         return cls(h, keep=cb)
 
+    @classmethod
+    def local(cls, devices):
+        """The ranks of ONE process over an in-process host transport (bw_comm_init_local): a
+        list of len(devices) communicators, rank r on devices[r] (a device may repeat).  Drive
+        each rank from its own thread."""
+        L = _lib.load()
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*devices)
+        hs = (ctypes.c_void_p * n)()
+        check(L.bw_comm_init_local(devs, n, hs))
+        return [cls(ctypes.c_void_p(h)) for h in hs]
+
+    @classmethod
+    def all(cls, devices, timeout_ms=_lib.BW_COMM_DEFAULT_TIMEOUT_MS):
+        """The ranks of ONE process over RCCL (bw_comm_init_all): one distinct device per rank."""
+        L = _lib.load()
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*devices)
+        hs = (ctypes.c_void_p * n)()
+        check(L.bw_comm_init_all(devs, n, int(timeout_ms), hs))
+        return [cls(ctypes.c_void_p(h)) for h in hs]
+
     def set_capacity(self, cap):
         """Obsolete (round 5): exchanges size every transfer from their own counts; ignored."""
         check(self._L.bw_comm_set_capacity(self.h, int(cap)))

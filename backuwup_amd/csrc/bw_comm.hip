@@ -19,9 +19,13 @@
 //     returns BW_ECOMM at once.
 #include <string.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include <rccl/rccl.h>
 
@@ -39,6 +43,7 @@ struct bw_comm {
                                           // [2W, 4W) / [4W, 6W) an allgather's send / receive
     bw_host_all_to_all host_fn = nullptr;  // or the caller's host transport
     void* user = nullptr;
+    void (*user_free)(void*) = nullptr;    // releases `user` with the communicator (bw_comm_init_local)
     void* exq = nullptr;                   // exchanges waiting for their counts (bw_capi.hip)
     uint32_t timeout_ms = BW_COMM_DEFAULT_TIMEOUT_MS;
     bool failed = false;                   // aborted: every call returns BW_ECOMM
@@ -425,7 +430,135 @@ extern "C" void bw_comm_destroy(bw_comm* c) {
     if (c->ctl_st) hipStreamDestroy(c->ctl_st);
     if (c->ctl_buf) hipFree(c->ctl_buf);
     if (c->pin_send) hipHostFree(c->pin_send);
+    if (c->user_free) c->user_free(c->user);
     delete c;
+}
+
+// ---------------------------------------------------------------- the ranks of one process
+//  The reference packs a backup inside one process (client/src/backup/mod.rs:64):
+// these two calls give such a process N ranks, one per context, without one process per GPU.  The
+// ranks are then driven from N threads (one per rank, like the tokio tasks that feed the packer):
+// each submits its share of the files, calls bw_exchange_dedup with its own context and
+// communicator, in the same batch order on every rank.
+
+namespace {
+
+// An all-to-all between the threads of one process: each rank posts its buffers, waits until all
+// have, copies its column out of every peer's send buffer, and waits until all have copied (so no
+// send buffer is reused under a peer still reading it).  A rank that does not arrive within the
+// group's deadline breaks the group: every waiting and later call fails (-> BW_ECOMM).
+struct LocalGroup {
+    int n = 0;
+    uint32_t timeout_ms = BW_COMM_DEFAULT_TIMEOUT_MS;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0, copied = 0;
+    uint64_t gen_arrive = 0, gen_copy = 0;
+    bool broken = false;
+    std::vector<const uint8_t*> send;
+    std::vector<uint64_t> bytes;
+    std::atomic<int> refs{0};
+};
+struct LocalMember {
+    LocalGroup* g;
+    int rank;
+};
+
+int local_all_to_all(void* user, const void* send, void* recv, uint64_t bytes) {
+    auto* m = (LocalMember*)user;
+    LocalGroup& g = *m->g;
+    const int r = m->rank;
+    std::unique_lock<std::mutex> lk(g.mu);
+    const auto dl = Clock::now() + std::chrono::milliseconds(g.timeout_ms);
+    auto wait_gen = [&](uint64_t& gen_now, uint64_t gen) {
+        if (!g.cv.wait_until(lk, dl, [&] { return gen_now != gen || g.broken; })) g.broken = true;
+        g.cv.notify_all();
+        return !g.broken;
+    };
+    if (g.broken) return 1;
+    g.send[r] = (const uint8_t*)send;
+    g.bytes[r] = bytes;
+    const uint64_t ga = g.gen_arrive;
+    if (++g.arrived == g.n) {
+        g.arrived = 0;
+        g.gen_arrive++;
+        g.cv.notify_all();
+    } else if (!wait_gen(g.gen_arrive, ga)) {
+        return 1;
+    }
+    for (int p = 0; p < g.n; p++)
+        if (g.bytes[p] != bytes) {  // the library pads to equal splits: a mismatch is a broken session
+            g.broken = true;
+            g.cv.notify_all();
+            return 1;
+        }
+    lk.unlock();
+    for (int p = 0; p < g.n; p++) memcpy((uint8_t*)recv + (uint64_t)p * bytes, g.send[p] + (uint64_t)r * bytes, bytes);
+    lk.lock();
+    const uint64_t gc = g.gen_copy;
+    if (++g.copied == g.n) {
+        g.copied = 0;
+        g.gen_copy++;
+        g.cv.notify_all();
+        return g.broken ? 1 : 0;
+    }
+    return wait_gen(g.gen_copy, gc) ? 0 : 1;
+}
+
+void local_member_free(void* user) {
+    auto* m = (LocalMember*)user;
+    if (m->g->refs.fetch_sub(1) == 1) delete m->g;
+    delete m;
+}
+
+}  // namespace
+
+extern "C" int bw_comm_init_local(const int* devices, int n, bw_comm** out) {
+    if (!devices || !out || n < 1 || !world_ok(0, n)) return BW_EINVAL;
+    for (int r = 0; r < n; r++) out[r] = nullptr;
+    auto* g = new LocalGroup();
+    g->n = n;
+    g->send.assign(n, nullptr);
+    g->bytes.assign(n, 0);
+    g->refs = n;
+    for (int r = 0; r < n; r++) {
+        auto* m = new LocalMember{g, r};
+        if (int rc = bw_comm_init_host(devices[r], r, n, local_all_to_all, m, &out[r])) {
+            delete m;
+            g->refs -= n - r;  // the members that were never attached (this one included)
+            if (r == 0) delete g;
+            for (int k = 0; k < r; k++) {  // the last one out deletes the group
+                bw_comm_destroy(out[k]);
+                out[k] = nullptr;
+            }
+            return rc;
+        }
+        out[r]->user_free = local_member_free;
+    }
+    return BW_OK;
+}
+
+extern "C" int bw_comm_init_all(const int* devices, int n, uint32_t timeout_ms, bw_comm** out) {
+    if (!devices || !out || n < 1 || !world_ok(0, n) || !timeout_ms) return BW_EINVAL;
+    for (int r = 0; r < n; r++) out[r] = nullptr;
+    uint8_t id[BW_COMM_ID_BYTES];
+    if (int rc = bw_comm_unique_id(id)) return rc;
+    // every rank's initialisation must be in progress at once (RCCL meets the ranks there): one
+    // thread per rank, as the ranks of separate processes would be
+    std::vector<int> rc(n, BW_OK);
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; r++)
+        th.emplace_back([&, r] { rc[r] = bw_comm_init_timeout(devices[r], r, n, id, timeout_ms, &out[r]); });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < n; r++)
+        if (rc[r] != BW_OK) {
+            for (int k = 0; k < n; k++) {
+                bw_comm_destroy(out[k]);
+                out[k] = nullptr;
+            }
+            return rc[r];
+        }
+    return BW_OK;
 }
 
 // Kept for the ABI (round 4 sized fixed buckets with it): every transfer is now sized exactly from

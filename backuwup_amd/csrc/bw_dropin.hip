@@ -802,8 +802,23 @@ extern "C" int bw_fastcdc_chunks_hashed(bw_ctx* c, const uint8_t* src, uint64_t 
     // the file goes up as one pageable hipMemcpy, not through the context's pinned staging ring: the
     // reference's tasks call this from many threads at once (one mmap'd file each), and 16 callers
     // each fanning their memcpy out over 16 ring threads ran at 35 GB/s on C1 against 47-56 for
-    // the runtime's own pageable copies (profiles/r04/s05_keptab)
-    if (int rc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n)) return rc;
+    // the runtime's own pageable copies (profiles/r04/s05_keptab).  BW_DROPIN_REGISTER_MIB=m (A/B,
+    // VERDICT r5 #6): files of at least m MiB are page-locked in place for the copy instead
+    // (hipHostRegister, read-only: the reference's mmap is a read-only mapping), so the runtime DMAs
+    // them directly, then unregistered.
+    static const uint64_t reg_min = [] {
+        const char* e = getenv("BW_DROPIN_REGISTER_MIB");
+        return e && atoll(e) > 0 ? (uint64_t)atoll(e) << 20 : UINT64_MAX;
+    }();
+    void* reg = nullptr;
+    if (len >= reg_min) {
+        const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095, b = ((uintptr_t)src + len + 4095) & ~(uintptr_t)4095;
+        if (hipHostRegister((void*)a, b - a, hipHostRegisterDefault | hipHostRegisterReadOnly) == hipSuccess) reg = (void*)a;
+        else (void)hipGetLastError();  // (not registrable: the pageable copy below)
+    }
+    const int prc = bw_process_files(c, src, len, &off, &len, 1, &p, tmp.data(), tmp.size(), &n);
+    if (reg) hipHostUnregister(reg);
+    if (prc) return prc;
     *n_out = n;
     if (n > cap) return BW_ENOSPC;
     auto k = std::make_shared<Kept>();

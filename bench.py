@@ -41,6 +41,7 @@ CALIBRATE_MS = 150.0
 # the dominant kernel; each mark costs the stream ~5 us, so the full stage split is taken after,
 # on the same batch with nothing beside it
 PROFILE_MASK_TIMED = (1 << 4) | (1 << 5)  # b3_leaf start, b3_tree start
+HOLD_S, HOLD_SKIP_S, PASS_S = 3.0, 0.5, 1.5  # untimed power holds after the timed steps (seconds)
 
 
 def log(*a):
@@ -139,6 +140,8 @@ def main():
                     help="also time the CPU baseline on os.cpu_count() threads (a whole node that is yours; the "
                          "default measures this GPU's 16-core share and one core, and estimates the node)")
     ap.add_argument("--no-power", action="store_true", help="do not sample socket power during the timed steps")
+    ap.add_argument("--no-holds", action="store_true",
+                    help="skip the untimed power holds after the timed steps (sustained pipeline, each pass alone)")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--streams", type=int, default=None,
                     help="batches in flight: consecutive steps alternate between this many contexts/streams "
@@ -207,7 +210,7 @@ def main():
     import ctypes
 
     from backuwup_amd import BLOB_DTYPE, Context, Index, _lib, make_params
-    from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
+    from backuwup_amd._lib import (BW_B3_LOADS_DEFAULT, BW_F_NO_DEDUP, BW_F_NO_HASH, BW_OPT_B3_LOADS, BW_OPT_DEPTH, BW_OPT_LATENCY_STREAM, BW_OPT_ORDER_HASH,
                                    BW_OPT_B3_GROUP, BW_OPT_B3_UPPER, BW_OPT_PROFILE_MASK, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_WAVES, BW_OPT_SPLIT, STAGES)
 
     rank = int(os.environ.get("RANK", 0))
@@ -429,6 +432,61 @@ def main():
     log("rank %d: %d blobs/step, stage ms/step: %s, host submit ms/step %.3f" %
         (rank, len(res), {k: round(v, 3) for k, v in per.items()}, host_ms[0] / args.steps))
 
+    # Power evidence, after the timed steps and outside them: socket power lags, so
+    # a short timed window mostly samples the ramp.  `sustained` keeps the same pipeline running for
+    # HOLD_S and drops the first HOLD_SKIP_S of samples; `passes` holds each pass alone for PASS_S:
+    # the scan (the batch chunked with BW_F_NO_HASH) and the BLAKE3 pass (the batch's own chunks
+    # submitted as whole-file blobs: unit table + k_b3_lines + k_b3_upper, no scan).
+    holds = None
+    if not multi and host is None and not args.no_power and not args.no_holds and rank == 0:
+        for c in ctxs:
+            c.profile_enable(False)
+
+        def hold(seconds, one):
+            sampler = PowerSampler(local)
+            t0, nb = time.perf_counter(), 0
+            while time.perf_counter() - t0 < seconds:
+                one()
+                nb += 1
+            drain()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            pw, missing = sampler.stop(skip_s=HOLD_SKIP_S)
+            return nb, el, pw, missing
+
+        nb, el_h, pw, missing = hold(HOLD_S, step)
+        holds = {"sustained": dict(pw or {"missing": missing}, seconds=round(el_h, 3), batches=nb,
+                                   gbs=round(processed * nb / el_h / 1e9, 1), skipped_s=HOLD_SKIP_S,
+                                   what="the timed pipeline (same contexts, same batch) kept running untimed")}
+        pn = make_params(flags=BW_F_NO_HASH | BW_F_NO_DEDUP)
+        cut_off = (file_off[res["file"].astype(np.int64)] + res["offset"]).astype(np.uint64)
+        cut_len = np.ascontiguousarray(res["length"], dtype=np.uint64)
+        ph = make_params(flags=BW_F_NO_DEDUP)
+        ph.small_file_threshold = int(cut_len.max()) if len(cut_len) else 0  # every chunk one whole blob
+        passes = {}
+        for name, pp, fo, fl, what in (
+                ("scan", pn, file_off, file_len, "the batch with BW_F_NO_HASH: k_scan + boundary resolution"),
+                ("blake3", ph, cut_off, cut_len, "the batch's chunks as whole-file blobs: k_b3_lines + k_b3_upper")):
+            def one(pp=pp, fo=fo, fl=fl):
+                k = step_no[0] % len(ctxs)
+                step_no[0] += 1
+                c = ctxs[k]
+                rc = L.bw_submit_device(c.h, c_data, n, fo.ctypes.data_as(_lib.u64p), fl.ctypes.data_as(_lib.u64p),
+                                        len(fo), ctypes.byref(pp), c_t)
+                if rc:
+                    _lib.check(rc, c.h)
+                inflight.append((c, t_out.value))
+                if len(inflight) >= len(ctxs):
+                    c0, t0_ = inflight.pop(0)
+                    wait(c0, t0_)
+            nb, el_h, pw, missing = hold(PASS_S, one)
+            passes[name] = dict(pw or {"missing": missing}, seconds=round(el_h, 3), batches=nb,
+                                gbs=round(processed * nb / el_h / 1e9, 1), what=what)
+            if pw:
+                passes[name]["pj_per_byte"] = round(pw["socket_w_median"] / (processed * nb / el_h) * 1e12, 1)
+        holds["passes"] = passes
+        log("rank 0: power holds %s" % json.dumps(holds))
+
     total_bytes = processed * world * args.steps
     value = total_bytes / el / 1e9
     ms_per_step = el / args.steps * 1e3
@@ -460,7 +518,14 @@ def main():
                 "pipeline_frac": round(value / world / HBM_PEAK_GBS, 4),
                 # every kernel of a batch (PMC FETCH + WRITE), per input byte: 1.0 would be one pass
                 "path_bytes_per_input_byte": path_bytes,
-                "stage_ms_per_step": {k: round(v, 3) for k, v in per.items()}}
+                # the bound the contract prices against is HBM; the limit this kernel meets is integer
+                # VALU issue (valu_issue.frac below) and the pipeline's is the socket power cap (power)
+                "limiter": "integer VALU issue (BLAKE3 compressions; see valu_issue), at the socket power cap",
+                "marked_stage_ms_per_step": ({k: round(v, 3) for k, v in per.items()} if args.all_stage_marks else
+                                             {dom: round(per[dom], 3)}),
+                "marked_stage_note": ("every stage marked (--all-stage-marks)" if args.all_stage_marks else
+                                      "only the leaf pass is marked in the timed region (each mark costs ~5 us); "
+                                      "the full stage split is isolated.stage_ms_per_step")}
     valu = None
     if kernel == leaf_kernel and not args.no_calibrate:
         # the limit this kernel actually meets: integer VALU issue, measured now on this chip
@@ -480,10 +545,19 @@ def main():
         # the limit the whole pipeline meets: the socket power cap; energy per byte
         # of this GPU's share of the work = its power / its throughput
         power["pj_per_byte"] = round(power["socket_w_median"] / (value / world * 1e9) * 1e12, 1)
+        power["window"] = "the timed steps (%.2f s; amdsmi's socket power lags a short window)" % el
         roofline["power"] = power
     elif sampler is not None:
         roofline["power"] = None
         roofline["power_missing"] = power_missing
+    if holds is not None:
+        sus = holds["sustained"]
+        if "socket_w_median" in sus:
+            sus["pj_per_byte"] = round(sus["socket_w_median"] / (sus["gbs"] * 1e9) * 1e12, 1)
+        roofline.setdefault("power", None)
+        if roofline["power"] is None:
+            roofline["power"] = {}
+        roofline["power"]["sustained"] = sus
     if iso is not None:
         # live durations above include the overlap with the other batch in flight
         a_iso = algo / (iso["b3_leaf" if kernel == leaf_kernel else "scan"] * 1e-3) / 1e9
@@ -492,6 +566,8 @@ def main():
         roofline["isolated"] = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
                                 "valu_issue_frac": (round(a_iso / valu["ceiling"], 4) if valu else None),
                                 "stage_ms_per_step": {k: round(v, 3) for k, v in iso.items()}}
+        if holds is not None:
+            roofline["isolated"]["passes"] = holds["passes"]
 
     trees = time_file_trees(ctx, res, file_len, args.steps) if args.trees else None
     seal = time_seal(ctx, data, res, file_off, args.steps) if args.seal else None
@@ -712,6 +788,7 @@ class PowerSampler:
     def __init__(self, dev):
         import threading
         self.samples, self.note = [], None
+        self.t0 = time.perf_counter()
         self._stop = threading.Event()
         self.h = None
         try:
@@ -758,10 +835,12 @@ class PowerSampler:
                 self.note = "amdsmi query failed: %s" % e
                 return
             if w is not None and not self._stop.is_set():
-                self.samples.append((w, clk))
+                self.samples.append((time.perf_counter() - self.t0, w, clk))
             self._stop.wait(self.PERIOD_S)
 
-    def stop(self):
+    def stop(self, skip_s=0.0):
+        """(summary, None) or (None, reason).  skip_s drops the samples of the first seconds (the
+        socket power reading lags: a window that starts at an idle GPU first samples the ramp)."""
         self._stop.set()
         if self.h is not None:
             self.t.join(timeout=10)
@@ -769,11 +848,12 @@ class PowerSampler:
             self.smi.amdsmi_shut_down()
         except Exception:
             pass
-        if len(self.samples) < self.MIN_SAMPLES:
-            return None, {"samples": len(self.samples), "note": self.note or
+        kept = [(w, c) for t, w, c in self.samples if t >= skip_s]
+        if len(kept) < self.MIN_SAMPLES:
+            return None, {"samples": len(kept), "note": self.note or
                           "fewer than %d samples in the timed window" % self.MIN_SAMPLES}
-        ps = sorted(p for p, _ in self.samples)
-        cs = [c for _, c in self.samples if c]
+        ps = sorted(p for p, _ in kept)
+        cs = [c for _, c in kept if c]
         return {"samples": len(ps), "period_s": self.PERIOD_S, "socket_w_median": ps[len(ps) // 2],
                 "socket_w_max": ps[-1], "gfx_mhz_mean": round(sum(cs) / len(cs)) if cs else None,
                 "source": "amdsmi (in-process): current_socket_power, GFX clock", "gpu_bdf": self.bdf}, None

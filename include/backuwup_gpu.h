@@ -368,6 +368,17 @@ int bw_comm_set_timeout(bw_comm* comm, uint32_t timeout_ms);
 /* BW_OK, or BW_ECOMM once the communicator was aborted (a peer failed or stalled). */
 int bw_comm_status(const bw_comm* comm);
 int bw_comm_init_host(int device, int rank, int world, bw_host_all_to_all fn, void* user, bw_comm** out);
+/* The N ranks of ONE process (the reference packs a backup in one process, backup/mod.rs:64):
+ * out[0..n) get ranks 0..n-1 on devices[r] (a device may repeat).  The ranks are driven from n
+ * threads, one per rank, each calling bw_exchange_dedup with its own context and out[r] in the
+ * same batch order (INTEGRATION.md "One process, every GPU").
+ *   bw_comm_init_all:   RCCL over xGMI (draws the id and initialises the n ranks concurrently;
+ *                       RCCL refuses two ranks on one device);
+ *   bw_comm_init_local: an in-process host transport (threads exchange through host memory; any
+ *                       devices, the same device for several ranks included).
+ * On failure every communicator created is destroyed and out[] is NULL. */
+int bw_comm_init_all(const int* devices, int n, uint32_t timeout_ms, bw_comm** out);
+int bw_comm_init_local(const int* devices, int n, bw_comm** out);
 void bw_comm_destroy(bw_comm* comm);
 const char* bw_comm_last_error(const bw_comm* comm);
 /* Obsolete since round 5 (accepted and ignored): every transfer of bw_exchange_dedup is sized

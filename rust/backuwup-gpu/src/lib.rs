@@ -233,6 +233,8 @@ pub mod ffi {
         pub fn bw_comm_status(comm: *const bw_comm) -> c_int;
         pub fn bw_comm_init_host(device: c_int, rank: c_int, world: c_int, fn_: bw_host_all_to_all, user: *mut c_void,
                                  out: *mut *mut bw_comm) -> c_int;
+        pub fn bw_comm_init_all(devices: *const c_int, n: c_int, timeout_ms: u32, out: *mut *mut bw_comm) -> c_int;
+        pub fn bw_comm_init_local(devices: *const c_int, n: c_int, out: *mut *mut bw_comm) -> c_int;
         pub fn bw_comm_destroy(comm: *mut bw_comm);
         pub fn bw_comm_last_error(comm: *const bw_comm) -> *const c_char;
         pub fn bw_comm_set_capacity(comm: *mut bw_comm, cap: u64) -> c_int;
@@ -602,6 +604,29 @@ impl Comm {
         Ok(Comm { raw, _host: Some(state) })
     }
 
+    /// The ranks of ONE process (`bw_comm_init_local`: an in-process host transport, any devices,
+    /// several ranks per device included): rank r on `devices[r]`.  Drive each from its own thread.
+    pub fn local(devices: &[i32]) -> Result<Vec<Comm>> {
+        let mut raw = vec![std::ptr::null_mut(); devices.len()];
+        let rc = unsafe { ffi::bw_comm_init_local(devices.as_ptr(), devices.len() as c_int, raw.as_mut_ptr()) };
+        if rc != ffi::BW_OK {
+            return Err(Error { rc, msg: "bw_comm_init_local".into() });
+        }
+        Ok(raw.into_iter().map(|raw| Comm { raw, _host: None }).collect())
+    }
+
+    /// The ranks of ONE process over RCCL (`bw_comm_init_all`), one distinct device per rank.
+    pub fn all(devices: &[i32], timeout_ms: u32) -> Result<Vec<Comm>> {
+        let mut raw = vec![std::ptr::null_mut(); devices.len()];
+        let rc = unsafe {
+            ffi::bw_comm_init_all(devices.as_ptr(), devices.len() as c_int, timeout_ms, raw.as_mut_ptr())
+        };
+        if rc != ffi::BW_OK {
+            return Err(Error { rc, msg: "bw_comm_init_all".into() });
+        }
+        Ok(raw.into_iter().map(|raw| Comm { raw, _host: None }).collect())
+    }
+
     /// Obsolete since round 5 (accepted and ignored): the exchange sizes its transfers itself.
     pub fn set_capacity(&mut self, cap: u64) -> Result<()> {
         let rc = unsafe { ffi::bw_comm_set_capacity(self.raw, cap) };
@@ -624,6 +649,93 @@ impl Comm {
 impl Drop for Comm {
     fn drop(&mut self) {
         unsafe { ffi::bw_comm_destroy(self.raw) }
+    }
+}
+
+/// One backup session over N ranks of THIS process (the reference packs a backup
+/// in one process, `client/src/backup/mod.rs:64`): rank r = a context on `devices[r]` whose private
+/// index is rank r's shard of the session's `BlobIndex` (owner = digest[0] >> (8 - log2 N)), and a
+/// communicator of `Comm::local` or `Comm::all`.  A batch's files are sharded rank-major (contiguous,
+/// balanced by bytes), so canonical order = rank order; each rank's thread chunks + hashes its
+/// share (`BW_F_NO_DEDUP`), exchanges its digests (`bw_exchange_dedup`) and waits for its verdicts.
+/// `backuwup_amd/session.py` is the same sequence (tested on the GPU at world 2 and 4).
+pub struct NodeSession {
+    ctxs: Vec<Context>,
+    comms: Vec<Comm>,
+    params: ffi::bw_params,
+}
+
+impl NodeSession {
+    /// `rccl`: RCCL over xGMI (one distinct device per rank); otherwise the in-process transport.
+    pub fn new(devices: &[i32], rccl: bool, index_hint: u64, mut params: ffi::bw_params) -> Result<NodeSession> {
+        assert!(devices.len().is_power_of_two(), "NodeSession: a power-of-two number of ranks");
+        let comms = if rccl { Comm::all(devices, ffi::BW_COMM_DEFAULT_TIMEOUT_MS)? } else { Comm::local(devices)? };
+        let mut ctxs = Vec::with_capacity(devices.len());
+        for &d in devices {
+            let c = Context::new(d)?;
+            c.check(unsafe { ffi::bw_index_reset(c.raw, index_hint) })?;
+            ctxs.push(c);
+        }
+        params.flags |= ffi::BW_F_NO_DEDUP;
+        Ok(NodeSession { ctxs, comms, params })
+    }
+
+    /// Every GPU of the node (`bw_device_count`), RCCL between them.
+    pub fn all_devices(index_hint: u64, params: ffi::bw_params) -> Result<NodeSession> {
+        let mut n: c_int = 0;
+        let rc = unsafe { ffi::bw_device_count(&mut n) };
+        if rc != ffi::BW_OK || n < 1 {
+            return Err(Error { rc, msg: "bw_device_count".into() });
+        }
+        let world = 1i32 << (31 - (n as u32).leading_zeros());  // the largest power of two <= n
+        NodeSession::new(&(0..world).collect::<Vec<_>>(), true, index_hint, params)
+    }
+
+    /// The batch (files `data[file_off[i] .. + file_len[i]]`) through every rank -> blobs in canonical
+    /// order, `file` = the index in this batch: `Context::submit_host` + `wait` with the gate spread
+    /// over the ranks.
+    pub fn process_files(&mut self, data: &[u8], file_off: &[u64], file_len: &[u64]) -> Result<Vec<Blob>> {
+        assert_eq!(file_off.len(), file_len.len());
+        let n = self.ctxs.len();
+        let total: f64 = file_len.iter().map(|&l| l as f64 + 1.0).sum();
+        let mut cuts = vec![0usize; n + 1];
+        let (mut acc, mut f) = (0.0f64, 0usize);
+        for r in 1..n {  // contiguous, balanced by bytes (+1 per file: empty files count too)
+            while f < file_len.len() && acc + file_len[f] as f64 + 1.0 <= total * r as f64 / n as f64 {
+                acc += file_len[f] as f64 + 1.0;
+                f += 1;
+            }
+            cuts[r] = f;
+        }
+        cuts[n] = file_len.len();
+        let params = self.params;
+        let results: Vec<Result<Vec<Blob>>> = std::thread::scope(|sc| {
+            let hs: Vec<_> = self.ctxs.iter_mut().zip(self.comms.iter_mut()).enumerate().map(|(r, (c, comm))| {
+                let (lo, hi) = (cuts[r], cuts[r + 1]);
+                sc.spawn(move || -> Result<Vec<Blob>> {
+                    let (a, b) = if hi > lo {
+                        (file_off[lo..hi].iter().copied().min().unwrap(),
+                         (lo..hi).map(|i| file_off[i] + file_len[i]).max().unwrap())
+                    } else {
+                        (0, 0)
+                    };
+                    let offs: Vec<u64> = file_off[lo..hi].iter().map(|&o| o - a).collect();
+                    let t = c.submit_host(&data[a as usize..b as usize], &offs, &file_len[lo..hi], &params)?;
+                    c.exchange_dedup(comm, t)?;
+                    let mut res = c.wait(t)?;
+                    for b in res.iter_mut() {
+                        b.file += lo as u64;
+                    }
+                    Ok(res)
+                })
+            }).collect();
+            hs.into_iter().map(|h| h.join().expect("a rank's thread panicked")).collect()
+        });
+        let mut out = Vec::new();
+        for r in results {
+            out.extend(r?);
+        }
+        Ok(out)
     }
 }
 

@@ -16,6 +16,7 @@ import os
 
 import numpy as np
 import pytest
+import torch
 
 from backuwup_amd import synth
 
@@ -52,6 +53,7 @@ def test_c2_full_16gib_whole_result(fresh_ctx):
     want = fixture("c2")
     n = want["bytes"]
     dev = synth.splitmix_torch(want["seed"], n, "cuda")
+    torch.cuda.synchronize()  # (generated on torch's stream; the context runs on its own)
     fresh_ctx.index_reset(want["blobs"] + 1024)
     fresh_ctx.submit_device(dev.data_ptr(), n, [0], [n])
     compare(fresh_ctx.results(), want)
@@ -61,6 +63,7 @@ def test_c2_full_16gib_whole_result(fresh_ctx):
 def test_c3_full_64gib_whole_result(fresh_ctx):
     want = fixture("c3")
     data, offs, lens = synth.vm_image_variants_torch(want["base_bytes"], want["files"], "cuda", seed=want["seed"])
+    torch.cuda.synchronize()
     assert int(np.sum(lens)) == want["bytes"]
     fresh_ctx.index_reset(want["blobs"] + 1024)
     fresh_ctx.submit_device(data.data_ptr(), data.numel(), offs, lens)
@@ -72,6 +75,7 @@ def test_c4_full_1m_files_whole_result(fresh_ctx):
     want = fixture("c4")
     u, offs, lens = synth.small_files_table(want["files"], seed=want["seed"])
     dev = synth.splitmix_torch(want["seed"], u, "cuda")
+    torch.cuda.synchronize()
     fresh_ctx.index_reset(want["blobs"] + 1024)
     fresh_ctx.submit_device(dev.data_ptr(), u, offs, lens)
     got = fresh_ctx.results()

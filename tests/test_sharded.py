@@ -106,3 +106,70 @@ def test_exchange_matches_single_index(world):
                 want.append(int(k in seen))
                 seen.add(k)
             assert got[r][batch] == want, (r, batch)
+
+
+# ------------------------------------------------------------------ ranks as threads of one process
+# backuwup_amd/session.py (NodeSession) drives N ranks from N threads of ONE process.
+# The same sequence on the CPU: rank-major shards of one batch, the oracle as each rank's chunk +
+# hash stand-in, the exchange of sharded.py over an in-process all-to-all between the threads.
+
+class ThreadAllToAll:
+    """all_to_all_single between the threads of one process (the role of bw_comm_init_local)."""
+
+    def __init__(self, n):
+        import threading
+        self.n, self.bar, self.slots = n, threading.Barrier(n, timeout=60), [None] * n
+
+    def __call__(self, out, inp, rank):
+        self.slots[rank] = inp
+        self.bar.wait()
+        k = inp.numel() // self.n
+        for p in range(self.n):
+            out[p * k:(p + 1) * k] = self.slots[p][rank * k:(rank + 1) * k]
+        self.bar.wait()
+
+
+def test_shard_rank_major_contiguous_and_balanced():
+    from backuwup_amd.session import shard_rank_major
+    for n in (1, 2, 4, 8):
+        for fl in ([], [5], [0, 0, 0], [1 << 20] * 10, list(np.random.default_rng(n).integers(0, 1 << 16, 333))):
+            r = shard_rank_major(fl, n)
+            assert len(r) == n and r[0][0] == 0 and r[-1][1] == len(fl)
+            assert all(r[k][1] == r[k + 1][0] and r[k][0] <= r[k][1] for k in range(n - 1))
+    r = shard_rank_major([1 << 20] * 16, 4)
+    assert [b - a for a, b in r] == [4, 4, 4, 4]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_node_session_threads_match_one_index(world, oracle):
+    import threading
+    from backuwup_amd.session import shard_rank_major
+    from backuwup_amd.synth import small_files
+    data, offs, lens = small_files(900, seed=58)
+    batches = [(0, 300), (300, 302), (0, 300), (200, 900)]  # a batch of 2 files: ranks without files
+    a2a = ThreadAllToAll(world)
+    shards = [CpuShardOps() for _ in range(world)]
+    got = [[None] * world for _ in batches]
+
+    def rank(r):
+        for b, (blo, bhi) in enumerate(batches):
+            lo, hi = shard_rank_major(lens[blo:bhi], world)[r]
+            lo, hi = blo + lo, blo + hi
+            res = oracle.process_files(data, offs[lo:hi], lens[lo:hi]) if hi > lo else None
+            d = res["digest"] if res is not None else np.zeros((0, 32), np.uint8)
+            n = len(d)
+            is_dup = torch.zeros(max(n, 1), dtype=torch.uint8)
+            cap = 900  # the session's largest batch bound
+            exchange_dedup(shards[r], (n, torch.from_numpy(d.reshape(-1).copy()), is_dup, n), world, cap,
+                           group=r, all_to_all=a2a)
+            got[b][r] = is_dup.numpy()[:n].tolist()
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    ix = oracle.Index()
+    for b, (blo, bhi) in enumerate(batches):
+        want = oracle.process_files(data, offs[blo:bhi], lens[blo:bhi], index=ix)["is_dup"].tolist()
+        assert sum(got[b], []) == want, b

@@ -17,7 +17,13 @@
 //   hipcc -O2 -std=c++17 -I include tools/dropin_c1.cpp -L backuwup_amd -lbackuwup_amd \
 //     -Wl,-rpath,$PWD/backuwup_amd -lpthread -o build_ab/dropin_c1
 // Run: build_ab/dropin_c1 <corpus.bin> [threads=16] [reps=3] [staging chunk MiB=64] [contexts=0: one per thread]
+//        [--devices=0,1,...]
 //   corpus.bin = u64 n, n offsets, n lengths, then the bytes (tools/gpu_dropin.sh writes bench.py's C1)
+//   --devices: the Rust pool's policy over several GPUs (rust/backuwup-gpu Pool): the
+//   contexts alternate over the listed devices (`contexts` per device), thread t's home device is
+//   devices[t % n] (its small files go to that device's hash service through
+//   bw_blake3_hash_dropin_device; BW_EAGAIN -> the context).  A device may repeat ([0,0] on one GPU).
+//   BW_DROPIN_REGISTER_MIB=m in the environment page-locks files >= m MiB for their upload (A/B).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -59,12 +65,14 @@ static bool load(const char* path, Corpus& c) {
 
 static const uint64_t SMALL = 1 << 20;  // dir_packer.rs:246
 
-static int process(bw_ctx* ctx, const uint8_t* p, uint64_t n, bool kept, FileOut& o, std::string& err) {
+static int process(bw_ctx* ctx, int home, const uint8_t* p, uint64_t n, bool kept, FileOut& o, std::string& err) {
     o.chunks.clear();
     o.dig.clear();
     uint8_t d[32];
     if (n <= SMALL) {  // fs::read + add_file_blob
-        if (int rc = bw_blake3_hash(ctx, p, n, d)) return err = bw_last_error(ctx), rc;
+        int rc = home >= 0 ? bw_blake3_hash_dropin_device(home, p, n, d) : BW_EAGAIN;
+        if (rc == BW_EAGAIN) rc = bw_blake3_hash(ctx, p, n, d);
+        if (rc) return err = bw_last_error(ctx), rc;
         o.chunks.push_back({0, 0, n});
         o.dig.insert(o.dig.end(), d, d + 32);
         return 0;
@@ -87,6 +95,22 @@ static int process(bw_ctx* ctx, const uint8_t* p, uint64_t n, bool kept, FileOut
 }
 
 int main(int argc, char** argv) {
+    std::vector<int> devs;  // --devices=LIST (anywhere on the line)
+    {
+        int k = 1;
+        for (int i = 1; i < argc; i++) {
+            if (!strncmp(argv[i], "--devices=", 10)) {
+                for (const char* q = argv[i] + 10; *q;) {
+                    devs.push_back(atoi(q));
+                    while (*q && *q != ',') q++;
+                    if (*q) q++;
+                }
+            } else {
+                argv[k++] = argv[i];
+            }
+        }
+        argc = k;
+    }
     if (argc < 2) {
         fprintf(stderr, "usage: %s corpus.bin [threads] [reps]\n", argv[0]);
         return 2;
@@ -98,22 +122,27 @@ int main(int argc, char** argv) {
     }
     const int T = argc > 2 ? atoi(argv[2]) : 16, reps = argc > 3 ? atoi(argv[3]) : 3;
     const uint64_t stage_mib = argc > 4 ? strtoull(argv[4], nullptr, 10) : 0;  // BW_OPT_STAGE_CHUNK (0: default)
-    const int P = argc > 5 && atoi(argv[5]) > 0 ? atoi(argv[5]) : T;             // contexts (0: one per thread)
+    const int P0 = argc > 5 && atoi(argv[5]) > 0 ? atoi(argv[5]) : T;             // contexts (0: one per thread)
+    const bool pool_devs = !devs.empty();
+    if (devs.empty()) devs.push_back(0);
+    const int ND = (int)devs.size(), P = pool_devs ? P0 * ND : P0;  // --devices: P0 contexts per listed device
     const uint64_t nf = c.off.size();
     uint64_t bytes = 0, big = 0;
     for (uint64_t i = 0; i < nf; i++) {
         bytes += c.len[i];
         big += c.len[i] > SMALL;
     }
-    printf("corpus: %llu files (%llu > 1 MiB), %.3f GB; %d threads, %d contexts\n", (unsigned long long)nf,
+    printf("corpus: %llu files (%llu > 1 MiB), %.3f GB; %d threads, %d contexts; devices", (unsigned long long)nf,
            (unsigned long long)big, bytes / 1e9, T, P);
+    for (int d : devs) printf(" %d", d);
+    printf("%s\n", pool_devs ? " (home device per thread, small files to its hash service)" : "");
     size_t free0 = 0, tot = 0;
     hipSetDevice(0);
     hipMemGetInfo(&free0, &tot);
     std::vector<bw_ctx*> ctxs(P);
     std::vector<std::mutex> ctx_mu(P);
     for (int t = 0; t < P; t++) {
-        if (bw_create(0, &ctxs[t])) return 3;
+        if (bw_create(devs[t % ND], &ctxs[t])) return 3;
         if (stage_mib && bw_set_option(ctxs[t], BW_OPT_STAGE_CHUNK, stage_mib << 20)) return 3;
     }
     if (stage_mib) printf("pinned staging chunks of %llu MiB\n", (unsigned long long)stage_mib);
@@ -141,7 +170,8 @@ int main(int argc, char** argv) {
                                 break;
                             }
                         std::lock_guard<std::mutex> lk(ctx_mu[k]);
-                        if (int rc = process(ctxs[k], c.data.data() + c.off[i], c.len[i], kept, out[i], errs[t % 64]))
+                        if (int rc = process(ctxs[k], pool_devs ? devs[t % ND] : -1, c.data.data() + c.off[i], c.len[i],
+                                             kept, out[i], errs[t % 64]))
                             fail = rc;
                     }
                 });

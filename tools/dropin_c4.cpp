@@ -17,8 +17,11 @@
 // Build (CPU, after the library):
 //   hipcc -O2 -std=c++17 -I include tools/dropin_c4.cpp -L backuwup_amd -lbackuwup_amd \
 //     -Wl,-rpath,$PWD/backuwup_amd -lpthread -o build_ab/dropin_c4
-// Run: build_ab/dropin_c4 <table.bin> <threads list, e.g. 16,64,256> [contexts=16] [reps=2]
+// Run: build_ab/dropin_c4 <table.bin> <threads list, e.g. 16,64,256> [contexts=16] [reps=2] [--devices=0,1,...]
 //   table.bin = u64 n, u64 unique_bytes, u64 seed, n offsets, n lengths (tools/gpu_dropin.sh writes it)
+//   --devices: the Rust pool's policy: thread t hashes on devices[t % n] through
+//   bw_blake3_hash_dropin_device (no context; BW_EAGAIN -> a pool context), `contexts` per device.
+//   A device may repeat ([0,0] on one GPU).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -26,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -40,6 +44,22 @@ static uint64_t mix(uint64_t z) {
 }
 
 int main(int argc, char** argv) {
+    std::vector<int> devs;  // --devices=LIST (anywhere on the line)
+    {
+        int k = 1;
+        for (int i = 1; i < argc; i++) {
+            if (!strncmp(argv[i], "--devices=", 10)) {
+                for (const char* q = argv[i] + 10; *q;) {
+                    devs.push_back(atoi(q));
+                    while (*q && *q != ',') q++;
+                    if (*q) q++;
+                }
+            } else {
+                argv[k++] = argv[i];
+            }
+        }
+        argc = k;
+    }
     if (argc < 3) {
         fprintf(stderr, "usage: %s table.bin threads[,threads...] [contexts] [reps]\n", argv[0]);
         return 2;
@@ -56,7 +76,11 @@ int main(int argc, char** argv) {
         std::stringstream ss(argv[2]);
         for (std::string t; std::getline(ss, t, ',');) tlist.push_back(atoi(t.c_str()));
     }
-    const int P = argc > 3 ? atoi(argv[3]) : 16, reps = argc > 4 ? atoi(argv[4]) : 2;
+    const bool pool_devs = !devs.empty();
+    if (devs.empty()) devs.push_back(0);
+    const int ND = (int)devs.size();
+    const int P = (argc > 3 ? atoi(argv[3]) : 16) * (pool_devs ? ND : 1), reps = argc > 4 ? atoi(argv[4]) : 2;
+    std::vector<std::mutex> pool_mu(P);
     // the unique bytes: splitmix64 stream `seed` (backuwup_amd/synth.py splitmix_torch), 16 threads
     std::vector<uint8_t> data((ubytes + 7) / 8 * 8);
     {
@@ -75,8 +99,8 @@ int main(int argc, char** argv) {
     hipSetDevice(0);
     hipMemGetInfo(&free0, &total_mem);
     std::vector<bw_ctx*> pool(P);
-    for (auto& c : pool)
-        if (bw_create(0, &c)) return 3;
+    for (int j = 0; j < P; j++)
+        if (bw_create(devs[j % ND], &pool[j])) return 3;
     printf("corpus: %llu files, %.3f GB of file bytes (%.3f GB unique); contexts %d\n", (unsigned long long)nf,
            bytes / 1e9, ubytes / 1e9, P);
     // one file's Tree (filesystem/mod.rs:63-77) as process_file builds it for a small file
@@ -106,16 +130,32 @@ int main(int argc, char** argv) {
         for (int r = 0; r < reps + 1; r++) {  // the first pass warms the library's buffers
             std::atomic<uint64_t> next{0};
             std::atomic<int> fail{0};
-            bw_blake3_coalesce_stats(0, &b0, &m0);
+            b0 = m0 = 0;
+            for (int d = 0; d < 64; d++) {
+                uint64_t b = 0, m = 0;
+                bw_blake3_coalesce_stats(d, &b, &m);
+                b0 += b;
+                m0 += m;
+            }
             auto t0 = std::chrono::steady_clock::now();
             std::vector<std::thread> th;
             for (int t = 0; t < T; t++)
                 th.emplace_back([&, t] {
                     bw_ctx* ctx = pool[t % P];  // small messages: the context only names the device
+                    const int home = devs[t % ND];
+                    // the Rust blake3::hash: the home device's service, BW_EAGAIN -> a pool context
+                    auto hash = [&](const uint8_t* m, uint64_t n, uint8_t* out) {
+                        if (!pool_devs) return bw_blake3_hash_dropin(ctx, m, n, out);
+                        int rc = bw_blake3_hash_dropin_device(home, m, n, out);
+                        if (rc != BW_EAGAIN) return rc;
+                        std::lock_guard<std::mutex> lk(pool_mu[t % P]);
+                        const uint64_t o = 0;
+                        return bw_blake3_hash_many(pool[t % P], m, n, &o, &n, 1, out);
+                    };
                     uint8_t tb[512];
                     for (uint64_t i; (i = next++) < nf && !fail;) {
                         uint8_t* d = &fdig[32 * i];
-                        if (int rc = bw_blake3_hash_dropin(ctx, data.data() + off[i], len[i], d)) {
+                        if (int rc = hash(data.data() + off[i], len[i], d)) {
                             fail = rc;
                             break;
                         }
@@ -124,7 +164,7 @@ int main(int argc, char** argv) {
                             fail = rc;
                             break;
                         }
-                        if (int rc = bw_blake3_hash_dropin(ctx, tb, n, &tdig[32 * i])) {
+                        if (int rc = hash(tb, n, &tdig[32 * i])) {
                             fail = rc;
                             break;
                         }
@@ -132,7 +172,13 @@ int main(int argc, char** argv) {
                 });
             for (auto& x : th) x.join();
             const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            bw_blake3_coalesce_stats(0, &b1, &m1);
+            b1 = m1 = 0;
+            for (int d = 0; d < 64; d++) {
+                uint64_t b = 0, m = 0;
+                bw_blake3_coalesce_stats(d, &b, &m);
+                b1 += b;
+                m1 += m;
+            }
             size_t fr = 0, tot = 0;
             hipMemGetInfo(&fr, &tot);
             free_min = std::min(free_min, fr);

@@ -7,7 +7,9 @@
 #      16 / 64 / 256 threads over a pool of 16 contexts (small calls served by the library's hash
 #      service; BW_DROPIN_SERVICE=0 selects the round-5 coalescer).
 #   CPU on the same files: bench.py's cpu_baseline (C1; C4 with --cpu-trees).
-# Build first (CPU): see the two tools' headers.  DROPIN_PARTS picks parts (default "c1 c4 cpu").
+# Build first (CPU): see the two tools' headers.  DROPIN_PARTS picks parts (default "c1 c4 cpu"; "c1reg"
+# after "c1": the BW_DROPIN_REGISTER_MIB A/B and the [0,0] device pool; DROPIN_C4_DEVICES=0,0 runs C4
+# through the device pool's policy).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
@@ -37,6 +39,17 @@ PY
     run dropin_c1_t${t}_p${p} 600 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 0 $p || exit 1
   done
 fi
+if [[ " $PARTS " == *" c1reg "* ]]; then  # round 6: page-locking in place, alternating A/B
+  [ -f /tmp/c1.bin ] || { echo "c1reg needs the c1 part first" >> "$OUT/dropin_summary.txt"; exit 1; }
+  for rep in 1 2; do
+    for t in 16 64 256; do
+      run c1_t${t}_pool16_plain_$rep 300 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 0 16 || exit 1
+      run c1_t${t}_pool16_reg64_$rep 300 env BW_DROPIN_REGISTER_MIB=64 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 0 16 || exit 1
+      run c1_t${t}_pool16_reg4_$rep 300 env BW_DROPIN_REGISTER_MIB=4 ./build_ab/dropin_c1 /tmp/c1.bin $t 3 0 16 || exit 1
+    done
+  done
+  run c1_t16_devices00 300 ./build_ab/dropin_c1 /tmp/c1.bin 16 3 0 8 --devices=0,0 || exit 1
+fi
 if [[ " $PARTS " == *" c4 "* ]]; then
   python3 - <<'PY' > "$OUT/corpus_c4.log" 2>&1 || exit 1
 import numpy as np, sys
@@ -49,7 +62,8 @@ with open("/tmp/c4_table.bin", "wb") as f:
     np.asarray(l, np.uint64).tofile(f)
 print("files", len(o), "unique bytes", u, "file bytes", int(np.sum(l)))
 PY
-  run dropin_c4 900 stdbuf -oL ./build_ab/dropin_c4 /tmp/c4_table.bin ${DROPIN_C4_THREADS:-16,64,256} 16 ${DROPIN_C4_REPS:-1} || exit 1
+  run dropin_c4 900 stdbuf -oL ./build_ab/dropin_c4 /tmp/c4_table.bin ${DROPIN_C4_THREADS:-16,64,256} 16 ${DROPIN_C4_REPS:-1} \
+    ${DROPIN_C4_DEVICES:+--devices=$DROPIN_C4_DEVICES} || exit 1
 fi
 if [[ " $PARTS " == *" cpu "* ]]; then
   run bench_c1_cpu 600 python3 bench.py --workload c1 --steps 300 || exit 1
