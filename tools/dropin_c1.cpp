@@ -41,6 +41,7 @@
 struct Corpus {
     std::vector<uint64_t> off, len;
     std::vector<uint8_t> data;
+    std::vector<uint8_t*> file;  // each file in page-aligned memory of its own, as its own mmap would be
 };
 
 struct FileOut {
@@ -60,7 +61,19 @@ static bool load(const char* path, Corpus& c) {
     c.data.resize(total);
     const bool ok = fread(c.data.data(), 1, total, f) == total;
     fclose(f);
-    return ok;
+    if (!ok) return false;
+    // one page-aligned buffer per file (the reference maps each file on its own, dir_packer.rs:252):
+    // no page is shared between two files, so page-locking one file in place (BW_DROPIN_REGISTER_MIB)
+    // never touches another's pages
+    c.file.resize(n);
+    for (uint64_t i = 0; i < n; i++) {
+        void* p = nullptr;
+        if (posix_memalign(&p, 4096, std::max<uint64_t>(c.len[i], 1))) return false;
+        memcpy(p, c.data.data() + c.off[i], c.len[i]);
+        c.file[i] = (uint8_t*)p;
+    }
+    std::vector<uint8_t>().swap(c.data);
+    return true;
 }
 
 static const uint64_t SMALL = 1 << 20;  // dir_packer.rs:246
@@ -170,7 +183,7 @@ int main(int argc, char** argv) {
                                 break;
                             }
                         std::lock_guard<std::mutex> lk(ctx_mu[k]);
-                        if (int rc = process(ctxs[k], pool_devs ? devs[t % ND] : -1, c.data.data() + c.off[i], c.len[i],
+                        if (int rc = process(ctxs[k], pool_devs ? devs[t % ND] : -1, c.file[i], c.len[i],
                                              kept, out[i], errs[t % 64]))
                             fail = rc;
                     }
