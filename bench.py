@@ -1195,22 +1195,26 @@ def pmc_traffic(args, kernel):
 
 def whole_result_fixture(args, rank):
     """The committed oracle fixture of this rank's whole first batch, if one exists for exactly this
-    workload (tests/golden/c{2,3,4}_full.json: bench.py's rank-0 corpora at their default sizes)."""
-    name = {"c2": "c2", "c3": "c3", "c4": "c4"}.get(args.workload)
-    path = os.path.join(ROOT, "tests", "golden", "%s_full.json" % name) if name else None
-    if rank != 0 or not path or not os.path.exists(path):
+    workload (tests/golden/c{1..5}_full.json: bench.py's rank-0 corpora at their default sizes; rank 0's
+    verdicts at N > 1 are the same: files are sharded rank-major, so rank 0's come first)."""
+    name = args.workload
+    path = os.path.join(ROOT, "tests", "golden", "%s_full.json" % name)
+    if rank != 0 or not os.path.exists(path):
         return None, path
     fx = json.load(open(path))
-    same = {"c2": args.gib * (1 << 30) == fx.get("bytes"),
+    same = {"c1": args.gib * (1 << 30) == fx.get("total_bytes"),
+            "c2": args.gib * (1 << 30) == fx.get("bytes"),
             "c3": args.gib * (1 << 30) == fx.get("base_bytes"),
-            "c4": args.files == fx.get("files")}[name]
+            "c4": args.files == fx.get("files"),
+            "c5": args.gib * (1 << 30) == fx.get("base_bytes")}.get(name, False)
     return (fx if same else None), path
 
 
 def parity_spot_check(args, ctx, data, file_off, file_len, rank, first=None):
     """Bit-exactness of the session's first batch (fresh index).  WHOLE result: where the oracle's
     fixture of this exact corpus is committed (C2 16 GiB, C3 4 GiB x 16, C4 1 M files; rank 0), the
-    sha256 over every blob's (file, offset, length, gear_hash, digest, is_dup) must equal it.  Plus a
+    sha256 over every blob's (file, offset, length, gear_hash, digest, is_dup) must equal it (C1 and C5
+    too).  Plus a
     live oracle run here: the first ~64 MiB of blobs (C2) or a sample of files (other workloads)."""
     from backuwup_amd import synth
     out = {}

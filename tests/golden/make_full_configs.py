@@ -17,7 +17,10 @@ the same way and compare.
   c4  1,000,000 small files of 4-64 KiB with 30 % whole-file copies (seed 3; copies alias their
       source's bytes, synth.small_files_table), one blob per file (dir_packer.rs:246), one index
 
-Usage: python tests/golden/make_full_configs.py [c2] [c3] [c4]   (all three by default; ~10 min)
+  c1  bench.py --workload c1 (rank 0): the 1 GiB directory tree (log-uniform sizes, 30 % copies)
+  c5  bench.py --workload c5 (rank 0): C3's family, files 0-7 (32 GiB), as rank 0 holds them
+
+Usage: python tests/golden/make_full_configs.py [c1] [c2] [c3] [c4] [c5]   (all by default; ~10 min)
 """
 import json
 import os
@@ -123,7 +126,21 @@ def c4(seed=3, n_files=1_000_000, window=1 << 30):
     return synth.result_digest(blobs)
 
 
+def c1(seed=0x6261636B, total=1 << 30):
+    data, offs, lens = synth.tree_corpus(total, seed=seed)
+    return synth.result_digest(oracle.process_files(data, offs, lens, threads=os.cpu_count() or 8))
+
+
+def c5(seed=1, base_bytes=4 << 30):
+    # rank 0 of bench.py --workload c5: family 0 (= C3's corpus, seed 1), its files 0-7, one index
+    return c3(seed=seed, base_bytes=base_bytes, n_images=8)
+
+
 CONFIGS = {
+    "c1": (c1, {"workload": "bench.py --workload c1 rank 0: tree_corpus(1 GiB, seed 0x6261636B), 30 % whole-file "
+                            "copies", "seed": 0x6261636B, "total_bytes": 1 << 30}),
+    "c5": (c5, {"workload": "bench.py --workload c5 rank 0: VM-image family 0 (vm_image_variants(4 GiB, 16, seed=1)), "
+                            "its files 0-7, from pinned host memory", "seed": 1, "base_bytes": 4 << 30, "files": 8}),
     "c2": (c2, {"workload": "bench.py --workload c2 rank 0: splitmix64 seed 42, 16 GiB, one file",
                 "seed": 42, "bytes": 16 << 30, "files": 1}),
     "c3": (c3, {"workload": "bench.py --workload c3 rank 0: vm_image_variants(4 GiB, 16, seed=1), 32 indels "
@@ -135,7 +152,7 @@ CONFIGS = {
 
 
 def main():
-    want = sys.argv[1:] or list(CONFIGS)
+    want = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5"]
     oracle.set_blake3_simd(True)
     for name in want:
         fn, meta = CONFIGS[name]

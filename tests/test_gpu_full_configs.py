@@ -10,6 +10,9 @@ count and bytes, and sha256 over the packed records (backuwup_amd/synth.py CANON
   C2  16 GiB splitmix64 stream (seed 42), one file: 13.6 k chunks, none duplicate
   C3  4 GiB base + 15 byte-shifted variants (seed 1) = 64 GiB, 16 files, one index
   C4  1,000,000 files of 4-64 KiB with 30 % copies (seed 3), one blob per file
+  C1  the 1 GiB directory tree (seed 0x6261636B), 122 files, 30 % whole-file copies
+  C5  rank 0's share of C5: VM-image family 0, files 0-7 (32 GiB), from pinned host memory
+      (bw_submit_host: the H2D copy overlapped with the processing)
 """
 import json
 import os
@@ -82,3 +85,26 @@ def test_c4_full_1m_files_whole_result(fresh_ctx):
     assert len(got) == want["files"]  # dir_packer.rs:246: one blob per file <= 1 MiB
     compare(got, want)
     del dev
+
+
+def test_c1_full_1gib_whole_result(fresh_ctx):
+    want = fixture("c1")
+    data, offs, lens = synth.tree_corpus(want["total_bytes"], seed=want["seed"])
+    fresh_ctx.index_reset(want["blobs"] + 1024)
+    got = fresh_ctx.process_files(data, offs, lens)
+    compare(got, want)
+
+
+def test_c5_rank0_32gib_from_pinned_host_whole_result(fresh_ctx):
+    want = fixture("c5")
+    full, offs, lens = synth.vm_image_variants_torch(want["base_bytes"], 16, "cuda", seed=want["seed"])
+    hi = int(offs[7] + lens[7])
+    host = torch.empty(hi, dtype=torch.uint8, pin_memory=True)
+    host.copy_(full[:hi])
+    torch.cuda.synchronize()
+    del full
+    torch.cuda.empty_cache()
+    fresh_ctx.index_reset(want["blobs"] + 1024)
+    t = fresh_ctx.submit_host(host.data_ptr(), offs[:8], lens[:8], data_len=hi)
+    compare(fresh_ctx.wait(t), want)
+    del host
