@@ -45,7 +45,7 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
-        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline) || exit 1
+        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-holds) || exit 1
       T=$(find "$OUT/prof" -name "*kernel_trace.csv" | head -1)
       [ -n "$T" ] && python3 tools/trace_split.py "$T" k_b3_lines 2 320 17179869184 > "$OUT/trace_split.json" 2>&1 ;;
     pmc) step pmc 900 bash tools/gpu_pmc.sh ;;
