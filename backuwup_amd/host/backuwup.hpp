@@ -14,14 +14,21 @@
 //   Manager::write_packfiles / serialize_packfile      packfile/pack.rs:115-227
 //   compress_encrypt_blob (zstd level 3) + write_packfiles   packfile/pack.rs:58-80
 //   BlobIndex::flush / load (index files)              packfile/blob_index.rs:151-240
+//   Pool (the drop-ins over every GPU of the node)     client/src/main.rs:43, dir_packer.rs:166
+//   NodeSession (N ranks in one process)               client/src/backup/mod.rs:64, blob_index.rs:130-148
 #pragma once
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdint>
+#include <exception>
+#include <memory>
+#include <mutex>
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/backuwup_gpu.h"
@@ -374,5 +381,160 @@ inline std::vector<IndexEntry> index_load(Context& ctx, const std::array<uint8_t
     std::sort(items.begin(), items.end(), [](const IndexEntry& a, const IndexEntry& b) { return a.first < b.first; });
     return items;
 }
+
+// ---------------------------------------------------------------- every GPU of the node
+// The drop-ins' context pool (the Rust crate's Pool, INTEGRATION.md "Every GPU of the node"): the
+// reference's tasks call FastCDC::new / blake3::hash with no context, one task per file on one
+// worker thread per core (client/src/main.rs:43, dir_packer.rs:166).  `per_device` contexts per
+// listed device (a device may repeat), context j on devices[j % n]; the k-th calling thread gets home
+// slot k and home device devices[k % n]; with_context takes the first free context from the home
+// slot on; hash() sends a small message to the home device's hash service with no context held
+// (bw_blake3_hash_dropin_device), and BW_EAGAIN (a message over 64 KiB, a service that could not take
+// it in time) through a pooled context's launch path.
+class Pool {
+public:
+    explicit Pool(std::vector<int> devices = {}, int per_device = 16) : devices_(std::move(devices)) {
+        if (devices_.empty()) {
+            int n = 0;
+            check(bw_device_count(&n));
+            if (n <= 0) throw Error(BW_EINVAL, "no GPU for the drop-in pool");
+            for (int d = 0; d < n; d++) devices_.push_back(d);
+        }
+        const size_t total = (size_t)std::max(per_device, 1) * devices_.size();
+        for (size_t j = 0; j < total; j++) ctx_.emplace_back(new Context(devices_[j % devices_.size()]));
+        mu_ = std::vector<std::mutex>(total);
+    }
+    const std::vector<int>& devices() const { return devices_; }
+    size_t home_slot() const {
+        thread_local size_t slot = next_slot().fetch_add(1);
+        return slot;
+    }
+    int home_device() const { return devices_[home_slot() % devices_.size()]; }
+    template <class F>
+    auto with_context(F&& f) -> decltype(f(std::declval<Context&>())) {
+        const size_t n = ctx_.size(), start = home_slot() % n;
+        for (size_t k = 0; k < n; k++) {
+            const size_t j = (start + k) % n;
+            std::unique_lock<std::mutex> lk(mu_[j], std::try_to_lock);
+            if (lk.owns_lock()) return f(*ctx_[j]);
+        }
+        std::lock_guard<std::mutex> lk(mu_[start]);
+        return f(*ctx_[start]);
+    }
+    // blake3::hash(data) for read-only memory (kept chunk digests answer first)
+    BlobHash hash(const uint8_t* data, size_t len) {
+        BlobHash h{};
+        const int rc = bw_blake3_hash_dropin_device(home_device(), data, len, h.data());
+        if (rc == BW_OK) return h;
+        if (rc != BW_EAGAIN) check(rc);
+        return with_context([&](Context& c) {
+            const uint64_t off = 0, n = len;
+            static const uint8_t empty[16] = {0};
+            check(bw_blake3_hash_many(c.get(), len ? data : empty, len, &off, &n, 1, h.data()), c.get());
+            return h;
+        });
+    }
+
+private:
+    static std::atomic<size_t>& next_slot() {
+        static std::atomic<size_t> n{0};
+        return n;
+    }
+    std::vector<int> devices_;
+    std::vector<std::unique_ptr<Context>> ctx_;
+    std::vector<std::mutex> mu_;
+};
+
+// ---------------------------------------------------------------- N ranks in one process
+// One backup session over N ranks of THIS process (the reference packs in one process,
+// client/src/backup/mod.rs:64): rank r = a context on devices[r] whose index is rank r's shard of
+// the session's BlobIndex (owner = digest[0] >> (8 - log2 N)) and a communicator from
+// bw_comm_init_all (RCCL, one device per rank) or bw_comm_init_local (in-process transport).
+// process_files shards the batch's files rank-major (contiguous, balanced by bytes), and each rank's
+// thread submits its share with BW_F_NO_DEDUP, exchanges its digests and waits for its verdicts;
+// the blobs come back in canonical order with `file` = the index in the batch.
+class NodeSession {
+public:
+    NodeSession(const std::vector<int>& devices, bool rccl, uint64_t index_hint = 1u << 16,
+                const bw_params* params = nullptr)
+        : comms_(devices.size(), nullptr) {
+        const size_t n = devices.size();
+        if (n == 0 || (n & (n - 1))) throw Error(BW_EINVAL, "NodeSession: a power-of-two number of ranks");
+        check(rccl ? bw_comm_init_all(devices.data(), (int)n, BW_COMM_DEFAULT_TIMEOUT_MS, comms_.data())
+                   : bw_comm_init_local(devices.data(), (int)n, comms_.data()));
+        for (int d : devices) {
+            ctx_.emplace_back(new Context(d));
+            check(bw_index_reset(ctx_.back()->get(), index_hint), ctx_.back()->get());
+        }
+        if (params) p_ = *params;
+        else bw_params_default(&p_);
+        p_.flags |= BW_F_NO_DEDUP;
+    }
+    ~NodeSession() {
+        ctx_.clear();
+        for (bw_comm* c : comms_) bw_comm_destroy(c);
+    }
+    NodeSession(const NodeSession&) = delete;
+    NodeSession& operator=(const NodeSession&) = delete;
+
+    std::vector<bw_blob> process_files(const uint8_t* data, const std::vector<uint64_t>& file_off,
+                                       const std::vector<uint64_t>& file_len) {
+        const size_t n = ctx_.size(), nf = file_len.size();
+        double total = 0;
+        for (uint64_t l : file_len) total += (double)l + 1.0;  // (+1: empty files count too)
+        std::vector<size_t> cut(n + 1, 0);
+        double acc = 0;
+        size_t f = 0;
+        for (size_t r = 1; r < n; r++) {
+            while (f < nf && acc + (double)file_len[f] + 1.0 <= total * (double)r / (double)n) acc += (double)file_len[f++] + 1.0;
+            cut[r] = f;
+        }
+        cut[n] = nf;
+        std::vector<std::vector<bw_blob>> out(n);
+        std::vector<std::exception_ptr> err(n);
+        std::vector<std::thread> th;
+        for (size_t r = 0; r < n; r++)
+            th.emplace_back([&, r] {
+                try {
+                    const size_t lo = cut[r], hi = cut[r + 1];
+                    uint64_t a = 0, b = 0;
+                    if (hi > lo) {
+                        a = UINT64_MAX;
+                        for (size_t i = lo; i < hi; i++) {
+                            a = std::min(a, file_off[i]);
+                            b = std::max(b, file_off[i] + file_len[i]);
+                        }
+                    }
+                    std::vector<uint64_t> offs(hi - lo), lens(file_len.begin() + lo, file_len.begin() + hi);
+                    uint64_t cap = 1;
+                    for (size_t i = lo; i < hi; i++) {
+                        offs[i - lo] = file_off[i] - a;
+                        cap += file_len[i] / (p_.min_size ? p_.min_size : 1) + 2;
+                    }
+                    bw_ctx* c = ctx_[r]->get();
+                    uint64_t t = 0, got = 0;
+                    check(bw_submit_host(c, b > a ? data + a : nullptr, b - a, offs.data(), lens.data(), offs.size(), &p_, &t), c);
+                    check(bw_exchange_dedup(c, comms_[r], t), c);
+                    out[r].resize(cap);
+                    check(bw_wait(c, t, out[r].data(), cap, &got), c);
+                    out[r].resize(got);
+                    for (auto& x : out[r]) x.file += lo;
+                } catch (...) {
+                    err[r] = std::current_exception();
+                }
+            });
+        for (auto& t : th) t.join();
+        for (auto& e : err)
+            if (e) std::rethrow_exception(e);
+        std::vector<bw_blob> all;
+        for (auto& v : out) all.insert(all.end(), v.begin(), v.end());
+        return all;
+    }
+
+private:
+    std::vector<std::unique_ptr<Context>> ctx_;
+    std::vector<bw_comm*> comms_;
+    bw_params p_{};
+};
 
 }  // namespace backuwup

@@ -2,6 +2,7 @@
 // pack.rs:31-39).  Prints one line per result; tests/test_cpp_host.py compares with the oracle.
 #include <algorithm>
 #include <cstdio>
+#include <thread>
 #include <vector>
 
 #include "../../backuwup_amd/host/backuwup.hpp"
@@ -130,6 +131,56 @@ int main() {
         printf("packfile-zstd-empty %zu ", pk.second.size());
         for (auto x : pk.second) printf("%02x", x);
         printf("\n");
+    }
+    // ---- N ranks in one process (NodeSession over bw_comm_init_local: four ranks on device 0), a
+    // corpus of small files with CDC files between them and 30 % copies; three batches, the third
+    // repeating the first, one with fewer files than ranks (tests/test_cpp_host.py: one oracle index)
+    {
+        const size_t nfiles = 603;
+        std::vector<uint64_t> off(nfiles), len(nfiles);
+        std::vector<uint8_t> corpus;
+        for (size_t i = 0; i < nfiles; i++) {
+            const size_t src = (i < 600 && i % 10 == 3) ? i - 3 : i;  // a copy of the file three before
+            const size_t n = src < 600 ? 4096 + (src * 7919) % 61440 : (1u << 20) + 1 + src * 12345;
+            auto bytes = splitmix(1000 + src, n);
+            off[i] = corpus.size();
+            len[i] = n;
+            corpus.insert(corpus.end(), bytes.begin(), bytes.end());
+        }
+        NodeSession ns({0, 0, 0, 0}, false, 1u << 14);
+        const size_t batches[3][2] = {{0, 301}, {600, 603}, {0, 301}};
+        for (int bi = 0; bi < 3; bi++) {
+            const size_t lo = batches[bi][0], hi = batches[bi][1];
+            std::vector<uint64_t> bo(off.begin() + lo, off.begin() + hi), bl(len.begin() + lo, len.begin() + hi);
+            // the big files first in the second batch: ranks get 0 or 1 files each
+            auto blobs = ns.process_files(corpus.data(), bo, bl);
+            for (const auto& b : blobs) {
+                printf("ns %d %llu %llu %llu %llu ", bi, (unsigned long long)(b.file + lo), (unsigned long long)b.offset,
+                       (unsigned long long)b.length, (unsigned long long)b.gear_hash);
+                for (auto x : b.digest) printf("%02x", x);
+                printf(" %d\n", (int)b.is_dup);
+            }
+        }
+        // ---- the drop-in pool over the device list [0, 0]: 8 threads, small messages (home device's
+        // service) and a few over 64 KiB (a pooled context), every digest printed
+        Pool pool({0, 0}, 2);
+        const size_t nm = 400;
+        std::vector<BlobHash> got(nm);
+        std::vector<std::thread> th;
+        for (int t = 0; t < 8; t++)
+            th.emplace_back([&, t] {
+                for (size_t i = t; i < nm; i += 8) {
+                    const size_t n = (i % 50 == 7) ? 70000 + i : (i * 331) % 65537;
+                    got[i] = pool.hash(corpus.data() + i * 1000, n);
+                }
+            });
+        for (auto& x : th) x.join();
+        for (size_t i = 0; i < nm; i++) {
+            const size_t n = (i % 50 == 7) ? 70000 + i : (i * 331) % 65537;
+            printf("ph %zu %zu ", i * 1000, n);
+            for (auto x : got[i]) printf("%02x", x);
+            printf("\n");
+        }
     }
     return 0;
 }

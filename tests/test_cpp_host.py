@@ -84,3 +84,32 @@ def test_cpp_mirror_parity(tmp_path, oracle):
     ewant = po.write_packfiles(prk, [e], zids[:1])
     egot = [bytes.fromhex(l.split()[2]) for l in out if l.startswith("packfile-zstd-empty ")]
     assert egot == [b for _, b in ewant]
+
+    # NodeSession: four ranks of one process on device 0 (bw_comm_init_local), against one oracle
+    # index over the canonical order of the three batches
+    import numpy as np
+    sizes, srcs, parts = [], [], []
+    for i in range(603):
+        src = i - 3 if (i < 600 and i % 10 == 3) else i
+        sizes.append(4096 + (src * 7919) % 61440 if src < 600 else (1 << 20) + 1 + src * 12345)
+        srcs.append(src)
+    corpus = np.concatenate([splitmix_bytes(1000 + s, n) for s, n in zip(srcs, sizes)])
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    lens = np.asarray(sizes, np.uint64)
+    ns = [l.split() for l in out if l.startswith("ns ")]
+    ix = oracle.Index()
+    k = 0
+    for bi, (lo, hi) in enumerate([(0, 301), (600, 603), (0, 301)]):
+        want = oracle.process_files(corpus, offs[lo:hi], lens[lo:hi], index=ix, threads=8)
+        for w in want:
+            _, b, f, o, ln, gh, d, dup = ns[k]
+            assert (int(b), int(f), int(o), int(ln), int(gh), d, int(dup)) == \
+                (bi, lo + int(w["file"]), int(w["offset"]), int(w["length"]), int(w["gear_hash"]),
+                 bytes(w["digest"]).hex(), int(w["is_dup"])), (bi, k)
+            k += 1
+    assert k == len(ns) and sum(int(x[-1]) for x in ns) > 0
+    # the drop-in pool over [0, 0]: every digest equal to the oracle's
+    ph = [l.split() for l in out if l.startswith("ph ")]
+    assert len(ph) == 400
+    for _, o, n, d in ph:
+        assert d == oracle.blake3(corpus[int(o):int(o) + int(n)]).hex(), (o, n)
