@@ -33,7 +33,7 @@ def _corpus():
     return np.concatenate(parts), np.asarray(fo, np.uint64)[order], np.asarray(fl, np.uint64)[order]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_node_session_local_transport_matches_one_index(gpu, oracle, world):
     from backuwup_amd.session import NodeSession
     data, offs, lens = _corpus()
