@@ -470,9 +470,9 @@ public:
         else bw_params_default(&p_);
         p_.flags |= BW_F_NO_DEDUP;
     }
-    ~NodeSession() {
-        ctx_.clear();
+    ~NodeSession() {  // the communicators first: destroying one finishes its queued exchanges, which use the contexts
         for (bw_comm* c : comms_) bw_comm_destroy(c);
+        ctx_.clear();
     }
     NodeSession(const NodeSession&) = delete;
     NodeSession& operator=(const NodeSession&) = delete;

@@ -86,10 +86,12 @@ class NodeSession:
         return np.concatenate(out)
 
     def close(self):
-        for c in self.ctxs:
-            c.close()
+        # the communicators first: destroying one finishes any exchange still queued on it, which
+        # uses its context
         for m in self.comms:
             m.close()
+        for c in self.ctxs:
+            c.close()
 
     def __enter__(self):
         return self

@@ -660,8 +660,10 @@ impl Drop for Comm {
 /// share (`BW_F_NO_DEDUP`), exchanges its digests (`bw_exchange_dedup`) and waits for its verdicts.
 /// `backuwup_amd/session.py` is the same sequence (tested on the GPU at world 2 and 4).
 pub struct NodeSession {
-    ctxs: Vec<Context>,
+    // (dropped in this order: a communicator's destruction finishes its queued exchanges, which use
+    // the contexts)
     comms: Vec<Comm>,
+    ctxs: Vec<Context>,
     params: ffi::bw_params,
 }
 
@@ -677,7 +679,7 @@ impl NodeSession {
             ctxs.push(c);
         }
         params.flags |= ffi::BW_F_NO_DEDUP;
-        Ok(NodeSession { ctxs, comms, params })
+        Ok(NodeSession { comms, ctxs, params })
     }
 
     /// Every GPU of the node (`bw_device_count`), RCCL between them.
