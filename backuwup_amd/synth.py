@@ -202,6 +202,41 @@ def small_files_table(n_files, seed=3, lo=4096, hi=65536, dup_fraction=0.30):
     return int(sizes.sum()), uniq_off[src], sizes[src].astype(np.uint64)
 
 
+def edge_corpus(seed=11, text_bytes=384 << 20):
+    """A corpus of the content and size edges of process_file + FastCDC at full scale (the whole-result
+    fixture tests/golden/edge_full.json): files at the small-file threshold (dir_packer.rs:246: 1 MiB
+    and one byte either side), empty and tiny files, odd and even tails, content with no cut candidates
+    (zeros: every chunk `max`), one-byte and 4 KiB periodic patterns, two-symbol bytes (dense
+    candidates), compressible text and mixed segments, random data with zero runs, and whole-file
+    copies and a concatenation of two files (cross-file duplicate chunks).  Returns (data, file_off,
+    file_len), files 16-byte aligned."""
+    rng = np.random.default_rng(seed)
+    MiB = 1 << 20
+    files = []
+    for n in (0, 1, 63, 64, 65, 4095, 4096, MiB - 1, MiB, MiB + 1, MiB + 2, 3 * MiB, 3 * MiB + 1, 6 * MiB + 5):
+        files.append(splitmix_bytes(seed * 100 + len(files), n))
+    files.append(np.zeros(32 * MiB + 7, np.uint8))                                   # no candidates
+    files.append(np.full(24 * MiB + 3, 0xAB, np.uint8))                               # 1-byte period
+    files.append(np.tile(splitmix_bytes(seed + 1, 4096), 16 * 1024)[:64 * MiB + 1])   # 4 KiB period
+    files.append((splitmix_bytes(seed + 2, 48 * MiB) & 1).astype(np.uint8))           # two symbols
+    files.append(compressible_corpus(text_bytes, "text", seed=seed + 3))
+    files.append(compressible_corpus(text_bytes // 2, "mixed", seed=seed + 4))
+    r = splitmix_bytes(seed + 5, 256 * MiB + 13)
+    for at in rng.integers(0, r.size - MiB, 64):                                       # zero runs
+        r[int(at):int(at) + int(rng.integers(1, MiB))] = 0
+    files.append(r)
+    files.append(files[-1].copy())                                                     # whole-file copy
+    files.append(np.concatenate([files[20][:40 * MiB], files[18][:8 * MiB + 9]]))      # zero-run random + text
+    files.append(files[7].copy())                                                      # 1 MiB - 1 copy
+    lens = np.array([f.size for f in files], dtype=np.uint64)
+    offs = np.zeros(len(files), dtype=np.uint64)
+    offs[1:] = np.cumsum((lens[:-1] + 15) // 16 * 16)
+    data = np.zeros(int(offs[-1] + lens[-1]) + 16, dtype=np.uint8)
+    for o, f in zip(offs, files):
+        data[int(o):int(o) + f.size] = f
+    return data, offs, lens
+
+
 # ------------------------------------------------------------------ whole-result fingerprints
 # The canonical record of one blob, packed little-endian with no padding: the fields the reference's
 # path decides (dir_packer.rs:246-286 boundaries and digests, blob_index.rs:130-148 verdicts).  The

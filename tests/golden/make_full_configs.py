@@ -19,6 +19,8 @@ the same way and compare.
 
   c1  bench.py --workload c1 (rank 0): the 1 GiB directory tree (log-uniform sizes, 30 % copies)
   c5  bench.py --workload c5 (rank 0): C3's family, files 0-7 (32 GiB), as rank 0 holds them
+  edge  synth.edge_corpus: the content and size edges (no candidates, dense candidates, periodic,
+      compressible text, threshold sizes, cross-file duplicates), 1.4 GB
 
 Usage: python tests/golden/make_full_configs.py [c1] [c2] [c3] [c4] [c5]   (all by default; ~10 min)
 """
@@ -136,7 +138,15 @@ def c5(seed=1, base_bytes=4 << 30):
     return c3(seed=seed, base_bytes=base_bytes, n_images=8)
 
 
+def edge():
+    data, offs, lens = synth.edge_corpus()
+    return synth.result_digest(oracle.process_files(data, offs, lens, threads=os.cpu_count() or 8))
+
+
 CONFIGS = {
+    "edge": (edge, {"workload": "synth.edge_corpus(seed=11): threshold sizes, empty/tiny files, zeros, periodic, "
+                                "two-symbol, text and mixed compressible content, zero runs, copies",
+                    "seed": 11, "files": 24}),
     "c1": (c1, {"workload": "bench.py --workload c1 rank 0: tree_corpus(1 GiB, seed 0x6261636B), 30 % whole-file "
                             "copies", "seed": 0x6261636B, "total_bytes": 1 << 30}),
     "c5": (c5, {"workload": "bench.py --workload c5 rank 0: VM-image family 0 (vm_image_variants(4 GiB, 16, seed=1)), "
@@ -152,7 +162,7 @@ CONFIGS = {
 
 
 def main():
-    want = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5"]
+    want = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "edge"]
     oracle.set_blake3_simd(True)
     for name in want:
         fn, meta = CONFIGS[name]

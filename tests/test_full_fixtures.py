@@ -59,7 +59,9 @@ def test_result_digest_is_order_and_field_sensitive():
 
 
 def test_committed_fixtures_describe_the_bench_corpora():
-    fx = {k: json.load(open(os.path.join(HERE, "golden", "%s_full.json" % k))) for k in ("c1", "c2", "c3", "c4", "c5")}
+    fx = {k: json.load(open(os.path.join(HERE, "golden", "%s_full.json" % k))) for k in ("c1", "c2", "c3", "c4", "c5",
+                                                                                         "edge")}
+    assert fx["edge"]["files"] == 24 and fx["edge"]["dup_blobs"] > 0
     assert fx["c1"]["total_bytes"] == 1 << 30 and fx["c1"]["dup_bytes"] > 0.2 * fx["c1"]["bytes"]
     # C5's rank 0 holds C3's first 8 images: its blobs are a prefix of C3's
     assert fx["c5"]["files"] == 8 and fx["c5"]["blobs"] < fx["c3"]["blobs"] and fx["c5"]["base_bytes"] == 4 << 30

@@ -13,6 +13,8 @@ count and bytes, and sha256 over the packed records (backuwup_amd/synth.py CANON
   C1  the 1 GiB directory tree (seed 0x6261636B), 122 files, 30 % whole-file copies
   C5  rank 0's share of C5: VM-image family 0, files 0-7 (32 GiB), from pinned host memory
       (bw_submit_host: the H2D copy overlapped with the processing)
+  edge  synth.edge_corpus: threshold sizes, empty files, zeros (no candidates), periodic and
+      two-symbol data (dense candidates), compressible text, zero runs, copies; both scan tile sizes
 """
 import json
 import os
@@ -108,3 +110,18 @@ def test_c5_rank0_32gib_from_pinned_host_whole_result(fresh_ctx):
     t = fresh_ctx.submit_host(host.data_ptr(), offs[:8], lens[:8], data_len=hi)
     compare(fresh_ctx.wait(t), want)
     del host
+
+
+@pytest.fixture(scope="module")
+def edge_data():
+    return synth.edge_corpus()
+
+
+@pytest.mark.parametrize("small_bytes", [0, 1 << 40])  # full-size scan tiles, half-size tiles
+def test_edge_corpus_whole_result(fresh_ctx, edge_data, small_bytes):
+    from backuwup_amd._lib import BW_OPT_SCAN_SMALL_BYTES
+    want = fixture("edge")
+    data, offs, lens = edge_data
+    fresh_ctx.set_option(BW_OPT_SCAN_SMALL_BYTES, small_bytes)
+    fresh_ctx.index_reset(want["blobs"] + 1024)
+    compare(fresh_ctx.process_files(data, offs, lens), want)
