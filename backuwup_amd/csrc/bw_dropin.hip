@@ -566,10 +566,13 @@ int device_count() {
     return n;
 }
 
+bool g_svc_failed[64] = {};  // (under g_svc_mu) creation failed once: every later call goes to a context
+
 Service* service(int device) {
     if (device < 0 || device >= 64 || device >= device_count()) return nullptr;
     std::lock_guard<std::mutex> lk(g_svc_mu);
-    if (!g_svc[device]) {
+    if (!g_svc[device] && !g_svc_failed[device]) {
+        g_svc_failed[device] = true;  // (cleared below once the service is complete)
         auto* sv = new Service();  // lives as long as the process
         sv->device = device;
         DeviceGuard g(device);
@@ -625,6 +628,7 @@ Service* service(int device) {
         static std::once_flag once;
         std::call_once(once, [] { atexit(svc_atexit); });
         g_svc[device] = sv;
+        g_svc_failed[device] = false;
     }
     return g_svc[device];
 }
