@@ -177,6 +177,10 @@ def main():
     ap.add_argument("--no-calibrate", action="store_true", help="skip the in-run VALU-issue calibration")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU digest exchange (RCCL) even at world size 1 (rehearses the N > 1 path)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="the exchange's transport: RCCL over xGMI (the product), or 'host' = the caller's host "
+                         "all-to-all over a gloo process group, with ranks allowed to share a GPU (rank r on "
+                         "device r mod the visible count): rehearses the N > 1 bench path on a one-GPU box")
     ap.add_argument("--split-files", action="store_true",
                     help="C3: every rank holds the same corpus and each file is split across the ranks "
                          "(bw_chunk_stream_shard, SURVEY.md §8e single long stream) then exchanged; strong "
@@ -216,6 +220,9 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    host_tp = args.transport == "host"
+    if host_tp:  # (rehearsal: ranks may share a GPU)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     multi = world > 1 or args.exchange  # the sharded-index path (digest all-to-all over RCCL)
@@ -224,8 +231,11 @@ def main():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29511")
             import datetime  # a rank that never joins (or dies) ends the run instead of hanging it
-            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world,
-                                    timeout=datetime.timedelta(minutes=5))
+            if host_tp:
+                dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=5))
+            else:
+                dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world,
+                                        timeout=datetime.timedelta(minutes=5))
         if dist.get_world_size() != world:
             raise SystemExit("process group has %d ranks, WORLD_SIZE says %d" % (dist.get_world_size(), world))
 
@@ -306,10 +316,13 @@ def main():
         # the digest exchange through the C ABI (bw_comm_init + bw_exchange_dedup): RCCL over
         # xGMI, every transfer sized from the exchange's own counts, no host wait for the peers;
         # rank 0 draws the RCCL id and the process group hands it to the others
-        from backuwup_amd.comm import Comm, unique_id
-        uid = [unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = Comm.rccl(local, rank, world, uid[0])
+        from backuwup_amd.comm import Comm, gloo_all_to_all, unique_id
+        if host_tp:
+            comm = Comm.host(local, rank, world, gloo_all_to_all())
+        else:
+            uid = [unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = Comm.rccl(local, rank, world, uid[0])
 
     def drain():
         while inflight:
@@ -394,7 +407,7 @@ def main():
     el = time.perf_counter() - t0
     power, power_missing = sampler.stop() if sampler else (None, None)
     if multi:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if host_tp else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ctx.index_check()  # no sticky index error anywhere in the session
@@ -582,7 +595,9 @@ def main():
         line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-                "config": {"workload": desc + (" -- streamed from pinned host memory" if host is not None else ""),
+                "config": {"workload": desc + (" -- streamed from pinned host memory" if host is not None else "") +
+                           (" -- REHEARSAL: host transport, %d ranks on %d GPU(s)" % (world, torch.cuda.device_count())
+                            if host_tp and multi else ""),
                            "bytes_per_gpu": processed, "blobs_per_gpu": int(len(res)),
                            "files_per_gpu": len(file_len),
                            "parallelism": "dp%d (files sharded, index by digest prefix)" % world,
