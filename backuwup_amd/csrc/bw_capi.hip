@@ -344,6 +344,7 @@ int check_collision(bw_ctx* c, bool all) {
 // ------------------------------------------------------------------ C ABI: basics
 
 extern "C" void bw_params_default(bw_params* p) {
+    if (!p) return;
     p->min_size = BW_BLOB_MINIMUM_TARGET_SIZE;
     p->avg_size = BW_BLOB_DESIRED_TARGET_SIZE;
     p->max_size = BW_BLOB_MAX_UNCOMPRESSED_SIZE;
