@@ -92,12 +92,35 @@ public:
         chunks_.reserve(n);
         for (uint64_t i = 0; i < n; i++) chunks_.push_back({out[i].hash, out[i].offset, out[i].length});
     }
+    // The Rust drop-in's form (rust/backuwup-gpu FastCDC::new): chunks AND hashes the source in one
+    // submit on a context of `pool` (any type with with_context, i.e. backuwup::Pool) and keeps the
+    // digests until destruction, so Pool::hash of one of these chunk slices is answered without a
+    // second trip (bw_fastcdc_chunks_hashed); the source must stay unchanged meanwhile.
+    template <class P, class = decltype(std::declval<P&>().home_device())>
+    FastCDC(P& pool, const uint8_t* source, size_t len, uint32_t min_size, uint32_t avg_size, uint32_t max_size) {
+        const uint32_t s0 = 2 * (min_size / 2);
+        const uint32_t mc = s0 < max_size ? s0 : max_size;
+        std::vector<bw_chunk> out(len / (mc ? mc : 1) + 2);
+        uint64_t n = 0;
+        pool.with_context([&](Context& ctx) {
+            check(bw_fastcdc_chunks_hashed(ctx.get(), source, len, min_size, avg_size, max_size, out.data(), out.size(),
+                                           &n, &kept_),
+                  ctx.get());
+            return 0;
+        });
+        chunks_.reserve(n);
+        for (uint64_t i = 0; i < n; i++) chunks_.push_back({out[i].hash, out[i].offset, out[i].length});
+    }
+    ~FastCDC() { bw_fastcdc_release(kept_); }
+    FastCDC(const FastCDC&) = delete;
+    FastCDC& operator=(const FastCDC&) = delete;
     std::vector<Chunk>::const_iterator begin() const { return chunks_.begin(); }
     std::vector<Chunk>::const_iterator end() const { return chunks_.end(); }
     size_t size() const { return chunks_.size(); }
 
 private:
     std::vector<Chunk> chunks_;
+    uint64_t kept_ = 0;  // bw_fastcdc_release(0) is a no-op
 };
 
 }  // namespace v2020

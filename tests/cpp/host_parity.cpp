@@ -2,6 +2,7 @@
 // pack.rs:31-39).  Prints one line per result; tests/test_cpp_host.py compares with the oracle.
 #include <algorithm>
 #include <cstdio>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -181,6 +182,28 @@ int main() {
             for (auto x : got[i]) printf("%02x", x);
             printf("\n");
         }
+        // the reference's loop exactly as the Rust drop-ins run it (dir_packer.rs:254-266 -> :286):
+        // FastCDC::new on a pooled context (chunks and digests in one submit), then blake3::hash of
+        // every chunk slice answered from the kept digests; the three big files, one thread each
+        const uint64_t hits0 = bw_blake3_kept_hits();
+        std::vector<std::vector<std::string>> lines(3);
+        std::vector<std::thread> tf;
+        for (int t = 0; t < 3; t++)
+            tf.emplace_back([&, t] {
+                const size_t f = 600 + t;
+                fastcdc::v2020::FastCDC chunker(pool, corpus.data() + off[f], len[f], 262144, 1048576, 3145728);
+                for (const auto& c : chunker) {
+                    BlobHash h = pool.hash(corpus.data() + off[f] + c.offset, c.length);
+                    char buf[160];
+                    int k = snprintf(buf, sizeof buf, "pf %zu %llu %zu %zu ", f, (unsigned long long)c.hash, c.offset, c.length);
+                    for (auto x : h) k += snprintf(buf + k, sizeof buf - k, "%02x", x);
+                    lines[t].push_back(buf);
+                }
+            });
+        for (auto& x : tf) x.join();
+        for (auto& v : lines)
+            for (auto& l : v) printf("%s\n", l.c_str());
+        printf("pf-kept %llu\n", (unsigned long long)(bw_blake3_kept_hits() - hits0));
     }
     return 0;
 }

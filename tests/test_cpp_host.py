@@ -113,3 +113,13 @@ def test_cpp_mirror_parity(tmp_path, oracle):
     assert len(ph) == 400
     for _, o, n, d in ph:
         assert d == oracle.blake3(corpus[int(o):int(o) + int(n)]).hex(), (o, n)
+    # FastCDC on the pool (kept digests) + Pool::hash per chunk: the Rust drop-ins' loop
+    pf = [l.split() for l in out if l.startswith("pf ")]
+    nk = 0
+    for f in (600, 601, 602):
+        got = [(int(h), int(o), int(n), d) for _, ff, h, o, n, d in pf if int(ff) == f]
+        fb = corpus[int(offs[f]):int(offs[f] + lens[f])]
+        want = [(h, o, n, oracle.blake3(fb[o:o + n]).hex()) for h, o, n in oracle.fastcdc(fb, 262144, 1048576, 3145728)]
+        assert got == want, f
+        nk += len(want)
+    assert [l for l in out if l.startswith("pf-kept ")] == ["pf-kept %d" % nk]
