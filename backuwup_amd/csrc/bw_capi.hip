@@ -91,6 +91,12 @@ static int make_masks(uint32_t mn, uint32_t av, uint32_t mx, Masks* mk) {
     if (mn < BW_MINIMUM_MIN || mn > BW_MINIMUM_MAX) return BW_EINVAL;
     if (av < BW_AVERAGE_MIN || av > BW_AVERAGE_MAX) return BW_EINVAL;
     if (mx < BW_MAXIMUM_MIN || mx > BW_MAXIMUM_MAX) return BW_EINVAL;
+    // avg > max passes the crate's asserts, but then cut() keeps center = avg past remaining = max:
+    // its first loop reads beyond max (a cut there makes a chunk longer than max) and, where the
+    // source ends first, indexes out of bounds -- a panic, on most inputs (oracle/bw_oracle.c
+    // ORC_CUT_PANIC restates it).  backuwup never passes such sizes (dir_packer.rs:254-259); the
+    // ABI refuses them instead of returning chunks the crate would not.
+    if (av > mx) return BW_EINVAL;
     const uint32_t bits = (uint32_t)lround(log2((double)av));  // logarithm2(): round(log2(avg))
     mk->min = mn;
     mk->avg = av;

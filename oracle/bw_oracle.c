@@ -135,10 +135,15 @@ size_t orc_fastcdc_cut(const uint8_t* src, size_t len, uint32_t min_size, uint32
     const uint64_t mask_s_ls = mask_s << 1, mask_l_ls = mask_l << 1;
     size_t index = min_size / 2;
     uint64_t hash = 0;
+    /* With avg > max and a source longer than max, `center` stays avg: the crate's first loop runs
+     * past `remaining` (a cut there gives a chunk longer than max) and, when the source ends first,
+     * indexes out of bounds -- a panic in Rust.  ORC_CUT_PANIC reports that. */
     while (index < center / 2) {
         size_t a = index * 2;
+        if (a >= len) return ORC_CUT_PANIC;
         hash = (hash << 2) + GEAR_LS[src[a]];
         if ((hash & mask_s_ls) == 0) { *out_hash = hash; return a; }
+        if (a + 1 >= len) return ORC_CUT_PANIC;
         hash = hash + GEAR[src[a + 1]];
         if ((hash & mask_s) == 0) { *out_hash = hash; return a + 1; }
         index++;
@@ -165,6 +170,7 @@ int orc_fastcdc_chunks(const uint8_t* src, size_t len, uint32_t min, uint32_t av
     while (off < len) {
         uint64_t h;
         size_t c = orc_fastcdc_cut(src + off, len - off, min, avg, max, ms, ml, &h);
+        if (c == ORC_CUT_PANIC) return -3;  /* the crate panics (index out of bounds) */
         if (c == 0) break;
         if (n < cap) {
             out_hash[n] = h;

@@ -40,10 +40,13 @@ void orc_gear_table(uint64_t out[256]);
 /* FastCDC::with_level(.., Level1) parameter validation + mask selection.  0 ok, -1 = the crate
  * would panic on an assert. */
 int orc_fastcdc_masks(uint32_t min, uint32_t avg, uint32_t max, uint64_t* mask_s, uint64_t* mask_l);
-/* fastcdc::v2020::cut() on src[0..len): returns the cut length, writes the gear hash. */
+/* fastcdc::v2020::cut() on src[0..len): returns the cut length, writes the gear hash; or
+ * ORC_CUT_PANIC where the crate indexes past the source (only with avg > max). */
+#define ORC_CUT_PANIC ((size_t)-1)
 size_t orc_fastcdc_cut(const uint8_t* src, size_t len, uint32_t min, uint32_t avg, uint32_t max,
                        uint64_t mask_s, uint64_t mask_l, uint64_t* hash);
-/* FastCDC::new(src, min, avg, max).collect(): chunks as (hash, offset, length) triples. */
+/* FastCDC::new(src, min, avg, max).collect(): chunks as (hash, offset, length) triples.  -1: the
+ * crate's asserts fail; -2: cap too small; -3: the crate panics while iterating (avg > max). */
 int orc_fastcdc_chunks(const uint8_t* src, size_t len, uint32_t min, uint32_t avg, uint32_t max,
                        uint64_t* out_hash, uint64_t* out_off, uint64_t* out_len, size_t cap,
                        size_t* n_out);

@@ -95,6 +95,10 @@ def masks(min_size, avg_size, max_size):
     return s.value, l.value
 
 
+class CratePanic(ValueError):
+    """The crate would panic here (index out of bounds in cut(), only with avg > max)."""
+
+
 def fastcdc(data, min_size, avg_size, max_size):
     """FastCDC::new(data, min, avg, max).collect() -> list of (hash, offset, length)."""
     ptr, n, keep = _buf(data)
@@ -103,6 +107,8 @@ def fastcdc(data, min_size, avg_size, max_size):
     cnt = ctypes.c_size_t()
     rc = lib().orc_fastcdc_chunks(ptr, n, min_size, avg_size, max_size, _u64p(h), _u64p(o),
                                   _u64p(l), cap, ctypes.byref(cnt))
+    if rc == -3:
+        raise CratePanic("fastcdc 3.0.3 cut() indexes past the source (avg %d > max %d)" % (avg_size, max_size))
     if rc:
         raise ValueError("orc_fastcdc_chunks rc=%d" % rc)
     k = cnt.value

@@ -212,3 +212,15 @@ def test_blake3_prefix_collision_fixture(oracle):
     ix = oracle.Index()  # the reference's BlobIndex keeps both
     assert not ix.is_blob_duplicate(d1) and ix.insert(d1) == 0
     assert not ix.is_blob_duplicate(d2) and ix.insert(d2) == 0
+
+
+def test_avg_above_max_follows_the_crate(oracle):
+    """avg > max passes FastCDC::with_level's asserts, but cut() then keeps center = avg past
+    remaining = max: its first loop reads beyond max, so a chunk can be longer than max, and where the
+    source ends first it indexes out of bounds (a panic in the crate).  The oracle restates both; the
+    GPU ABI refuses such sizes with BW_EINVAL (tests/test_gpu_fuzz.py)."""
+    from backuwup_amd.synth import splitmix_bytes
+    c = oracle.fastcdc(splitmix_bytes(3, 6000), 64, 4096, 1024)
+    assert [l for _, _, l in c] == [1024, 3961, 360, 655]  # the second chunk is longer than max
+    with pytest.raises(oracle.CratePanic):
+        oracle.fastcdc(splitmix_bytes(0, 6000), 64, 4096, 1024)
