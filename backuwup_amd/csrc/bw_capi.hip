@@ -865,7 +865,9 @@ static int submit(bw_ctx* c, Slot& s, const uint8_t* d_data, uint64_t data_len, 
         }
     }, nf);
     Part tot;
-    tot.max_blob_len = mk.max;
+    // a CDC chunk is <= max, or <= min where cut() returns a remainder <= min whole before clipping
+    // to max (min > max is legal in the crate; round-6 fuzz: a 70,325 B chunk under max = 1,520)
+    tot.max_blob_len = std::max<uint64_t>(mk.max, mk.min);
     for (uint64_t k = 0; k < T; k++) {
         base[k] = tot;
         tot.nseg += part[k].nseg;

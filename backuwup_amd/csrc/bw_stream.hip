@@ -84,6 +84,9 @@ extern "C" int bw_chunk_stream_shard(bw_ctx* c, bw_comm* comm, const uint8_t* d_
     if (params->min_size < BW_MINIMUM_MIN || params->min_size > BW_MINIMUM_MAX || params->avg_size < BW_AVERAGE_MIN ||
         params->avg_size > BW_AVERAGE_MAX || params->max_size < BW_MAXIMUM_MIN || params->max_size > BW_MAXIMUM_MAX)
         return BW_EINVAL;
+    // the halos are max wide: with min > max a truncated window's last chunk (<= min, returned whole
+    // by cut()) is not the file's, and its true chain can enter before lo (the header's note)
+    if (params->min_size > params->max_size || params->avg_size > params->max_size) return BW_EINVAL;
     if (comm_failed(comm)) return BW_ECOMM;
     const int r = comm_rank(comm), W = comm_world(comm);
     if (comm_device(comm) != ctx_device(c)) return BW_EINVAL;

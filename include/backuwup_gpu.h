@@ -416,7 +416,9 @@ int bw_comm_progress(bw_comm* comm);
  * comm, ticket) sends only those to their owners.  d_window = file byte lo in device memory, any
  * alignment (the library may read up to 15 bytes before it, inside its 16-byte granule).  Every rank
  * calls it for the same file at the same point in its sequence of calls on the communicator; it
- * returns once the ranks settled (host-synchronous, deadline-bounded like every wait on peers). */
+ * returns once the ranks settled (host-synchronous, deadline-bounded like every wait on peers).
+ * min_size > max_size (legal in the crate, whose cut() then returns a remainder <= min whole, longer
+ * than max) is refused with BW_EINVAL: the windows rest on every chunk being <= max. */
 typedef struct bw_stream_shard {
     uint64_t ticket;      /* batch holding this rank's final chain                             */
     uint64_t first_blob;  /* the chunks this rank emits: blobs [first_blob, first_blob + n_blobs) */

@@ -99,3 +99,22 @@ def test_process_files_random_batches(ctx, oracle, case):
     want = oracle.process_files(data, offs, lens, mn, av, mx, small_threshold=thr, index=oracle.Index(b"".join(seeded)),
                                 threads=8)
     _blobs_equal(got, want)
+
+
+def test_min_above_max_hashes_whole_remainders(ctx, oracle):
+    """min > max (the crate allows it): cut() returns a remainder <= min whole, so chunks run up to min,
+    past max -- the leaf pass and the upper levels are sized for max(min, max) (fuzz case 23 above
+    found a 70,325 B chunk hashed as if it were <= max = 1,520)."""
+    p = (496561, 1520, 1520)
+    files = [splitmix_bytes(90 + k, n) for k, n in enumerate([70325, 1520, 1521, 496561, 496562, 3 << 20, 0])]
+    lens = np.array([f.size for f in files], np.uint64)
+    offs = np.zeros(len(files), np.uint64)
+    offs[1:] = np.cumsum((lens[:-1] + 15) // 16 * 16)
+    data = np.zeros(int(offs[-1] + lens[-1]) + 16, np.uint8)
+    for o, f in zip(offs, files):
+        data[int(o):int(o) + f.size] = f
+    ctx.index_reset()
+    got = ctx.process_files(data, offs, lens, make_params(*p, small_file_threshold=0))
+    want = oracle.process_files(data, offs, lens, *p, small_threshold=0)
+    assert int(want["length"].max()) == 496561 > p[2]
+    _blobs_equal(got, want)

@@ -222,6 +222,10 @@ def test_stream_shard_c_abi_rccl_world1(ctx, oracle):
     torch.cuda.synchronize()
     with Comm.rccl(0, 0, 1, unique_id()) as comm:
         ctx.index_reset(1 << 12)
+        from backuwup_amd._lib import BW_EINVAL, BwError
+        with pytest.raises(BwError) as e:  # min > max: refused (the windows rest on chunks <= max)
+            ctx.chunk_stream_shard(comm, win.data_ptr(), data.size, make_params(8192, 2048, 4096))
+        assert e.value.rc == BW_EINVAL
         sh = ctx.chunk_stream_shard(comm, win.data_ptr(), data.size, make_params())
         ctx.exchange_dedup(comm, sh["ticket"])
         res = ctx.wait(sh["ticket"])
