@@ -859,6 +859,8 @@ pub mod fastcdc {
                 assert!((MINIMUM_MIN..=MINIMUM_MAX).contains(&min_size));
                 assert!((AVERAGE_MIN..=AVERAGE_MAX).contains(&avg_size));
                 assert!((MAXIMUM_MIN..=MAXIMUM_MAX).contains(&max_size));
+                // the crate's cut() reads past max here and panics on most sources; the ABI refuses it
+                assert!(avg_size <= max_size, "FastCDC: avg_size > max_size");
                 let (cuts, kept) = super::super::with_default(|c| {
                     c.fastcdc_chunks_hashed(source, min_size, avg_size, max_size)
                 })
