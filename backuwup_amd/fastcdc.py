@@ -8,7 +8,8 @@ in one submit when it is constructed (bw_fastcdc_chunks_hashed) and iterates `Ch
 length)` like the crate's iterator.  While the object lives, `blake3.hash(view[offset:offset +
 length])` of one of its chunks (a zero-copy view of the same memory, as the reference slices its
 mmap) is answered from the kept digests instead of a second trip to the GPU.  Size parameters
-outside the crate's asserted ranges raise ValueError (the crate panics).
+outside the crate's asserted ranges raise ValueError (the crate panics), and so does avg > max
+(the crate's cut() then reads past max: a chunk longer than max, or an index panic).
 """
 from collections import namedtuple
 
@@ -36,6 +37,8 @@ class FastCDC:
                 and MAXIMUM_MIN <= max_size <= MAXIMUM_MAX):
             raise ChunkParameterError("fastcdc size parameters out of range: %d/%d/%d"
                                       % (min_size, avg_size, max_size))
+        if avg_size > max_size:  # the crate's cut() reads past max and panics on most sources
+            raise ChunkParameterError("fastcdc avg_size %d > max_size %d" % (avg_size, max_size))
         if ctx is None:  # the drop-in pool over the node's GPUs (backuwup_amd/pool.py)
             from .pool import default_pool
             run = default_pool().with_context

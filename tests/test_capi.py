@@ -99,6 +99,18 @@ def test_blake3_module_validates_before_any_device_call():
         blake3.hash(np.zeros(4, dtype=np.uint32))
 
 
+
+def test_fastcdc_mirror_validates_before_any_device_call():
+    """backuwup_amd.fastcdc.FastCDC (the fastcdc::v2020 mirror) refuses sizes outside the crate's
+    asserted ranges, and avg > max (the crate's cut() reads past max there), on the host."""
+    import pytest
+    from backuwup_amd.fastcdc import ChunkParameterError, FastCDC
+    for bad in [(63, 256, 1024), (64, 255, 1024), (64, 256, 1023), (1 << 20 | 1, 4096, 8192), (64, 4096, 1024)]:
+        with pytest.raises(ChunkParameterError):
+            FastCDC(b"x" * 5000, *bad)
+    assert issubclass(ChunkParameterError, ValueError)
+
+
 _NULL_PROBE = """
 import ctypes, sys
 sys.path.insert(0, %r)
