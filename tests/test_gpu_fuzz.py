@@ -70,26 +70,42 @@ def test_fastcdc_random_params_and_content(ctx, oracle, case):
     assert ctx.fastcdc_chunks(data, mn, av, mx) == oracle.fastcdc(data, mn, av, mx), (kind, n, mn, av, mx)
 
 
-@pytest.mark.parametrize("case", range(24))
-def test_process_files_random_batches(ctx, oracle, case):
-    rng = np.random.default_rng(5000 + case)
+def _valid_params(rng, case):
     mn, av, mx = _params(rng) if case % 3 else (262144, 1048576, 3145728)
     if av > mx:  # (refused: test_fastcdc_random_params_and_content)
         av = max(256, mx)
-    thr = int(rng.choice([0, 1, 4096, MiB, 8 * MiB]))  # the small-file threshold (dir_packer.rs:246 = 1 MiB)
-    nf = int(rng.integers(1, 400))
+    return mn, av, mx
+
+
+def _batch(rng, nf_max=400, pool=()):
+    """A ragged batch: empty and tiny files up to 3 MiB, every content kind, whole-file copies within
+    the batch and of `pool` (files of earlier batches: prior backups' blobs)."""
+    nf = int(rng.integers(1, nf_max))
     lens = np.where(rng.random(nf) < 0.1, 0, rng.integers(0, 3 * MiB, nf) >> rng.integers(0, 12, nf)).astype(np.uint64)
     files = [_content(rng, KINDS[int(rng.integers(len(KINDS)))] if rng.random() < 0.3 else "random", int(m))
              for m in lens]
     for k in range(1, nf):  # whole-file copies: duplicates across the batch
         if rng.random() < 0.15:
             files[k] = files[int(rng.integers(k))].copy()
+    for k in range(nf):
+        if pool and rng.random() < 0.1:
+            files[k] = pool[int(rng.integers(len(pool)))].copy()
     lens = np.array([f.size for f in files], np.uint64)
     offs = np.zeros(nf, np.uint64)
     offs[1:] = np.cumsum((lens[:-1] + 15) // 16 * 16)
     data = np.zeros(int(offs[-1] + lens[-1]) + 16, np.uint8)
     for o, f in zip(offs, files):
         data[int(o):int(o) + f.size] = f
+    return data, offs, lens, files
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_process_files_random_batches(ctx, oracle, case):
+    rng = np.random.default_rng(5000 + case)
+    mn, av, mx = _valid_params(rng, case)
+    thr = int(rng.choice([0, 1, 4096, MiB, 8 * MiB]))  # the small-file threshold (dir_packer.rs:246 = 1 MiB)
+    data, offs, lens, files = _batch(rng)
+    nf = len(files)
     # a seeded index: the digests of a few of the batch's own files (prior backups, BlobIndex::load)
     seed_files = rng.choice(nf, size=min(nf, 5), replace=False)
     seeded = sorted({oracle.blake3(files[int(k)]) for k in seed_files})
@@ -118,3 +134,72 @@ def test_min_above_max_hashes_whole_remainders(ctx, oracle):
     want = oracle.process_files(data, offs, lens, *p, small_threshold=0)
     assert int(want["length"].max()) == 496561 > p[2]
     _blobs_equal(got, want)
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_host_batches_in_flight_random(ctx, oracle, case):
+    """bw_submit_host (row N1): up to three random batches in flight on one context (the ring's
+    depth), pageable, one backup session's index across them -- every blob equal to the oracle's with
+    one Index over the batches in submit order."""
+    rng = np.random.default_rng(7000 + case)
+    mn, av, mx = _valid_params(rng, case)
+    thr = int(rng.choice([0, 4096, MiB]))
+    p = make_params(mn, av, mx, small_file_threshold=thr)
+    ctx.index_reset()
+    ix, pool, pending = oracle.Index(), [], []
+    for _ in range(int(rng.integers(2, 7))):
+        data, offs, lens, files = _batch(rng, 120, pool)
+        pool += files
+        pending.append((ctx.submit_host(data, offs, lens, p), data, offs, lens))
+        if len(pending) == 3 or rng.random() < 0.3:
+            t, d, o, l = pending.pop(0)
+            _blobs_equal(ctx.wait(t), oracle.process_files(d, o, l, mn, av, mx, small_threshold=thr, index=ix, threads=8))
+    for t, d, o, l in pending:
+        _blobs_equal(ctx.wait(t), oracle.process_files(d, o, l, mn, av, mx, small_threshold=thr, index=ix, threads=8))
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_node_session_random_batches(oracle, case):
+    """NodeSession (row e, one process, N ranks on the local transport): random batches, parameters
+    and world sizes, files repeated across batches -- the digest-prefix-partitioned index decides
+    exactly as one oracle.Index over the batches in order."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from backuwup_amd.session import NodeSession
+    rng = np.random.default_rng(9000 + case)
+    world = [2, 4, 8][case % 3]
+    mn, av, mx = _valid_params(rng, case)
+    thr = int(rng.choice([0, 4096, MiB]))
+    ix, pool = oracle.Index(), []
+    with NodeSession([0] * world, transport="local", params=make_params(mn, av, mx, small_file_threshold=thr)) as s:
+        for _ in range(3):
+            data, offs, lens, files = _batch(rng, 200, pool)
+            pool += files
+            got = s.process_files(data, offs, lens)
+            _blobs_equal(got, oracle.process_files(data, offs, lens, mn, av, mx, small_threshold=thr, index=ix,
+                                                   threads=8))
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_dropin_kept_digests_random(ctx, oracle, case):
+    """The drop-in call sites (dir_packer.rs:254-266, :286) at random parameters: FastCDC over the
+    whole source with digests kept, then blake3::hash of every chunk slice answered from them, and of
+    slices that are not chunks (hashed afresh) -- all against the oracle."""
+    rng = np.random.default_rng(11000 + case)
+    mn, av, mx = _valid_params(rng, case)
+    n = int(min(16 * MiB, rng.integers(1, 30) * max(mn, mx) + rng.integers(0, 4096)))
+    buf = _content(rng, KINDS[case % len(KINDS)], n)
+    buf.flags.writeable = False
+    cuts, h = ctx.fastcdc_chunks_hashed(buf, mn, av, mx)
+    try:
+        want = oracle.fastcdc(buf, mn, av, mx)
+        assert cuts == want
+        for _, o, ln in cuts:
+            assert ctx.blake3_at(buf, o, ln, kept=True) == oracle.blake3(buf[o:o + ln]), (o, ln)
+        for _ in range(8):  # not chunks: a shifted start, a shorter length
+            o = int(rng.integers(0, n))
+            ln = int(rng.integers(0, min(n - o, 70000) + 1))
+            assert ctx.blake3_at(buf, o, ln, kept=True) == oracle.blake3(buf[o:o + ln]), (o, ln)
+    finally:
+        ctx.fastcdc_release(h)
