@@ -137,25 +137,34 @@ def test_min_above_max_hashes_whole_remainders(ctx, oracle):
 
 
 @pytest.mark.parametrize("case", range(8))
-def test_host_batches_in_flight_random(ctx, oracle, case):
-    """bw_submit_host (row N1): up to three random batches in flight on one context (the ring's
-    depth), pageable, one backup session's index across them -- every blob equal to the oracle's with
-    one Index over the batches in submit order."""
+def test_host_batches_in_flight_random(oracle, case):
+    """bw_submit_host (row N1): random batches in flight on one context up to its ring depth
+    (BW_OPT_DEPTH 2-4), pageable, one backup session's index across them -- every blob equal to the
+    oracle's with one Index over the batches in submit order."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from backuwup_amd import Context
+    from backuwup_amd._lib import BW_OPT_DEPTH
     rng = np.random.default_rng(7000 + case)
     mn, av, mx = _valid_params(rng, case)
     thr = int(rng.choice([0, 4096, MiB]))
+    depth = int(rng.integers(2, 5))
     p = make_params(mn, av, mx, small_file_threshold=thr)
-    ctx.index_reset()
     ix, pool, pending = oracle.Index(), [], []
-    for _ in range(int(rng.integers(2, 7))):
-        data, offs, lens, files = _batch(rng, 120, pool)
-        pool += files
-        pending.append((ctx.submit_host(data, offs, lens, p), data, offs, lens))
-        if len(pending) == 3 or rng.random() < 0.3:
-            t, d, o, l = pending.pop(0)
-            _blobs_equal(ctx.wait(t), oracle.process_files(d, o, l, mn, av, mx, small_threshold=thr, index=ix, threads=8))
-    for t, d, o, l in pending:
-        _blobs_equal(ctx.wait(t), oracle.process_files(d, o, l, mn, av, mx, small_threshold=thr, index=ix, threads=8))
+    with Context(0) as c:
+        c.set_option(BW_OPT_DEPTH, depth)
+        c.index_reset()
+        for _ in range(int(rng.integers(2, 7))):
+            data, offs, lens, files = _batch(rng, 120, pool)
+            pool += files
+            pending.append((c.submit_host(data, offs, lens, p), data, offs, lens))
+            if len(pending) == depth or rng.random() < 0.3:
+                t, d, o, l = pending.pop(0)
+                _blobs_equal(c.wait(t), oracle.process_files(d, o, l, mn, av, mx, small_threshold=thr, index=ix,
+                                                             threads=8))
+        for t, d, o, l in pending:
+            _blobs_equal(c.wait(t), oracle.process_files(d, o, l, mn, av, mx, small_threshold=thr, index=ix, threads=8))
 
 
 @pytest.mark.parametrize("case", range(6))
