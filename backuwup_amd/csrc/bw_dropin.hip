@@ -525,7 +525,16 @@ int svc_ensure(Service* sv, bool probe = false) {
 // wakes the sleeping callers whose digests landed (tickets t with t % SVC_COMPLETERS == k); sleeps
 // itself while no caller sleeps.  Several of them: at 256 callers one thread making every wake-up
 // system call (~600 k a second) was the limit.
+// A completer that found nothing to wake yields its core (round 6): with more callers than cores
+// (C4 through the drop-in at 256 threads on a 16-core share) four completers polling with only a
+// pause between scans held 4 of the 16 cores whenever any caller slept.  sched_yield returns at once
+// when no other thread wants the core, so an idle machine still polls.  BW_SVC_COMPLETER=spin keeps
+// the old loop (A/B).
 constexpr int SVC_COMPLETERS = 4;
+const bool g_completer_spin = [] {
+    const char* e = getenv("BW_SVC_COMPLETER");
+    return e && strcmp(e, "spin") == 0;
+}();
 void svc_completer(Service* sv, int k) {
     uint64_t lo = 0;  // tickets below lo have returned to their callers
     for (;;) {
@@ -536,15 +545,20 @@ void svc_completer(Service* sv, int k) {
         }
         const uint64_t hi = sv->next.load(std::memory_order_acquire);
         while (lo < hi && sv->free_at[lo % B3_SVC_RING].load(std::memory_order_acquire) > lo) lo++;
+        bool woke = false;
         for (uint64_t t = lo + ((k - lo % SVC_COMPLETERS) + SVC_COMPLETERS) % SVC_COMPLETERS; t < hi; t += SVC_COMPLETERS) {
             const uint32_t i = (uint32_t)(t % B3_SVC_RING);
             uint64_t d[4];
             if (sv->sleep[i].load(std::memory_order_acquire) == 1 && svc_done(sv->resp + i, t, d)) {
                 uint32_t one = 1;
-                if (sv->sleep[i].compare_exchange_strong(one, 2)) futex(&sv->sleep[i], FUTEX_WAKE_PRIVATE, 1);
+                if (sv->sleep[i].compare_exchange_strong(one, 2)) {
+                    futex(&sv->sleep[i], FUTEX_WAKE_PRIVATE, 1);
+                    woke = true;
+                }
             }
         }
-        __builtin_ia32_pause();
+        if (woke || g_completer_spin) __builtin_ia32_pause();
+        else sched_yield();
     }
 }
 
@@ -724,9 +738,13 @@ int service_hash(Service* sv, const uint8_t* data, uint64_t len, uint8_t out[32]
         }
         if (!ok) {  // sleep until the completer wakes this slot; re-check the instance every millisecond
             sv->sleep[i].store(1, std::memory_order_release);
-            sv->sleepers.fetch_add(1, std::memory_order_acq_rel);
-            sv->comp_gen.fetch_add(1, std::memory_order_acq_rel);
-            futex(&sv->comp_gen, FUTEX_WAKE_PRIVATE, SVC_COMPLETERS);
+            // the completers sleep only after seeing no sleeper, so only the first sleeper wakes them
+            // (a completer that saw sleepers == 0 waits on the generation read before; this bump
+            // changes it)
+            if (sv->sleepers.fetch_add(1, std::memory_order_acq_rel) == 0 || g_completer_spin) {
+                sv->comp_gen.fetch_add(1, std::memory_order_acq_rel);
+                futex(&sv->comp_gen, FUTEX_WAKE_PRIVATE, SVC_COMPLETERS);
+            }
             double next_trace = 2000;
             while (!svc_done(sl, t, d)) {
                 const timespec ts1 = {0, 1000000};

@@ -9,7 +9,8 @@
 #   CPU on the same files: bench.py's cpu_baseline (C1; C4 with --cpu-trees).
 # Build first (CPU): see the two tools' headers.  DROPIN_PARTS picks parts (default "c1 c4 cpu"; "c1reg"
 # after "c1": the BW_DROPIN_REGISTER_MIB A/B and the [0,0] device pool; DROPIN_C4_DEVICES=0,0 runs C4
-# through the device pool's policy).
+# through the device pool's policy; "c4ab" after "c4": the hash service's completers yielding vs
+# spinning; "c4cpu": the CPU on C4 alone).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
@@ -64,6 +65,17 @@ print("files", len(o), "unique bytes", u, "file bytes", int(np.sum(l)))
 PY
   run dropin_c4 900 stdbuf -oL ./build_ab/dropin_c4 /tmp/c4_table.bin ${DROPIN_C4_THREADS:-16,64,256} 16 ${DROPIN_C4_REPS:-1} \
     ${DROPIN_C4_DEVICES:+--devices=$DROPIN_C4_DEVICES} || exit 1
+fi
+if [[ " $PARTS " == *" c4ab "* ]]; then  # round 6: the service's completers yielding (default) vs spinning, alternating
+  [ -f /tmp/c4_table.bin ] || { echo "c4ab needs the c4 part first" >> "$OUT/dropin_summary.txt"; exit 1; }
+  for rep in 1 2; do
+    run c4_yield_$rep 600 stdbuf -oL ./build_ab/dropin_c4 /tmp/c4_table.bin 16,64,256 16 1 --devices=0,0 || exit 1
+    run c4_spin_$rep 600 env BW_SVC_COMPLETER=spin stdbuf -oL ./build_ab/dropin_c4 /tmp/c4_table.bin 16,64,256 16 1 \
+      --devices=0,0 || exit 1
+  done
+fi
+if [[ " $PARTS " == *" c4cpu "* ]]; then
+  run bench_c4_cpu 900 python3 bench.py --workload c4 --steps 20 --cpu-trees || exit 1
 fi
 if [[ " $PARTS " == *" cpu "* ]]; then
   run bench_c1_cpu 600 python3 bench.py --workload c1 --steps 300 || exit 1
