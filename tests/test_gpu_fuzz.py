@@ -212,3 +212,45 @@ def test_dropin_kept_digests_random(ctx, oracle, case):
             assert ctx.blake3_at(buf, o, ln, kept=True) == oracle.blake3(buf[o:o + ln]), (o, ln)
     finally:
         ctx.fastcdc_release(h)
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_random_options_random_batches(oracle, case):
+    """The product's free context options drawn at random on a fresh context -- the small-batch tile
+    size threshold, a candidate array forced too small (the walkers' direct path), BLAKE3 leaves per
+    lane, when the scan is enqueued, the pinned staging chunk -- under random batches through
+    process_files, submit_host (pageable) and submit_device, one index across them."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from backuwup_amd import Context
+    from backuwup_amd._lib import BW_OPT_B3_GROUP, BW_OPT_CAND_CAP, BW_OPT_SCAN_FIRST, BW_OPT_SCAN_SMALL_BYTES, \
+        BW_OPT_STAGE_CHUNK
+    rng = np.random.default_rng(13000 + case)
+    mn, av, mx = _valid_params(rng, case)
+    thr = int(rng.choice([0, 4096, MiB]))
+    p = make_params(mn, av, mx, small_file_threshold=thr)
+    opts = {BW_OPT_SCAN_SMALL_BYTES: int(rng.choice([0, 1 << 40, int(rng.integers(1, 64 * MiB))])),
+            BW_OPT_CAND_CAP: int(rng.choice([0, 0, 0, 16, 1000, int(rng.integers(1, 50000))])),
+            BW_OPT_B3_GROUP: int(rng.choice([0, 1, 2, 4])),
+            BW_OPT_SCAN_FIRST: int(rng.integers(0, 3)),
+            BW_OPT_STAGE_CHUNK: int(rng.choice([(1 << 20) + 13, (3 << 20) + 4097, 64 * MiB]))}
+    ix, pool = oracle.Index(), []
+    with Context(0) as c:
+        for k, v in opts.items():
+            c.set_option(k, v)
+        c.index_reset()
+        for _ in range(3):
+            data, offs, lens, files = _batch(rng, 150, pool)
+            pool += files
+            how = int(rng.integers(0, 3))
+            if how == 0:
+                got = c.process_files(data, offs, lens, p)
+            elif how == 1:
+                got = c.wait(c.submit_host(data, offs, lens, p))
+            else:
+                dev = torch.from_numpy(data).cuda()
+                torch.cuda.synchronize()
+                got = c.wait(c.submit_device(dev.data_ptr(), data.size, offs, lens, p))
+            want = oracle.process_files(data, offs, lens, mn, av, mx, small_threshold=thr, index=ix, threads=8)
+            _blobs_equal(got, want)
