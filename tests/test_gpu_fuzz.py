@@ -254,3 +254,19 @@ def test_random_options_random_batches(oracle, case):
                 got = c.wait(c.submit_device(dev.data_ptr(), data.size, offs, lens, p))
             want = oracle.process_files(data, offs, lens, mn, av, mx, small_threshold=thr, index=ix, threads=8)
             _blobs_equal(got, want)
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_zstd_random_blobs(ctx, oracle, case):
+    """Per-blob zstd level 3 (§8f row 2, pack.rs:58-64) on the chunker fuzz's content kinds --
+    periods of 2 to 9,000 bytes, two-symbol bytes, one-byte fills, zeros, zero runs in random data,
+    text -- at log-uniform sizes up to the 3 MiB blob limit, many per call: every frame equal to the
+    oracle's (and to the image's libzstd through it, tests/test_zstd.py)."""
+    rng = np.random.default_rng(15000 + case)
+    blobs = []
+    for _ in range(int(rng.integers(10, 40))):
+        n = min(3 * MiB, int(np.exp(rng.uniform(0, np.log(3 * MiB)))) - 1)
+        blobs.append(_content(rng, KINDS[int(rng.integers(len(KINDS)))], max(n, 0)).tobytes())
+    frames = ctx.zstd_compress(blobs)
+    for i, (b, f) in enumerate(zip(blobs, frames)):
+        assert f == oracle.zstd3_compress(b), (i, len(b))
