@@ -10,6 +10,7 @@
 #   bench    python bench.py $BENCH_ARGS         prof    rocprofv3 --kernel-trace --stats of the bench
 #   pmc      tools/gpu_pmc.sh (FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json)
 #   debug    tools/debug_check.py (BW_DEBUG + BW_DIAG library)
+#   rehearse bench.py --gpus 2 / 4 --transport host on one GPU (the N > 1 path end to end)
 #   zstd     tools/zstd_bench.py on 1 GiB and 8 GiB of text (level-3 frames, oracle-checked sample)
 #   zstream  the same 1 GiB batch with 2, 3 and 4 calls in flight
 #   zspmc    SQ counter passes of the zstd kernels (1 GiB of text)
@@ -57,6 +58,11 @@ for s in $STEPS; do
       step bench_c4 600 python bench.py --workload c4 --steps 60 --no-cpu-baseline &&
       step bench_c5 600 python bench.py --workload c5 --steps 3 --no-cpu-baseline ;;
     debug) step debug_check 600 python tools/debug_check.py ;;
+    rehearse)  # round 6: the driver's N > 1 bench path on one GPU (host transport, ranks share the GPU)
+      step bench_n2_host 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 2 --transport host --steps 20 --warmup 2 --no-holds &&
+      step bench_n4_host 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29534 bench.py --gpus 4 --transport host --steps 10 --warmup 2 --no-holds ;;
     attrib)  # round 5, VERDICT r4 #4: what limits the overlap of the scan and the leaf pass (build first:
              # python backuwup_amd/build.py --clock); then the bench at the driver's 20 steps, the
              # default 320 and 2,000 (18 s), each with its power and clock samples
