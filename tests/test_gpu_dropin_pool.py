@@ -227,3 +227,44 @@ def test_hash_service_posts_at_the_idle_boundary(gpu, oracle):
         with open(os.path.join(out, "idle_boundary_latency.json"), "w") as f:
             json.dump({"calls": len(lat), "instances": b1.value - b0.value, "us_p50_p90_p99_max": q}, f)
     assert worst < 0.1, "a post at the idle boundary waited %.1f ms" % (worst * 1e3)
+
+
+def test_hash_service_thread_churn_oversubscribed(gpu, oracle):
+    """Short-lived callers, as tokio's blocking pool makes them: 12 waves of 48 fresh threads (more
+    callers than the box's cores, so most sleep and the completer threads wake them), each hashing a
+    few random messages of up to 64 KiB and exiting (its message copy goes back to the service's pool
+    for the next wave's threads); pauses between some waves let the instance's idle exit happen.
+    Every digest equals the oracle's, and no ticket is abandoned."""
+    from backuwup_amd import _lib
+    blob = splitmix_bytes(66, 4 << 20)
+    a0, r0, v0 = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    gpu.bw_blake3_service_faults(0, ctypes.byref(a0), ctypes.byref(r0), ctypes.byref(v0))
+    rng = np.random.default_rng(66)
+    errors, calls = [], []
+
+    def worker(seed):
+        g = np.random.default_rng(seed)
+        o = (ctypes.c_uint8 * 32)()
+        for _ in range(int(g.integers(1, 6))):
+            n = int(g.integers(0, (64 << 10) + 1))
+            at = int(g.integers(0, blob.size - n + 1))
+            rc = gpu.bw_blake3_hash_dropin_device(0, ctypes.c_void_p(blob.ctypes.data + at), n, o)
+            calls.append((at, n, rc, bytes(o)))
+
+    for wave in range(12):
+        th = [threading.Thread(target=worker, args=(1000 * wave + t,)) for t in range(48)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+        if wave % 3 == 2:
+            time.sleep(0.008)  # past the 5 ms idle exit: the next wave starts a new instance
+    a1, r1, v1 = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    gpu.bw_blake3_service_faults(0, ctypes.byref(a1), ctypes.byref(r1), ctypes.byref(v1))
+    assert len(calls) > 12 * 48
+    for at, n, rc, d in calls:
+        assert rc == _lib.BW_OK, rc
+        if d != oracle.blake3(blob[at:at + n]):
+            errors.append((at, n))
+    assert not errors, errors[:5]
+    assert a1.value == a0.value and v1.value == v0.value
