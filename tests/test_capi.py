@@ -140,3 +140,27 @@ def test_every_entry_point_survives_null_arguments():
             assert rc[name] == str(_lib.BW_EINVAL), (name, rc[name])
         elif name in benign:
             assert rc[name] == benign[name], (name, rc[name])
+
+
+def test_pool_device_list_from_environment(monkeypatch):
+    """backuwup_amd.pool (the Rust crate's Pool policy): BACKUWUP_GPU_DEVICES lists devices (a device
+    may repeat), the single BACKUWUP_GPU_DEVICE of earlier versions applies only when the list is
+    unset; "all" / empty asks the library for the visible devices (bw_device_count: none here)."""
+    import pytest
+    from backuwup_amd.pool import devices_from_env
+    monkeypatch.setenv("BACKUWUP_GPU_DEVICES", "0,0,3")
+    monkeypatch.setenv("BACKUWUP_GPU_DEVICE", "5")
+    assert devices_from_env() == [0, 0, 3]
+    monkeypatch.delenv("BACKUWUP_GPU_DEVICES")
+    assert devices_from_env() == [5]
+    import ctypes
+    from backuwup_amd import _lib
+    n = ctypes.c_int()
+    assert _lib.load().bw_device_count(ctypes.byref(n)) == 0
+    for v in ("all", ""):
+        monkeypatch.setenv("BACKUWUP_GPU_DEVICES", v)
+        if n.value:
+            assert devices_from_env() == list(range(n.value))
+        else:
+            with pytest.raises(RuntimeError):  # no GPU (the build container)
+                devices_from_env()
