@@ -10,7 +10,7 @@ oracle to finish in well under a second."""
 import numpy as np
 import pytest
 
-from backuwup_amd import make_params
+from backuwup_amd import make_params, make_tree
 from backuwup_amd._lib import BW_EINVAL, BwError
 from backuwup_amd.synth import compressible_corpus, splitmix_bytes
 
@@ -270,3 +270,47 @@ def test_zstd_random_blobs(ctx, oracle, case):
     frames = ctx.zstd_compress(blobs)
     for i, (b, f) in enumerate(zip(blobs, frames)):
         assert f == oracle.zstd3_compress(b), (i, len(b))
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_tree_blobs_random(ctx, oracle, case):
+    """Tree blobs (§8f row 1, dir_packer.rs:314-390) on random trees: names of any bytes up to 3,000
+    long, metadata absent or at the u64 extremes, child counts at and around the 10,000-per-piece
+    split (pieces over 64 KiB hash through the context's launch path), repeated trees, and an index
+    seeded with some pieces of earlier backups -- every piece's bytes, hash and verdict against the
+    oracle's split_serialize_tree and Index."""
+    rng = np.random.default_rng(17000 + case)
+    specs = []
+    for i in range(int(rng.integers(40, 200))):
+        if specs and rng.random() < 0.1:
+            specs.append(specs[int(rng.integers(len(specs)))])
+            continue
+        nl = int(rng.choice([0, 1, int(rng.integers(2, 64)), int(rng.integers(64, 3000))]))
+        name = rng.integers(0, 256, nl, dtype=np.uint8).tobytes()
+        meta = [None if rng.random() < 0.25 else [0, 2**64 - 1, int(rng.integers(0, 2**63))][int(rng.integers(3))]
+                for _ in range(3)]
+        nch = int(rng.choice([0, 1, 2, int(rng.integers(3, 2000)), 9999, 10000, 10001, 20000, 25001]))
+        ch = rng.integers(0, 256, nch * 32, dtype=np.uint8).tobytes()
+        specs.append((int(rng.integers(2)), name, *meta, ch))
+    dedup = bool(case % 3)
+    pieces = [oracle.split_serialize_tree(*s) for s in specs]
+    prior = sorted({h for ps in pieces for _, h in ps if rng.random() < 0.1})
+    ctx.index_reset()
+    if prior:
+        ctx.index_seed(np.frombuffer(b"".join(prior), np.uint8).reshape(-1, 32))
+    hashes, blobs = ctx.tree_blobs([make_tree(*s) for s in specs], dedup=dedup)
+    ix = oracle.Index(b"".join(prior))
+    k = 0
+    for i, ps in enumerate(pieces):
+        assert bytes(hashes[i]) == ps[0][1], i
+        for p, (data, h) in enumerate(ps):
+            b = blobs[k]
+            assert (int(b["tree"]), int(b["piece"]), int(b["length"])) == (i, p, len(data)), (i, p)
+            assert bytes(b["hash"]) == h, (i, p)
+            if dedup:
+                dup = ix.is_blob_duplicate(h)
+                if not dup:
+                    ix.insert(h)
+                assert int(b["is_dup"]) == int(dup), (i, p)
+            k += 1
+    assert k == len(blobs)
