@@ -350,3 +350,50 @@ def test_seal_open_random(ctx, oracle, case):
     assert ok.all()
     for i in range(n):
         assert np.array_equal(plain[int(off[i]):int(off[i] + lens[i])], data[int(off[i]):int(off[i] + lens[i])]), i
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_packfiles_and_index_files_random(ctx, oracle, case):
+    """Packfiles (§8f row 4: write_packfiles + serialize_packfile, pack.rs:115-227) of random blob
+    queues -- many tiny blobs, some up to 3 MiB, ragged source offsets, store frames (flags default)
+    -- equal byte for byte to the format oracle's; then the index files of the same entries
+    (BlobIndex::push/flush, blob_index.rs:151-240) built, loaded back and gating new digests."""
+    from oracle import pack_oracle as po
+    rng = np.random.default_rng(21000 + case)
+    prk = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    n = int(rng.integers(1, 300))
+    sizes = [int(rng.integers(0, 64)) if rng.random() < 0.5 else
+             min(3 * MiB, int(np.exp(rng.uniform(0, np.log(3 * MiB))))) for _ in range(n)]
+    while sum(sizes) > 24 * MiB:
+        sizes[int(np.argmax(sizes))] //= 4
+    datas = [splitmix_bytes(int(rng.integers(1 << 30)), s).tobytes() for s in sizes]
+    align = int(rng.integers(1, 17))
+    offs, cur = [], 0
+    for d in datas:
+        offs.append(cur)
+        cur += len(d) + (-len(d)) % align
+    src = np.zeros(max(cur, 1), np.uint8)
+    for o, d in zip(offs, datas):
+        src[o:o + len(d)] = np.frombuffer(d, np.uint8)
+    offs = np.asarray(offs, np.uint64)
+    lens = np.asarray(sizes, np.uint64)
+    hashes = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    kinds = rng.integers(0, 2, n).astype(np.uint8)
+    nonces = rng.integers(0, 256, (n, 12), dtype=np.uint8)
+    plan, total = ctx.pack_plan(lens)
+    ids = rng.integers(0, 256, (len(plan), 12), dtype=np.uint8)
+    got = ctx.pack_build(prk, src, offs, lens, hashes, kinds, nonces, plan, total, ids)
+    blobs = [(bytes(hashes[i]), int(kinds[i]), bytes(nonces[i]),
+              po.seal_blob_payload(prk, hashes[i], nonces[i], po.zstd_store(d))) for i, d in enumerate(datas)]
+    want = po.write_packfiles(prk, blobs, [bytes(x) for x in ids])
+    assert len(want) == len(plan)
+    for p, (_, buf) in zip(plan, want):
+        assert got[int(p["offset"]):int(p["offset"] + p["size"])].tobytes() == buf
+    ents = np.concatenate([hashes, rng.integers(0, 256, (n, 12), dtype=np.uint8)], axis=1)
+    last = int(rng.integers(0, 1000))
+    files = ctx.index_files_build(prk, ents, last_file_num=last)
+    assert [(f, b) for f, b in files] == po.push_and_flush(prk, last, [(bytes(e[:32]), bytes(e[32:])) for e in ents])
+    ctx.index_reset()
+    assert ctx.index_load_files(prk, files).tobytes() == ents.tobytes()
+    probe = np.concatenate([hashes[::3], rng.integers(0, 256, (7, 32), dtype=np.uint8)])
+    assert ctx.index_check_insert(probe).tolist() == [1] * len(hashes[::3]) + [0] * 7
