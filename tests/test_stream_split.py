@@ -232,3 +232,94 @@ def test_stream_shard_c_abi_rccl_world1(ctx, oracle):
     want = oracle.process_files(data, [0], [data.size], small_threshold=0)
     assert sh["rounds"] == 1 and sh["first_blob"] == 0 and sh["n_blobs"] == len(want) == len(res)
     assert np.array_equal(res["offset"], want["offset"]) and np.array_equal(res["digest"], want["digest"])
+
+
+def rand_file(seed, kind, n):
+    """Content for the random shard cases: random, zeros, a short period, two-symbol bytes."""
+    if kind == "random":
+        return splitmix_bytes(seed, n)
+    if kind == "zeros":
+        return np.zeros(n, dtype=np.uint8)
+    if kind == "period":
+        return np.resize(splitmix_bytes(seed, 1 + seed % 5000), n)
+    return (splitmix_bytes(seed, n) & 1).astype(np.uint8)
+
+
+def random_shard_cases(seed, k):
+    """k random (kind, n, params, seed) cases: min <= max and avg <= max (the shard's domain), files
+    from empty to 24 MiB (most of them several max long), parameters log-uniform in the crate's
+    ranges."""
+    rng = np.random.default_rng(seed)
+    lu = lambda lo, hi: int(np.exp(rng.uniform(np.log(lo), np.log(hi + 1))))  # noqa: E731
+    out = []
+    for i in range(k):
+        mx = min(lu(1024, 4 << 20), 16 << 20)
+        mn = min(lu(64, 1 << 20), mx)
+        av = min(lu(256, 4 << 20), mx)
+        r = rng.random()
+        n = 0 if r < 0.08 else int(rng.integers(mx, 8 * mx + 2)) if r < 0.6 else lu(1, 12 << 20)
+        n = min(n, 24 << 20)
+        out.append((["random", "zeros", "period", "two"][i % 4], n, (mn, av, mx), seed * 100 + i))
+    return out
+
+
+def _rand_shard_worker(rank, world, port, q, cases):
+    import torch
+    from backuwup_amd import Context, make_params
+    from backuwup_amd.comm import Comm, gloo_all_to_all
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = []
+        with Context(0) as c, Comm.host(0, rank, world, gloo_all_to_all()) as comm:
+            c.index_reset(1 << 14)
+            for kind, n, params, seed in cases:
+                data = rand_file(seed, kind, n)
+                lo, hi = ss.window(n, rank, world, params[2])
+                win = torch.from_numpy(data[lo:hi].copy()).cuda() if hi > lo else None
+                torch.cuda.synchronize()
+                sh = c.chunk_stream_shard(comm, win.data_ptr() if win is not None else 0, n, make_params(*params))
+                if sh["ticket"]:
+                    c.exchange_dedup(comm, sh["ticket"])
+                    res = c.wait(sh["ticket"])
+                    mine = res[sh["first_blob"]:sh["first_blob"] + sh["n_blobs"]]
+                    out.append([(int(sh["chain_start"] + b["offset"]), int(b["length"]), int(b["gear_hash"]),
+                                 bytes(b["digest"]), int(b["is_dup"])) for b in mine])
+                else:
+                    out.append([])
+            c.index_check()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_stream_shard_c_abi_random(world, oracle):
+    """bw_chunk_stream_shard at random parameters, sizes and contents (round 6 fuzz), `world`
+    processes sharing the one GPU over the host transport, one backup session across the files:
+    every chunk, Chunk.hash, digest and verdict equal to serial chunking and one oracle.Index."""
+    cases = random_shard_cases(23000 + world, 6)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_rand_shard_worker, args=(r, world, port, q, cases)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ix = oracle.Index()
+    for c, (kind, n, params, seed) in enumerate(cases):
+        chunks = [b for r in range(world) for b in got[r][c]]
+        if n == 0:
+            assert chunks == []
+            continue
+        data = rand_file(seed, kind, n)
+        want = oracle.process_files(data, [0], [n], *params, small_threshold=0, index=ix)
+        assert [(s, l) for s, l, _, _, _ in chunks] == [(int(o), int(l)) for o, l in zip(want["offset"], want["length"])], \
+            (kind, n, params)
+        assert [g for _, _, g, _, _ in chunks] == [int(x) for x in want["gear_hash"]], (kind, n, params)
+        assert [d for _, _, _, d, _ in chunks] == [bytes(x) for x in want["digest"]], (kind, n, params)
+        assert [v for _, _, _, _, v in chunks] == [int(x) for x in want["is_dup"]], (kind, n, params)
