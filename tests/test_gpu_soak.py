@@ -1,8 +1,9 @@
 """Soak run of the seeded fuzz (round 6): the generators of tests/test_gpu_fuzz.py at many more seeds,
 for as long as BW_SOAK_SECONDS says (skipped when it is unset, so the driver's `pytest -m gpu` does
-not run it).  Alternates the chunker case (parameters anywhere in the crate's ranges, every content
-kind) and the batch case (ragged batches, the small-file threshold anywhere, a seeded index); every
-result against the oracle.  Failing seeds are collected and reported together; the counts go to
+not run it).  By default it alternates the chunker case (parameters anywhere in the crate's ranges,
+every content kind) and the batch case (ragged batches, the small-file threshold anywhere, a seeded
+index); BW_SOAK_KINDS=all adds the fuzz's options, in-flight, NodeSession, drop-in, zstd and tree
+generators.  Every result against the oracle.  Failing seeds are collected and reported together; the counts go to
 gpurun_out/soak.json when that directory exists."""
 import json
 import os
@@ -50,20 +51,46 @@ def _batch_case(ctx, oracle, seed):
     return all(np.array_equal(got[f], want[f]) for f in ("file", "offset", "length", "gear_hash", "is_dup", "digest"))
 
 
+def _wrap(fn):
+    def run(ctx, oracle, seed):
+        try:
+            fn(ctx, oracle, seed)
+            return True
+        except AssertionError:
+            return False
+    return run
+
+
+# BW_SOAK_KINDS picks the rotation (default: the chunker and batch cases); "all" adds the fuzz's other
+# generators, each called with the seed as its case number
+KINDS = {
+    "chunker": _chunker_case,
+    "batch": _batch_case,
+    "options": _wrap(lambda c, o, s: F.test_random_options_random_batches(o, s)),
+    "inflight": _wrap(lambda c, o, s: F.test_host_batches_in_flight_random(o, s)),
+    "nodes": _wrap(lambda c, o, s: F.test_node_session_random_batches(o, s)),
+    "dropin": _wrap(lambda c, o, s: F.test_dropin_kept_digests_random(c, o, s)),
+    "zstd": _wrap(lambda c, o, s: F.test_zstd_random_blobs(c, o, s)),
+    "trees": _wrap(lambda c, o, s: F.test_tree_blobs_random(c, o, s)),
+}
+
+
 def test_soak(ctx, oracle):
     seconds = float(os.environ.get("BW_SOAK_SECONDS", "0"))
     if seconds <= 0:
         pytest.skip("set BW_SOAK_SECONDS to run the soak")
     base = int(os.environ.get("BW_SOAK_SEED", "100000"))
     t_end = time.time() + seconds
-    done = {"chunker": 0, "batch": 0}
+    sel = os.environ.get("BW_SOAK_KINDS", "chunker,batch")
+    rot = list(KINDS) if sel == "all" else sel.split(",")
+    done = {k: 0 for k in rot}
     failed = []
     k = 0
     last = time.time()
     while time.time() < t_end:
         seed = base + k
-        kind = "chunker" if k % 2 == 0 else "batch"
-        ok = (_chunker_case if kind == "chunker" else _batch_case)(ctx, oracle, seed)
+        kind = rot[k % len(rot)]
+        ok = KINDS[kind](ctx, oracle, seed)
         done[kind] += 1
         if not ok:
             failed.append((kind, seed))
@@ -74,5 +101,5 @@ def test_soak(ctx, oracle):
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
     if os.path.isdir(out):
         with open(os.path.join(out, "soak.json"), "w") as f:
-            json.dump({"seconds": seconds, "first_seed": base, "cases": done, "failed": failed}, f)
+            json.dump({"seconds": seconds, "first_seed": base, "kinds": rot, "cases": done, "failed": failed}, f)
     assert not failed, failed[:10]
