@@ -3,8 +3,8 @@ for as long as BW_SOAK_SECONDS says (skipped when it is unset, so the driver's `
 not run it).  By default it alternates the chunker case (parameters anywhere in the crate's ranges,
 every content kind) and the batch case (ragged batches, the small-file threshold anywhere, a seeded
 index); BW_SOAK_KINDS=all adds the fuzz's options, in-flight, NodeSession, drop-in, zstd and tree
-generators.  Every result against the oracle.  Failing seeds are collected and reported together; the counts go to
-gpurun_out/soak.json when that directory exists."""
+generators.  Every result against the oracle.  Failing seeds are collected and reported together;
+the counts go to gpurun_out/soak.json when that directory exists."""
 import json
 import os
 import time
