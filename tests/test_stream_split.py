@@ -299,14 +299,16 @@ def test_stream_shard_c_abi_random(world, oracle):
     """bw_chunk_stream_shard at random parameters, sizes and contents (round 6 fuzz), `world`
     processes sharing the one GPU over the host transport, one backup session across the files:
     every chunk, Chunk.hash, digest and verdict equal to serial chunking and one oracle.Index."""
-    cases = random_shard_cases(23000 + world, 6)
+    # (BW_SHARD_RANDOM_CASES / BW_SHARD_RANDOM_SEED widen it into a soak)
+    cases = random_shard_cases(int(os.environ.get("BW_SHARD_RANDOM_SEED", 23000)) + world,
+                               int(os.environ.get("BW_SHARD_RANDOM_CASES", 6)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_rand_shard_worker, args=(r, world, port, q, cases)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=300) for _ in range(world))
+    got = dict(q.get(timeout=max(300, 3 * len(cases))) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
