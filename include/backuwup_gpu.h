@@ -55,7 +55,9 @@ enum {
                            through a context (bw_blake3_hash_many)                                 */
 };
 
-/* fastcdc::v2020 size bounds (asserted by FastCDC::with_level) */
+/* fastcdc::v2020 size bounds (asserted by FastCDC::with_level).  avg > max passes those asserts, but
+ * the crate's cut() then reads past max (a chunk longer than max, or an index panic): the ABI refuses
+ * it with BW_EINVAL too.  min > max is legal: a remainder <= min is one chunk, longer than max. */
 #define BW_MINIMUM_MIN 64u
 #define BW_MINIMUM_MAX 1048576u
 #define BW_AVERAGE_MIN 256u
